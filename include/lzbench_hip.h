@@ -1,0 +1,103 @@
+/*
+ * include/lzbench_hip.h -- C-ABI of liblzbench_hip.so, the MI355X (gfx950) drop-in for the
+ * lzbench chunk-loop hot path (LZ4 block + snappy raw codecs, bit-exact with the reference
+ * lz4 1.9.3 / snappy 1.1.8).  Plain pointers and sizes only.
+ *
+ * Three layers:
+ *
+ *  1. lzbench rows -- the exact compressor_desc_t function-pointer signatures of
+ *     /root/reference/_lzbench/lzbench.h:113-115, so a maintainer adds rows to comp_desc[]
+ *     (lzbench.h:140-219) next to the CUDA rows (lzbench.h:217-218) under BENCH_HAS_HIP:
+ *       compress_func   int64_t (*)(char *in, size_t insize, char *out, size_t outsize,
+ *                                   size_t level, size_t param2, char *workmem)
+ *       init_func       char* (*)(size_t chunk_size, size_t level, size_t ngpus)
+ *       deinit_func     void (*)(char *workmem)
+ *     Replaces: lzbench_lz4_compress / lzbench_lz4fast_compress / lzbench_lz4_decompress
+ *     (compressors.cpp:343-362), lzbench_snappy_compress / _decompress (compressors.cpp:1282-1292),
+ *     lzbench_cuda_{init,deinit,memcpy,return_0} and lzbench_nvcomp_* (compressors.cpp:1813-2014).
+ *     Error conventions are lzbench's (lzbench.cpp:284-288, :321): compress returns the
+ *     compressed length, <= 0 on failure (driver then stores raw); decompress returns the
+ *     decompressed length, <= 0 on error.
+ *
+ *  2. batched rows -- one call per chunk list instead of one per chunk (the per-chunk ABI
+ *     serialises a GPU); replaces the two chunk loops
+ *     lzbench_compress / lzbench_decompress (lzbench.cpp:266-298 / :301-329) including the
+ *     raw-store rule (clen <= 0 || clen == part -> stored raw, compr_size = part) and the
+ *     contiguous packing in chunk order.  Chunks are sharded over the GPUs given to init
+ *     (param2 = ngpus) by contiguous index ranges with one host-side gather.
+ *
+ *  3. device-resident API -- inputs already in HBM, asynchronous on a caller stream
+ *     (the nvcomp batched API analogue, reference nvcomp/lz4.h:239-371).  The input is n
+ *     bytes cut into ceil(n/chunk_size) chunks of chunk_size (last one ragged).
+ *     Readable-size arguments give how many bytes past the start may be read (>= n + 16):
+ *     kernels read whole dwords and rely on that slack.
+ */
+#ifndef LZBENCH_HIP_H
+#define LZBENCH_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { LZH_CODEC_LZ4 = 0, LZH_CODEC_SNAPPY = 1, LZH_CODEC_MEMCPY = 2 };
+enum { LZH_OK = 0, LZH_EARG = -1, LZH_EHIP = -2, LZH_ESPACE = -3, LZH_ECORRUPT = -4 };
+
+/* ---- 1. lzbench rows (per-chunk ABI) ------------------------------------------------ */
+char*   lzbench_hip_lz4_init(size_t chunk_size, size_t level, size_t ngpus);
+char*   lzbench_hip_snappy_init(size_t chunk_size, size_t level, size_t ngpus);
+char*   lzbench_hip_memcpy_init(size_t chunk_size, size_t level, size_t ngpus);
+void    lzbench_hip_deinit(char* workmem);
+/* lz4: LZ4_compress_default semantics; lz4fast: level = acceleration (LZ4_compress_fast) */
+int64_t lzbench_hip_lz4_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+int64_t lzbench_hip_lz4fast_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+int64_t lzbench_hip_lz4_decompress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+int64_t lzbench_hip_snappy_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+int64_t lzbench_hip_snappy_decompress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+/* hipMemcpy plumbing row: host -> HBM -> host round trip of the chunk */
+int64_t lzbench_hip_memcpy(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+
+/* ---- 2. batched rows ----------------------------------------------------------------- */
+/* Compress nchunks consecutive chunks of in (sizes chunk_sizes[]) into out (capacity
+ * outcap), filling compr_sizes[]; applies the raw-store rule. Returns total packed bytes,
+ * <= 0 on failure.  The codec and level come from the init call that made workmem. */
+int64_t lzbench_hip_compress_batch(const char* in, const size_t* chunk_sizes, int nchunks, char* out,
+                                   size_t outcap, size_t* compr_sizes, size_t level, size_t p2, char* workmem);
+/* Inverse: out receives sum(chunk_sizes) bytes. Returns that total, <= 0 on error. */
+int64_t lzbench_hip_decompress_batch(const char* in, const size_t* compr_sizes, const size_t* chunk_sizes,
+                                     int nchunks, char* out, size_t outcap, size_t level, size_t p2, char* workmem);
+
+/* ---- 3. device-resident API ---------------------------------------------------------- */
+/* bytes of the per-chunk staging slot (>= worst-case compressed chunk, 256-aligned) */
+size_t lzh_stage_stride(int codec, size_t chunk_size);
+/* upper bound of the packed output for n bytes */
+size_t lzh_max_packed_bytes(int codec, size_t n, size_t chunk_size);
+size_t lzh_compress_temp_bytes(int codec, size_t n, size_t chunk_size);
+size_t lzh_decompress_temp_bytes(int codec, size_t n, size_t chunk_size);
+size_t lzh_num_chunks(size_t n, size_t chunk_size);
+
+/* d_csizes: nchunks u32 (out); d_offsets: nchunks+1 u64 (out; [nchunks] = packed total).
+ * level: lz4 acceleration (<=1 -> LZ4_compress_default); ignored by snappy. */
+int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t in_readable, size_t chunk_size,
+                       void* d_packed, size_t packed_cap, uint32_t* d_csizes, uint64_t* d_offsets,
+                       void* d_temp, size_t temp_bytes, void* hip_stream);
+/* d_offsets may be NULL (then derived from d_csizes into d_temp).  d_status: nchunks i32,
+ * decoded size per chunk or negative on malformed input. */
+int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable, const uint32_t* d_csizes,
+                         const uint64_t* d_offsets, size_t n, size_t chunk_size, void* d_out, int32_t* d_status,
+                         void* d_temp, size_t temp_bytes, void* hip_stream);
+
+/* Dispatch the stages of lzh_compress_async separately (profiling / roofline): the codec
+ * kernel alone writes the staging slots and per-chunk sizes. */
+int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, size_t in_readable,
+                             size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream);
+
+/* synthetic corpora of SURVEY.md 8(d): 0 random, 1 text, 2 json logs, 3 mixed, 4 binary */
+size_t lzh_datagen(int kind, uint64_t seed, void* buf, size_t n);
+const char* lzh_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,405 @@
+// lzbench_amd/csrc/api.cpp -- the C-ABI of include/lzbench_hip.h.
+//
+// Device-resident layer: stage -> scan -> pack for compression, scan -> decode for
+// decompression, all asynchronous on the caller's stream.
+// Host layer: lzbench rows and batched rows.  A row's workmem is an LzhCtx holding, per GPU,
+// a stream and device buffers sized at init for the chunk size (grown on demand).  A batch
+// is cut into runs of uniform chunking (lzbench's chunk list is uniform per input file,
+// lzbench.cpp:366-373); each run is sharded over the GPUs by contiguous chunk ranges, every
+// GPU compresses its slab, and the host gathers the packed slabs in chunk order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/lzbench_hip.h"
+#include "launch.h"
+
+extern "C" size_t lzb_datagen(int kind, uint64_t seed, uint8_t* buf, size_t n);
+
+#define LZH_CHECK(x)                                                                  \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "lzbench_hip: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return LZH_EHIP;                                                          \
+        }                                                                             \
+    } while (0)
+
+static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+extern "C" {
+
+const char* lzh_version(void) { return "lzbench_hip 0.1 (lz4 1.9.3 / snappy 1.1.8 bit-exact, gfx950)"; }
+
+size_t lzh_datagen(int kind, uint64_t seed, void* buf, size_t n) { return lzb_datagen(kind, seed, (uint8_t*)buf, n); }
+
+size_t lzh_num_chunks(size_t n, size_t chunk_size) {
+    if (chunk_size == 0) return 0;
+    return n == 0 ? 1 : (n + chunk_size - 1) / chunk_size;
+}
+
+static size_t codec_bound(int codec, size_t part) {
+    if (codec == LZH_CODEC_LZ4) return part + part / 255 + 16;     // LZ4_compressBound, lz4.h:171
+    if (codec == LZH_CODEC_SNAPPY) return 32 + part + part / 6;    // MaxCompressedLength, snappy.cc:99-121
+    return part;
+}
+
+size_t lzh_stage_stride(int codec, size_t chunk_size) { return align_up(codec_bound(codec, chunk_size) + 16, 256); }
+
+size_t lzh_max_packed_bytes(int codec, size_t n, size_t chunk_size) {
+    size_t k = lzh_num_chunks(n, chunk_size);
+    return n + k * (codec_bound(codec, chunk_size) - chunk_size + 8) + 64;
+}
+
+size_t lzh_compress_temp_bytes(int codec, size_t n, size_t chunk_size) {
+    size_t k = lzh_num_chunks(n, chunk_size);
+    if (codec == LZH_CODEC_MEMCPY) return 256;
+    return align_up(k * lzh_stage_stride(codec, chunk_size), 256) + 256;
+}
+
+size_t lzh_decompress_temp_bytes(int codec, size_t n, size_t chunk_size) {
+    (void)codec;
+    return align_up((lzh_num_chunks(n, chunk_size) + 1) * sizeof(uint64_t), 256) + 256;
+}
+
+int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, size_t in_readable,
+                             size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream) {
+    hipStream_t s = (hipStream_t)hip_stream;
+    if (!chunk_size || !d_stage || !d_csizes || (n && !d_in)) return LZH_EARG;
+    const size_t k = lzh_num_chunks(n, chunk_size);
+    if (k > 0xffffffffu || chunk_size > 0x7fff0000u) return LZH_EARG;
+    const size_t stride = lzh_stage_stride(codec, chunk_size);
+    if (codec == LZH_CODEC_LZ4) {
+        LZH_CHECK(lzh_launch_lz4_compress((const uint8_t*)d_in, n, in_readable, chunk_size, level < 1 ? 1 : level,
+                                          (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
+    } else if (codec == LZH_CODEC_SNAPPY) {
+        LZH_CHECK(lzh_launch_snappy_compress((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
+                                             stride, d_csizes, (uint32_t)k, s));
+    } else {
+        return LZH_EARG;
+    }
+    return LZH_OK;
+}
+
+__global__ void lzh_fill_raw_sizes(uint32_t* cs, uint64_t k, uint64_t n, uint64_t chunk) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) cs[i] = (uint32_t)std::min<uint64_t>(chunk, n - i * chunk);
+}
+
+int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t in_readable, size_t chunk_size,
+                       void* d_packed, size_t packed_cap, uint32_t* d_csizes, uint64_t* d_offsets, void* d_temp,
+                       size_t temp_bytes, void* hip_stream) {
+    hipStream_t s = (hipStream_t)hip_stream;
+    if (!chunk_size || !d_packed || !d_csizes || !d_offsets || (n && !d_in)) return LZH_EARG;
+    if (in_readable < n) return LZH_EARG;
+    const size_t k = lzh_num_chunks(n, chunk_size);
+    if (codec == LZH_CODEC_MEMCPY) {
+        if (packed_cap < n) return LZH_ESPACE;
+        if (n == 0) return LZH_OK;
+        hipLaunchKernelGGL(lzh_fill_raw_sizes, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, s, d_csizes,
+                           (uint64_t)k, (uint64_t)n, (uint64_t)chunk_size);
+        LZH_CHECK(hipGetLastError());
+        LZH_CHECK(lzh_launch_scan(d_csizes, k, d_offsets, nullptr, s));
+        LZH_CHECK(lzh_launch_memcpy(d_in, d_packed, n, s));
+        return LZH_OK;
+    }
+    if (temp_bytes < lzh_compress_temp_bytes(codec, n, chunk_size) || !d_temp) return LZH_ESPACE;
+    const size_t stride = lzh_stage_stride(codec, chunk_size);
+    int rc = lzh_compress_kernel_only(codec, level, d_in, n, in_readable, chunk_size, d_temp, d_csizes, hip_stream);
+    if (rc) return rc;
+    LZH_CHECK(lzh_launch_scan(d_csizes, k, d_offsets, nullptr, s));
+    LZH_CHECK(lzh_launch_pack((const uint8_t*)d_in, n, in_readable, chunk_size, (const uint8_t*)d_temp, stride,
+                              d_csizes, d_offsets, (uint8_t*)d_packed, packed_cap, (uint32_t)k, s));
+    return LZH_OK;
+}
+
+int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable, const uint32_t* d_csizes,
+                         const uint64_t* d_offsets, size_t n, size_t chunk_size, void* d_out, int32_t* d_status,
+                         void* d_temp, size_t temp_bytes, void* hip_stream) {
+    hipStream_t s = (hipStream_t)hip_stream;
+    if (!chunk_size || !d_csizes || !d_status || (n && (!d_out || !d_packed))) return LZH_EARG;
+    if (codec < 0 || codec > 2) return LZH_EARG;
+    const size_t k = lzh_num_chunks(n, chunk_size);
+    if (n == 0) return LZH_OK;
+    const uint64_t* offs = d_offsets;
+    if (!offs) {
+        if (!d_temp || temp_bytes < lzh_decompress_temp_bytes(codec, n, chunk_size)) return LZH_ESPACE;
+        LZH_CHECK(lzh_launch_scan(d_csizes, k, (uint64_t*)d_temp, nullptr, s));
+        offs = (const uint64_t*)d_temp;
+    }
+    LZH_CHECK(lzh_launch_decompress(codec, (const uint8_t*)d_packed, packed_readable, offs, d_csizes, n, chunk_size,
+                                    (uint8_t*)d_out, d_status, (uint32_t)k, s));
+    return LZH_OK;
+}
+
+}  // extern "C"
+
+// ======================================================================= host layer
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = align_up(bytes + 4096, 1 << 20);
+        if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return -1; }
+        cap = want;
+        return 0;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct Dev {
+    int id = 0;
+    hipStream_t s = nullptr;
+    DevBuf in, packed, temp, csizes, offsets, status;
+    std::vector<uint32_t> h_cs;
+    std::vector<int32_t> h_status;
+};
+
+struct LzhCtx {
+    uint32_t magic = 0x4c5a4858;  // "LZHX"
+    int codec = 0;
+    size_t chunk_size = 0;
+    std::vector<Dev> devs;
+};
+
+LzhCtx* ctx_of(char* wm) {
+    LzhCtx* c = (LzhCtx*)wm;
+    return (c && c->magic == 0x4c5a4858) ? c : nullptr;
+}
+
+char* ctx_new(int codec, size_t chunk_size, size_t ngpus) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        fprintf(stderr, "lzbench_hip: no HIP device available\n");
+        return nullptr;
+    }
+    if (ngpus == 0) ngpus = 1;
+    if ((int)ngpus > count) ngpus = (size_t)count;
+    LzhCtx* c = new LzhCtx();
+    c->codec = codec;
+    c->chunk_size = chunk_size;
+    c->devs.resize(ngpus);
+    for (size_t g = 0; g < ngpus; g++) {
+        c->devs[g].id = (int)g;
+        if (hipSetDevice((int)g) != hipSuccess || hipStreamCreateWithFlags(&c->devs[g].s, hipStreamNonBlocking) != hipSuccess) {
+            fprintf(stderr, "lzbench_hip: cannot open device %zu\n", g);
+            delete c;
+            return nullptr;
+        }
+    }
+    return (char*)c;
+}
+
+// process one run: chunks [0, k) of uniform size `chunk` (last ragged) covering n bytes of
+// host input; results appended at out (capacity outcap). Returns packed bytes or < 0.
+int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t chunk, uint8_t* out, size_t outcap,
+                     size_t* compr_sizes) {
+    const size_t k = lzh_num_chunks(n, chunk);
+    const size_t G = std::min(c->devs.size(), k);
+    std::vector<size_t> c0(G + 1), totals(G, 0);
+    for (size_t g = 0; g <= G; g++) c0[g] = k * g / G;
+    for (size_t g = 0; g < G; g++) {
+        Dev& d = c->devs[g];
+        if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
+        const size_t off = c0[g] * chunk, nn = std::min(n, c0[g + 1] * chunk) - off, kk = c0[g + 1] - c0[g];
+        if (d.in.ensure(nn + 64) || d.packed.ensure(lzh_max_packed_bytes(c->codec, nn, chunk) + 64) ||
+            d.temp.ensure(lzh_compress_temp_bytes(c->codec, nn, chunk)) || d.csizes.ensure(kk * 4 + 64) ||
+            d.offsets.ensure((kk + 1) * 8 + 64))
+            return LZH_ESPACE;
+        if (hipMemcpyAsync(d.in.p, in + off, nn, hipMemcpyHostToDevice, d.s) != hipSuccess) return LZH_EHIP;
+        int rc = lzh_compress_async(c->codec, level, d.in.p, nn, d.in.cap, chunk, d.packed.p, d.packed.cap,
+                                    (uint32_t*)d.csizes.p, (uint64_t*)d.offsets.p, d.temp.p, d.temp.cap, d.s);
+        if (rc) return rc;
+        d.h_cs.resize(kk);
+        if (hipMemcpyAsync(d.h_cs.data(), d.csizes.p, kk * 4, hipMemcpyDeviceToHost, d.s) != hipSuccess) return LZH_EHIP;
+    }
+    size_t base = 0;
+    for (size_t g = 0; g < G; g++) {   // host-side gather in chunk order
+        Dev& d = c->devs[g];
+        if (hipSetDevice(d.id) != hipSuccess || hipStreamSynchronize(d.s) != hipSuccess) return LZH_EHIP;
+        size_t tot = 0;
+        for (size_t i = 0; i < d.h_cs.size(); i++) { compr_sizes[c0[g] + i] = d.h_cs[i]; tot += d.h_cs[i]; }
+        if (base + tot > outcap) return 0;   // lzbench: cannot store
+        if (hipMemcpyAsync(out + base, d.packed.p, tot, hipMemcpyDeviceToHost, d.s) != hipSuccess) return LZH_EHIP;
+        totals[g] = tot;
+        base += tot;
+    }
+    for (size_t g = 0; g < G; g++) {
+        if (hipSetDevice(c->devs[g].id) != hipSuccess || hipStreamSynchronize(c->devs[g].s) != hipSuccess) return LZH_EHIP;
+    }
+    return (int64_t)base;
+}
+
+int64_t run_decompress(LzhCtx* c, const uint8_t* in, const size_t* compr_sizes, size_t n, size_t chunk, uint8_t* out) {
+    const size_t k = lzh_num_chunks(n, chunk);
+    const size_t G = std::min(c->devs.size(), k);
+    std::vector<size_t> c0(G + 1);
+    for (size_t g = 0; g <= G; g++) c0[g] = k * g / G;
+    std::vector<size_t> coff(k + 1, 0);
+    for (size_t i = 0; i < k; i++) coff[i + 1] = coff[i] + compr_sizes[i];
+    for (size_t g = 0; g < G; g++) {
+        Dev& d = c->devs[g];
+        if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
+        const size_t kk = c0[g + 1] - c0[g];
+        const size_t off = c0[g] * chunk, nn = std::min(n, c0[g + 1] * chunk) - off;
+        const size_t pin = coff[c0[g + 1]] - coff[c0[g]];
+        if (d.in.ensure(pin + 64) || d.packed.ensure(nn + 64) || d.csizes.ensure(kk * 4 + 64) ||
+            d.status.ensure(kk * 4 + 64) || d.temp.ensure(lzh_decompress_temp_bytes(c->codec, nn, chunk)))
+            return LZH_ESPACE;
+        d.h_cs.resize(kk);
+        for (size_t i = 0; i < kk; i++) d.h_cs[i] = (uint32_t)compr_sizes[c0[g] + i];
+        if (hipMemcpyAsync(d.in.p, in + coff[c0[g]], pin, hipMemcpyHostToDevice, d.s) != hipSuccess ||
+            hipMemcpyAsync(d.csizes.p, d.h_cs.data(), kk * 4, hipMemcpyHostToDevice, d.s) != hipSuccess)
+            return LZH_EHIP;
+        int rc = lzh_decompress_async(c->codec, d.in.p, d.in.cap, (const uint32_t*)d.csizes.p, nullptr, nn, chunk,
+                                      d.packed.p, (int32_t*)d.status.p, d.temp.p, d.temp.cap, d.s);
+        if (rc) return rc;
+        d.h_status.resize(kk);
+        if (hipMemcpyAsync(d.h_status.data(), d.status.p, kk * 4, hipMemcpyDeviceToHost, d.s) != hipSuccess ||
+            hipMemcpyAsync(out + off, d.packed.p, nn, hipMemcpyDeviceToHost, d.s) != hipSuccess)
+            return LZH_EHIP;
+    }
+    int64_t sum = 0;
+    bool bad = false;
+    for (size_t g = 0; g < G; g++) {
+        Dev& d = c->devs[g];
+        if (hipSetDevice(d.id) != hipSuccess || hipStreamSynchronize(d.s) != hipSuccess) return LZH_EHIP;
+        for (size_t i = 0; i < d.h_status.size(); i++) {
+            if (d.h_status[i] < 0) bad = true;
+            sum += d.h_status[i];
+        }
+    }
+    return bad ? LZH_ECORRUPT : sum;
+}
+
+int64_t one_chunk_compress(int codec_expect, char* in, size_t insize, char* out, size_t outsize, size_t level, char* wm) {
+    LzhCtx* c = ctx_of(wm);
+    if (!c || c->codec != codec_expect) return 0;
+    size_t cs = 0;
+    const size_t chunk = std::max<size_t>(insize, 1);
+    int64_t r = run_compress(c, (int)level, (const uint8_t*)in, insize, chunk, (uint8_t*)out, outsize, &cs);
+    return r <= 0 ? 0 : (int64_t)cs;
+}
+
+int64_t one_chunk_decompress(int codec_expect, char* in, size_t insize, char* out, size_t outsize, char* wm) {
+    LzhCtx* c = ctx_of(wm);
+    if (!c || c->codec != codec_expect) return 0;
+    size_t cs = insize;
+    const size_t chunk = std::max<size_t>(outsize, 1);
+    int64_t r = run_decompress(c, (const uint8_t*)in, &cs, outsize, chunk, (uint8_t*)out);
+    return r < 0 ? r : (int64_t)outsize;
+}
+
+}  // namespace
+
+extern "C" {
+
+char* lzbench_hip_lz4_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_LZ4, chunk_size, ngpus); }
+char* lzbench_hip_snappy_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_SNAPPY, chunk_size, ngpus); }
+char* lzbench_hip_memcpy_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_MEMCPY, chunk_size, ngpus); }
+
+void lzbench_hip_deinit(char* wm) {
+    LzhCtx* c = ctx_of(wm);
+    if (!c) return;
+    for (Dev& d : c->devs) {
+        (void)hipSetDevice(d.id);
+        d.in.release(); d.packed.release(); d.temp.release(); d.csizes.release(); d.offsets.release(); d.status.release();
+        if (d.s) (void)hipStreamDestroy(d.s);
+    }
+    c->magic = 0;
+    delete c;
+}
+
+int64_t lzbench_hip_lz4_compress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
+    return one_chunk_compress(LZH_CODEC_LZ4, in, insize, out, outsize, 1, wm);
+}
+int64_t lzbench_hip_lz4fast_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t, char* wm) {
+    return one_chunk_compress(LZH_CODEC_LZ4, in, insize, out, outsize, level, wm);
+}
+int64_t lzbench_hip_lz4_decompress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
+    return one_chunk_decompress(LZH_CODEC_LZ4, in, insize, out, outsize, wm);
+}
+int64_t lzbench_hip_snappy_compress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
+    return one_chunk_compress(LZH_CODEC_SNAPPY, in, insize, out, outsize, 0, wm);
+}
+int64_t lzbench_hip_snappy_decompress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
+    return one_chunk_decompress(LZH_CODEC_SNAPPY, in, insize, out, outsize, wm);
+}
+int64_t lzbench_hip_memcpy(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
+    LzhCtx* c = ctx_of(wm);
+    if (!c || outsize < insize) return 0;
+    Dev& d = c->devs[0];
+    if (hipSetDevice(d.id) != hipSuccess || d.in.ensure(insize + 64)) return 0;
+    if (hipMemcpyAsync(d.in.p, in, insize, hipMemcpyHostToDevice, d.s) != hipSuccess ||
+        hipMemcpyAsync(out, d.in.p, insize, hipMemcpyDeviceToHost, d.s) != hipSuccess ||
+        hipStreamSynchronize(d.s) != hipSuccess)
+        return 0;
+    return (int64_t)insize;
+}
+
+int64_t lzbench_hip_compress_batch(const char* in, const size_t* chunk_sizes, int nchunks, char* out, size_t outcap,
+                                   size_t* compr_sizes, size_t level, size_t, char* wm) {
+    LzhCtx* c = ctx_of(wm);
+    if (!c || nchunks < 0) return 0;
+    // runs of uniform chunking: a run ends after a chunk shorter than the first of the run
+    int64_t total = 0;
+    size_t ipos = 0;
+    int i = 0;
+    while (i < nchunks) {
+        const size_t chunk = chunk_sizes[i];
+        int j = i;
+        size_t n = 0;
+        while (j < nchunks && chunk_sizes[j] <= chunk) {
+            n += chunk_sizes[j];
+            if (chunk_sizes[j++] < chunk) break;
+        }
+        int64_t r = run_compress(c, (int)level, (const uint8_t*)in + ipos, n, std::max<size_t>(chunk, 1),
+                                 (uint8_t*)out + total, outcap - (size_t)total, compr_sizes + i);
+        if (r <= 0 && n > 0) return r;
+        total += r;
+        ipos += n;
+        i = j;
+    }
+    return total;
+}
+
+int64_t lzbench_hip_decompress_batch(const char* in, const size_t* compr_sizes, const size_t* chunk_sizes, int nchunks,
+                                     char* out, size_t outcap, size_t, size_t, char* wm) {
+    LzhCtx* c = ctx_of(wm);
+    if (!c || nchunks < 0) return 0;
+    int64_t total = 0;
+    size_t ipos = 0;
+    int i = 0;
+    while (i < nchunks) {
+        const size_t chunk = chunk_sizes[i];
+        int j = i;
+        size_t n = 0, cn = 0;
+        while (j < nchunks && chunk_sizes[j] <= chunk) {
+            n += chunk_sizes[j];
+            cn += compr_sizes[j];
+            if (chunk_sizes[j++] < chunk) break;
+        }
+        if ((size_t)total + n > outcap) return 0;
+        int64_t r = run_decompress(c, (const uint8_t*)in + ipos, compr_sizes + i, n, std::max<size_t>(chunk, 1),
+                                   (uint8_t*)out + total);
+        if (r < 0) return r;
+        total += (int64_t)n;
+        ipos += cn;
+        i = j;
+    }
+    return total;
+}
+
+}  // extern "C"

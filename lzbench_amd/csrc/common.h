@@ -1,0 +1,98 @@
+// lzbench_amd/csrc/common.h -- gfx950 device helpers shared by the codec kernels.
+//
+// Every global access of the codecs goes through raw buffer descriptors
+// (__builtin_amdgcn_make_buffer_rsrc): loads past num_records return 0 and stores past it
+// are dropped, so a malformed stream or an indexing bug cannot fault the GPU.  The
+// descriptor inputs are made provably wave-uniform with readfirstlane (guide T20) so no
+// waterfall loops are generated.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LZH_WAVE 64
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int unii(int v) { return (int)__builtin_amdgcn_readfirstlane((uint32_t)v); }
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+    uint64_t a = (uint64_t)p;
+    uint32_t lo = uni((uint32_t)a), hi = uni((uint32_t)(a >> 32));
+    const void* pu = (const void*)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)pu, (short)0, (int)uni(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ uint32_t ld_b32(rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0); }
+__device__ __forceinline__ uint32_t ld_u8(rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0); }
+__device__ __forceinline__ void st_u8(rsrc_t r, int off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0); }
+__device__ __forceinline__ void st_b32(rsrc_t r, int off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0); }
+
+// unaligned little-endian 32-bit read at byte position pos (>= 0) from two aligned dwords
+__device__ __forceinline__ uint32_t ld_u32(rsrc_t r, int pos) {
+    int a = pos & ~3;
+    uint32_t lo = ld_b32(r, a), hi = ld_b32(r, a + 4);
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)pos & 3u);
+}
+// 40-bit read (bytes pos..pos+4) for LZ4's hash5
+__device__ __forceinline__ uint64_t ld_u40(rsrc_t r, int pos) {
+    int a = pos & ~3;
+    uint32_t s = (uint32_t)pos & 3u;
+    uint32_t lo = ld_b32(r, a), hi = ld_b32(r, a + 4);
+    uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, s);
+    uint32_t b4 = (hi >> (8u * s)) & 0xffu;
+    return (uint64_t)v | ((uint64_t)b4 << 32);
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int ffs64(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int rdlanei(int v, int l) { return (int)__builtin_amdgcn_readlane((uint32_t)v, l); }
+// cross-lane gather: value of v held by lane `src` (any lane, 0..63)
+__device__ __forceinline__ uint32_t lane_gather(uint32_t v, int src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+
+// compiler-level ordering for LDS traffic between lanes of the one wave of a workgroup
+// (DS instructions of a wave execute in order in hardware)
+__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Byte-addressed view of a global span through a 4-aligned buffer descriptor: position p
+// lives at descriptor offset p + sh (sh = base address mod 4), so chunk bases of any
+// alignment are handled with aligned dword accesses only.
+struct Bytes {
+    rsrc_t r;
+    int sh;
+    __device__ __forceinline__ void init(const void* p, uint64_t bytes) {
+        const uint64_t a = (uint64_t)p;
+        sh = (int)uni((uint32_t)a & 3u);
+        r = make_rsrc((const void*)(a - (uint64_t)sh), (uint32_t)(bytes + (uint64_t)sh));
+    }
+    __device__ __forceinline__ uint32_t b(int pos) const { return ld_u8(r, pos + sh); }
+    __device__ __forceinline__ uint32_t w32(int pos) const { return ld_u32(r, pos + sh); }
+    __device__ __forceinline__ uint64_t w40(int pos) const { return ld_u40(r, pos + sh); }
+    __device__ __forceinline__ uint32_t b_sc1(int pos) const {   // L1-bypassing byte read
+        return __builtin_amdgcn_raw_buffer_load_b8(r, pos + sh, 0, 16);
+    }
+    __device__ __forceinline__ void st8(int pos, uint32_t v) const { st_u8(r, pos + sh, v); }
+    __device__ __forceinline__ void st32_aligned(int pos, uint32_t v) const { st_b32(r, pos + sh, v); }
+    __device__ __forceinline__ uint32_t aligned_word(int pos) const { return ld_b32(r, pos + sh); }
+};
+
+// dst[d0, d0+len) = src[s0, s0+len) by threads t = 0..nt-1 of the caller's group:
+// destination-aligned dword stores for the body (source words assembled with v_alignbyte),
+// bytewise head and tail (those may share a dword with a neighbour's bytes).
+__device__ __forceinline__ void copy_span(const Bytes& src, int s0, const Bytes& dst, int d0, int len, int t, int nt) {
+    if (len <= 0) return;
+    const int head = min(len, (4 - ((d0 + dst.sh) & 3)) & 3);
+    if (t < head) dst.st8(d0 + t, src.b(s0 + t));
+    const int nd = (len - head) >> 2;
+    for (int d = t; d < nd; d += nt) {
+        const int o = head + 4 * d;
+        dst.st32_aligned(d0 + o, src.w32(s0 + o));
+    }
+    const int tail0 = head + 4 * nd;
+    if (t < len - tail0) dst.st8(d0 + tail0 + t, src.b(s0 + tail0 + t));
+}

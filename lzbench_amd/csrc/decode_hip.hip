@@ -1,0 +1,227 @@
+// lzbench_amd/csrc/decode_hip.hip -- LZ4 and snappy block decoders for gfx950.
+//
+// One 64-lane wavefront per chunk.  The sequence/tag parse is wave-uniform: the compressed
+// stream is held in a 512-byte register window (two VGPRs across the wave) and read with
+// v_readlane, so token, length and offset bytes cost no memory round trip.  Literal and
+// match bytes are moved 64 lanes at a time.  Match sources are read back from the output
+// with L1-bypassing (sc1) loads after the wave's own earlier stores have drained, only
+// when the source overlaps bytes written since the last drain.
+//
+// Acceptance rules follow the reference decoders so malformed input is rejected:
+//   LZ4_decompress_safe   /root/reference/lz4/lz4.c:1707-1729, :1929-2151, :2170-2176
+//   snappy RawUncompress  /root/reference/snappy/snappy.cc:819-1036, :1319-1407
+// (lzbench itself calls LZ4_decompress_fast, compressors.cpp:358-362, which trusts its
+// input; on valid streams both produce identical bytes.)
+#include "common.h"
+
+namespace {
+
+
+struct Win {
+    rsrc_t r;
+    int sh;       // descriptor offset of stream byte 0
+    int wb;       // descriptor offset (4-aligned) of the window start
+    uint32_t w0, w1;
+    __device__ __forceinline__ void bind(const Bytes& b) { r = b.r; sh = b.sh; }
+    __device__ __forceinline__ void load(int pos, int lane) {
+        wb = (pos + sh) & ~3;
+        w0 = ld_b32(r, wb + 4 * lane);
+        w1 = ld_b32(r, wb + 256 + 4 * lane);
+    }
+    // make stream bytes [pos, pos+16) addressable
+    __device__ __forceinline__ void ensure(int pos, int lane) {
+        const int x = pos + sh;
+        if (x >= wb && x + 16 <= wb + 512) return;
+        if (x >= wb + 256 && x + 16 <= wb + 768) {
+            w0 = w1;
+            wb += 256;
+            w1 = ld_b32(r, wb + 256 + 4 * lane);
+            return;
+        }
+        load(pos, lane);
+    }
+    __device__ __forceinline__ uint32_t byte(int pos) const {
+        const int x = pos + sh;
+        const int d = (x - wb) >> 2;
+        const uint32_t v = d < 64 ? rdlane(w0, d) : rdlane(w1, d - 64);
+        return (v >> (8 * (x & 3))) & 0xffu;
+    }
+};
+
+__device__ __forceinline__ void copy_in_out(const Bytes& in, int src, const Bytes& out, int dst, int len, int lane) {
+    copy_span(in, src, out, dst, len, lane, LZH_WAVE);
+}
+
+// out[op + t] = out[op - off + (t mod off)] for t < len; all sources precede op
+__device__ __forceinline__ void copy_match(const Bytes& out, int op, int off, int len, int& flushed, int lane) {
+    const int src0 = op - off;
+    if (src0 + min(off, len) > flushed) { wait_vm(); flushed = op; }
+    for (int base = 0; base < len; base += LZH_WAVE) {
+        const int t = base + lane;
+        if (t < len) {
+            const int s = src0 + (off >= len ? t : (int)((uint32_t)t % (uint32_t)off));
+            const uint32_t v = out.b_sc1(s);
+            out.st8(op + t, v);
+        }
+    }
+}
+
+__device__ __forceinline__ void copy_raw(const Bytes& in, const Bytes& out, int len, int lane) {
+    copy_span(in, 0, out, 0, len, lane, LZH_WAVE);
+}
+
+// returns decoded size or a negative error
+__device__ int lz4_decode(const Bytes& in, int cs, const Bytes& out, int cap, int lane) {
+    if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
+    if (cs <= 0) return -1;
+    Win w;
+    w.bind(in);
+    w.load(0, lane);
+    int ip = 0, op = 0, flushed = 0;
+    for (int guard = 0; guard <= cs; guard++) {
+        if (ip >= cs) return -ip - 1;
+        w.ensure(ip, lane);
+        const uint32_t tok = w.byte(ip++);
+        int lit = (int)(tok >> 4);
+        if (lit == 15) {
+            if (ip >= cs - 15) return -ip - 1;
+            for (int it = 0; it <= cs; it++) {
+                w.ensure(ip, lane);
+                const uint32_t s = w.byte(ip++);
+                lit += (int)s;
+                if (ip >= cs - 15 || s != 255) break;
+            }
+        }
+        if (op + lit > cap - 12 || ip + lit > cs - 8) {
+            if (ip + lit != cs || op + lit > cap) return -ip - 1;
+            copy_in_out(in, ip, out, op, lit, lane);
+            op += lit;
+            break;
+        }
+        copy_in_out(in, ip, out, op, lit, lane);
+        ip += lit;
+        op += lit;
+        w.ensure(ip, lane);
+        const int off = (int)(w.byte(ip) | (w.byte(ip + 1) << 8));
+        ip += 2;
+        int ml = (int)(tok & 15u);
+        if (ml == 15) {
+            for (int it = 0; it <= cs; it++) {
+                w.ensure(ip, lane);
+                const uint32_t s = w.byte(ip++);
+                ml += (int)s;
+                if (ip >= cs - 4) return -ip - 1;
+                if (s != 255) break;
+            }
+        }
+        ml += 4;
+        if (off > op) return -ip - 1;
+        if (op + ml > cap - 5) return -ip - 1;
+        if (off == 0) {   // reference leaves zeros here; never produced by a compressor
+            for (int base = 0; base < ml; base += LZH_WAVE) if (base + lane < ml) out.st8(op + base + lane, 0);
+        } else {
+            copy_match(out, op, off, ml, flushed, lane);
+        }
+        op += ml;
+    }
+    return op;
+}
+
+__device__ int snappy_decode(const Bytes& in, int cs, const Bytes& out, int cap, int lane) {
+    Win w;
+    w.bind(in);
+    w.load(0, lane);
+    int ip = 0;
+    uint32_t ulen = 0;
+    for (int shift = 0;; shift += 7) {
+        if (ip >= cs || shift >= 32) return -1;
+        const uint32_t c = w.byte(ip++);
+        const uint32_t val = c & 0x7fu;
+        if (shift == 28 && val > 15) return -1;
+        ulen |= val << shift;
+        if (c < 128) break;
+    }
+    if (ulen > (uint32_t)cap) return -1;
+    const int ul = (int)ulen;
+    int op = 0, flushed = 0;
+    for (int guard = 0; guard <= cs && ip < cs; guard++) {
+        w.ensure(ip, lane);
+        const uint32_t c = w.byte(ip++);
+        const uint32_t kind = c & 3u;
+        if (kind == 0) {
+            int len = (int)(c >> 2) + 1;
+            if (len > 60) {
+                const int nb = len - 60;
+                if (ip + nb > cs) return -1;
+                uint32_t v = 0;
+                for (int i = 0; i < nb; i++) v |= w.byte(ip + i) << (8 * i);
+                len = (int)v + 1;
+                if (v >= 0x7fffffffu) return -1;
+                ip += nb;
+            }
+            if ((int64_t)ip + len > cs || (int64_t)op + len > ul) return -1;
+            copy_in_out(in, ip, out, op, len, lane);
+            ip += len;
+            op += len;
+        } else {
+            const int extra = kind == 1 ? 1 : (kind == 2 ? 2 : 4);
+            if (ip + extra > cs) return -1;
+            int len;
+            uint32_t off;
+            if (kind == 1) {
+                len = (int)((c >> 2) & 7u) + 4;
+                off = ((c >> 5) << 8) | w.byte(ip);
+            } else {
+                len = (int)(c >> 2) + 1;
+                off = 0;
+                for (int i = 0; i < extra; i++) off |= w.byte(ip + i) << (8 * i);
+            }
+            ip += extra;
+            if (off == 0 || off > (uint32_t)op || op + len > ul) return -1;
+            copy_match(out, op, (int)off, len, flushed, lane);
+            op += len;
+        }
+    }
+    return op == ul ? op : -1;
+}
+
+}  // namespace
+
+// codec: 0 = lz4, 1 = snappy, 2 = raw copy only.  offsets[i] = byte offset of chunk i in
+// `packed`; a chunk whose csize equals its size was stored raw (lzbench.cpp:311-315).
+extern "C" __global__ void __launch_bounds__(64)
+lzh_decompress_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                      const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
+                      int32_t* status, uint32_t chunk0) {
+    const int lane = threadIdx.x;
+    const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
+    const uint64_t ooff = chunk * chunk_size;
+    if (ooff >= n_total) return;
+    const int part = (int)min(chunk_size, n_total - ooff);
+    const uint64_t ioff = offsets[chunk];
+    const int cs = (int)csizes[chunk];
+    const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+    Bytes rin, rout;
+    rin.init(packed + ioff, readable);
+    rout.init(out + ooff, (uint64_t)part);
+    int r;
+    if (cs == part || codec == 2) {
+        copy_raw(rin, rout, part, lane);
+        r = part;
+    } else if (codec == 0) {
+        r = lz4_decode(rin, cs, rout, part, lane);
+    } else {
+        r = snappy_decode(rin, cs, rout, part, lane);
+    }
+    if (lane == 0) status[chunk] = r;
+}
+
+#include "launch.h"
+hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                                 const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
+                                 int32_t* status, uint32_t nchunks, hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(lzh_decompress_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
+                       offsets, csizes, n_total, chunk_size, out, status, 0u);
+    return hipGetLastError();
+}

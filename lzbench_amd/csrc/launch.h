@@ -1,0 +1,21 @@
+// lzbench_amd/csrc/launch.h -- host-side launchers exported by each kernel translation unit
+// (internal to liblzbench_hip.so; the public C-ABI is include/lzbench_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+hipError_t lzh_launch_lz4_compress(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                                   int acc, uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
+                                   hipStream_t s);
+hipError_t lzh_launch_snappy_compress(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                                      uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
+                                      hipStream_t s);
+hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                                 const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
+                                 int32_t* status, uint32_t nchunks, hipStream_t s);
+hipError_t lzh_launch_scan(const uint32_t* csizes, uint64_t nchunks, uint64_t* offsets, uint64_t* total,
+                           hipStream_t s);
+hipError_t lzh_launch_pack(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                           const uint8_t* stage, uint64_t stride, const uint32_t* csizes, const uint64_t* offsets,
+                           uint8_t* packed, uint64_t packed_cap, uint32_t nchunks, hipStream_t s);
+hipError_t lzh_launch_memcpy(const void* src, void* dst, uint64_t n, hipStream_t s);

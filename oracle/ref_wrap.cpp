@@ -1,0 +1,149 @@
+/*
+ * oracle/ref_wrap.cpp -- extern "C" shims over the REFERENCE codecs, compiled straight from
+ * /root/reference/lz4/lz4.c and /root/reference/snappy/*.cc by oracle/Makefile into
+ * oracle/_ref/libref.so.  TEST INFRASTRUCTURE ONLY: used to pin the oracle restatement
+ * (golden vectors) and as bench.py's cpu_baseline (kind "reference").  No reference source
+ * is copied into this repository; this file only calls the reference's public API.
+ *
+ * The chunk loops mirror lzbench's exactly:
+ *   lzbench_compress   /root/reference/_lzbench/lzbench.cpp:266-298
+ *   lzbench_decompress /root/reference/_lzbench/lzbench.cpp:301-329
+ *   lz4 row adapters   /root/reference/_lzbench/compressors.cpp:343-362
+ *     (LZ4_compress_default / LZ4_compress_fast(level), LZ4_decompress_fast)
+ *   snappy adapters    /root/reference/_lzbench/compressors.cpp:1282-1292
+ */
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+#include "lz4.h"
+#include "snappy.h"
+
+#define REF_COMPRESS_BOUND(n) ((n) + (n) / 6 + 16 * 1024)   /* GET_COMPRESS_BOUND, lzbench.h:17 */
+
+extern "C" {
+
+int ref_lz4_version(void) { return LZ4_versionNumber(); }
+int ref_lz4_compress_fast(const char* s, char* d, int n, int cap, int acc) { return LZ4_compress_fast(s, d, n, cap, acc); }
+int ref_lz4_compress_default(const char* s, char* d, int n, int cap) { return LZ4_compress_default(s, d, n, cap); }
+int ref_lz4_decompress_safe(const char* s, char* d, int csize, int cap) { return LZ4_decompress_safe(s, d, csize, cap); }
+int ref_lz4_decompress_fast(const char* s, char* d, int osize) { return LZ4_decompress_fast(s, d, osize); }
+size_t ref_snappy_compress(const char* s, size_t n, char* d) { size_t out = 0; snappy::RawCompress(s, n, d, &out); return out; }
+int ref_snappy_uncompress(const char* s, size_t csize, char* d) { return snappy::RawUncompress(s, csize, d) ? 1 : 0; }
+size_t ref_snappy_max_compressed_length(size_t n) { return snappy::MaxCompressedLength(n); }
+
+static int64_t one_compress(int codec, int level, const char* in, size_t part, char* out, size_t outpart) {
+    if (codec == 0) {
+        if (level <= 1) return LZ4_compress_default(in, out, (int)part, (int)outpart);
+        return LZ4_compress_fast(in, out, (int)part, (int)outpart, level);
+    }
+    size_t o = outpart;
+    snappy::RawCompress(in, part, out, &o);
+    return (int64_t)o;
+}
+
+static int64_t one_decompress(int codec, const char* in, size_t csize, char* out, size_t osize) {
+    if (codec == 0) { LZ4_decompress_fast(in, out, (int)osize); return (int64_t)osize; }
+    snappy::RawUncompress(in, csize, out);
+    return (int64_t)osize;
+}
+
+/* lzbench_compress over [c0,c1): packs into out, returns bytes */
+static int64_t range_compress(int codec, int level, const uint8_t* in, size_t n, size_t chunk,
+                              size_t c0, size_t c1, uint8_t* out, size_t outsize, uint64_t* csizes) {
+    size_t nchunks = (n + chunk - 1) / chunk;
+    int64_t sum = 0;
+    for (size_t i = c0; i < c1; i++) {
+        size_t part = (i + 1 < nchunks) ? chunk : n - i * chunk;
+        size_t outpart = REF_COMPRESS_BOUND(part);
+        if (outpart > outsize) outpart = outsize;
+        const uint8_t* src = in + i * chunk;
+        int64_t clen = one_compress(codec, level, (const char*)src, part, (char*)out, outpart);
+        if (clen <= 0 || (size_t)clen == part) {
+            if (part > outsize) return 0;
+            memcpy(out, src, part);
+            clen = (int64_t)part;
+        }
+        out += clen; outsize -= (size_t)clen; csizes[i] = (uint64_t)clen; sum += clen;
+    }
+    return sum;
+}
+
+int64_t ref_compress_chunks(int codec, int level, const uint8_t* in, size_t n, size_t chunk,
+                            uint8_t* out, uint64_t* csizes) {
+    size_t nchunks = (n + chunk - 1) / chunk;
+    return range_compress(codec, level, in, n, chunk, 0, nchunks, out, REF_COMPRESS_BOUND(n), csizes);
+}
+
+int64_t ref_decompress_chunks(int codec, const uint8_t* packed, const uint64_t* csizes, size_t n,
+                              size_t chunk, uint8_t* out) {
+    size_t nchunks = (n + chunk - 1) / chunk;
+    int64_t sum = 0;
+    for (size_t i = 0; i < nchunks; i++) {
+        size_t part = (i + 1 < nchunks) ? chunk : n - i * chunk;
+        int64_t d;
+        if (csizes[i] == part) { memcpy(out, packed, part); d = (int64_t)part; }
+        else d = one_decompress(codec, (const char*)packed, csizes[i], (char*)out, part);
+        if (d <= 0) return d;
+        packed += csizes[i]; out += d; sum += d;
+    }
+    return sum;
+}
+
+/* all-cores variants: contiguous chunk ranges per thread, private staging, ordered gather */
+int64_t ref_compress_chunks_mt(int codec, int level, const uint8_t* in, size_t n, size_t chunk,
+                               uint8_t* out, uint64_t* csizes, int threads) {
+    size_t nchunks = (n + chunk - 1) / chunk;
+    if (threads < 1) threads = 1;
+    if ((size_t)threads > nchunks) threads = nchunks ? (int)nchunks : 1;
+    std::vector<std::vector<uint8_t>> stage((size_t)threads);
+    std::vector<int64_t> res((size_t)threads, 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+        size_t c0 = nchunks * (size_t)t / (size_t)threads, c1 = nchunks * (size_t)(t + 1) / (size_t)threads;
+        size_t span = (c1 - c0) * chunk;
+        stage[(size_t)t].resize(REF_COMPRESS_BOUND(span) + 64);
+        th.emplace_back([&, t, c0, c1]() {
+            res[(size_t)t] = range_compress(codec, level, in, n, chunk, c0, c1, stage[(size_t)t].data(),
+                                            stage[(size_t)t].size(), csizes);
+        });
+    }
+    int64_t sum = 0;
+    for (int t = 0; t < threads; t++) {
+        th[(size_t)t].join();
+        memcpy(out + sum, stage[(size_t)t].data(), (size_t)res[(size_t)t]);
+        sum += res[(size_t)t];
+    }
+    return sum;
+}
+
+int64_t ref_decompress_chunks_mt(int codec, const uint8_t* packed, const uint64_t* csizes, size_t n,
+                                 size_t chunk, uint8_t* out, int threads) {
+    size_t nchunks = (n + chunk - 1) / chunk;
+    if (threads < 1) threads = 1;
+    if ((size_t)threads > nchunks) threads = nchunks ? (int)nchunks : 1;
+    std::vector<uint64_t> off(nchunks + 1, 0);
+    for (size_t i = 0; i < nchunks; i++) off[i + 1] = off[i] + csizes[i];
+    std::vector<int64_t> res((size_t)threads, 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+        size_t c0 = nchunks * (size_t)t / (size_t)threads, c1 = nchunks * (size_t)(t + 1) / (size_t)threads;
+        th.emplace_back([&, t, c0, c1]() {
+            int64_t s = 0;
+            for (size_t i = c0; i < c1; i++) {
+                size_t part = (i + 1 < nchunks) ? chunk : n - i * chunk;
+                int64_t d;
+                if (csizes[i] == part) { memcpy(out + i * chunk, packed + off[i], part); d = (int64_t)part; }
+                else d = one_decompress(codec, (const char*)packed + off[i], csizes[i], (char*)out + i * chunk, part);
+                if (d <= 0) { s = d; break; }
+                s += d;
+            }
+            res[(size_t)t] = s;
+        });
+    }
+    int64_t sum = 0;
+    for (int t = 0; t < threads; t++) { th[(size_t)t].join(); if (res[(size_t)t] <= 0) return -1; sum += res[(size_t)t]; }
+    return sum;
+}
+
+}  // extern "C"
