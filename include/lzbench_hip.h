@@ -93,6 +93,12 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
 int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, size_t in_readable,
                              size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream);
 
+/* The rest of lzh_compress_async after lzh_compress_kernel_only: scan the per-chunk sizes
+ * into d_offsets and pack the staged streams (or the raw input) into d_packed. */
+int lzh_compress_finish_async(int codec, const void* d_in, size_t n, size_t in_readable, size_t chunk_size,
+                              const void* d_stage, const uint32_t* d_csizes, void* d_packed, size_t packed_cap,
+                              uint64_t* d_offsets, void* hip_stream);
+
 /* synthetic corpora of SURVEY.md 8(d): 0 random, 1 text, 2 json logs, 3 mixed, 4 binary */
 size_t lzh_datagen(int kind, uint64_t seed, void* buf, size_t n);
 const char* lzh_version(void);

@@ -74,6 +74,7 @@ SIGNATURES = {
     "lzh_compress_async": (C.c_int, [C.c_int, C.c_int, _P, _SZ, _SZ, _SZ, _P, _SZ, _P, _P, _P, _SZ, _P]),
     "lzh_decompress_async": (C.c_int, [C.c_int, _P, _SZ, _P, _P, _SZ, _SZ, _P, _P, _P, _SZ, _P]),
     "lzh_compress_kernel_only": (C.c_int, [C.c_int, C.c_int, _P, _SZ, _SZ, _SZ, _P, _P, _P]),
+    "lzh_compress_finish_async": (C.c_int, [C.c_int, _P, _SZ, _SZ, _SZ, _P, _P, _P, _SZ, _P, _P]),
     "lzh_datagen": (_SZ, [C.c_int, C.c_uint64, _P, _SZ]),
     "lzh_version": (C.c_char_p, []),
 }
@@ -273,6 +274,13 @@ class DeviceCodec:
                                             self._stream())
         if rc:
             raise RuntimeError(f"lzh_compress_kernel_only failed ({rc})")
+
+    def compress_finish(self, d_in) -> None:
+        rc = lib().lzh_compress_finish_async(self.codec, d_in.data_ptr(), self.n, d_in.numel(), self.chunk_size,
+                                             self.ctemp.data_ptr(), self.csizes.data_ptr(), self.packed.data_ptr(),
+                                             self.packed.numel(), self.offsets.data_ptr(), self._stream())
+        if rc:
+            raise RuntimeError(f"lzh_compress_finish_async failed ({rc})")
 
     def decompress(self, packed=None, csizes=None, offsets=None) -> None:
         packed = self.packed if packed is None else packed

@@ -109,11 +109,22 @@ int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t 
         return LZH_OK;
     }
     if (temp_bytes < lzh_compress_temp_bytes(codec, n, chunk_size) || !d_temp) return LZH_ESPACE;
-    const size_t stride = lzh_stage_stride(codec, chunk_size);
     int rc = lzh_compress_kernel_only(codec, level, d_in, n, in_readable, chunk_size, d_temp, d_csizes, hip_stream);
     if (rc) return rc;
+    return lzh_compress_finish_async(codec, d_in, n, in_readable, chunk_size, d_temp, d_csizes, d_packed, packed_cap,
+                                     d_offsets, hip_stream);
+}
+
+int lzh_compress_finish_async(int codec, const void* d_in, size_t n, size_t in_readable, size_t chunk_size,
+                              const void* d_stage, const uint32_t* d_csizes, void* d_packed, size_t packed_cap,
+                              uint64_t* d_offsets, void* hip_stream) {
+    hipStream_t s = (hipStream_t)hip_stream;
+    if (!chunk_size || !d_stage || !d_csizes || !d_packed || !d_offsets) return LZH_EARG;
+    if (codec != LZH_CODEC_LZ4 && codec != LZH_CODEC_SNAPPY) return LZH_EARG;
+    const size_t k = lzh_num_chunks(n, chunk_size);
+    const size_t stride = lzh_stage_stride(codec, chunk_size);
     LZH_CHECK(lzh_launch_scan(d_csizes, k, d_offsets, nullptr, s));
-    LZH_CHECK(lzh_launch_pack((const uint8_t*)d_in, n, in_readable, chunk_size, (const uint8_t*)d_temp, stride,
+    LZH_CHECK(lzh_launch_pack((const uint8_t*)d_in, n, in_readable, chunk_size, (const uint8_t*)d_stage, stride,
                               d_csizes, d_offsets, (uint8_t*)d_packed, packed_cap, (uint32_t)k, s));
     return LZH_OK;
 }

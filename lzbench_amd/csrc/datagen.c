@@ -15,6 +15,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 
 enum { LZB_DATA_RANDOM = 0, LZB_DATA_TEXT = 1, LZB_DATA_JSON = 2, LZB_DATA_MIXED = 3, LZB_DATA_BINARY = 4 };
 
@@ -28,10 +29,12 @@ static uint64_t sm_next(sm64* r) {
 static double sm_unit(sm64* r) { return (double)(sm_next(r) >> 11) * (1.0 / 9007199254740992.0); }
 
 #define VOCAB 5000
+#define ZIPF_LUT_BITS 20
 typedef struct {
     char words[VOCAB][11];
     uint8_t lens[VOCAB];
     double cdf[VOCAB];
+    uint16_t lut[1 << ZIPF_LUT_BITS];   /* inverse CDF quantised to 2^20 buckets */
 } vocab_t;
 
 static void vocab_init(vocab_t* v, uint64_t seed) {
@@ -46,13 +49,16 @@ static void vocab_init(vocab_t* v, uint64_t seed) {
         v->cdf[i] = acc;
     }
     for (int i = 0; i < VOCAB; i++) v->cdf[i] /= acc;
+    int w = 0;
+    for (int b = 0; b < (1 << ZIPF_LUT_BITS); b++) {
+        double u = ((double)b + 0.5) / (double)(1 << ZIPF_LUT_BITS);
+        while (w < VOCAB - 1 && v->cdf[w] < u) w++;
+        v->lut[b] = (uint16_t)w;
+    }
 }
 
 static int vocab_pick(const vocab_t* v, sm64* r) {
-    double u = sm_unit(r);
-    int lo = 0, hi = VOCAB - 1;
-    while (lo < hi) { int mid = (lo + hi) >> 1; if (v->cdf[mid] < u) lo = mid + 1; else hi = mid; }
-    return lo;
+    return v->lut[sm_next(r) >> (64 - ZIPF_LUT_BITS)];
 }
 
 static size_t gen_random(uint8_t* buf, size_t n, uint64_t seed) {
@@ -126,25 +132,57 @@ static size_t gen_binary(uint8_t* buf, size_t n, uint64_t seed) {
     return n;
 }
 
-/* Fill buf[0..n) with corpus `kind`. Returns n, or 0 on bad kind. */
-size_t lzb_datagen(int kind, uint64_t seed, uint8_t* buf, size_t n) {
-    static vocab_t vocab;     /* fixed vocabulary (independent of seed) */
-    static int vocab_ready = 0;
-    if (!vocab_ready) { vocab_init(&vocab, 12345); vocab_ready = 1; }
+static vocab_t g_vocab;
+static pthread_once_t g_vocab_once = PTHREAD_ONCE_INIT;
+static void vocab_once(void) { vocab_init(&g_vocab, 12345); }
+
+static size_t gen_one(int kind, uint64_t seed, uint8_t* buf, size_t n) {
     switch (kind) {
     case LZB_DATA_RANDOM: return gen_random(buf, n, seed);
-    case LZB_DATA_TEXT: return gen_text(buf, n, seed, &vocab);
-    case LZB_DATA_JSON: return gen_json(buf, n, seed, &vocab);
+    case LZB_DATA_TEXT: return gen_text(buf, n, seed, &g_vocab);
+    case LZB_DATA_JSON: return gen_json(buf, n, seed, &g_vocab);
     case LZB_DATA_BINARY: return gen_binary(buf, n, seed);
-    case LZB_DATA_MIXED: {
-        const size_t stripe = (size_t)64 << 20;
-        for (size_t pos = 0, s = 0; pos < n; pos += stripe, s++) {
-            size_t len = n - pos < stripe ? n - pos : stripe;
-            static const int order[4] = { LZB_DATA_TEXT, LZB_DATA_JSON, LZB_DATA_BINARY, LZB_DATA_RANDOM };
-            lzb_datagen(order[s % 4], seed + s, buf + pos, len);
-        }
-        return n;
-    }
     default: return 0;
     }
+}
+
+/* Corpora are generated in independent 16 MiB segments (segment s seeded with
+ * seed * 1000003 + s), so the bytes do not depend on how many threads produce them. */
+#define SEG ((size_t)16 << 20)
+typedef struct { int kind; uint64_t seed; uint8_t* buf; size_t n, s0, s1; } seg_job;
+
+static int kind_of_segment(int kind, size_t s) {
+    static const int order[4] = { LZB_DATA_TEXT, LZB_DATA_JSON, LZB_DATA_BINARY, LZB_DATA_RANDOM };
+    if (kind != LZB_DATA_MIXED) return kind;
+    return order[(s * SEG / ((size_t)64 << 20)) % 4];     /* 64 MiB stripes */
+}
+
+static void* seg_worker(void* a) {
+    seg_job* j = (seg_job*)a;
+    for (size_t s = j->s0; s < j->s1; s++) {
+        size_t off = s * SEG, len = j->n - off < SEG ? j->n - off : SEG;
+        gen_one(kind_of_segment(j->kind, s), j->seed * 1000003ull + s, j->buf + off, len);
+    }
+    return NULL;
+}
+
+/* Fill buf[0..n) with corpus `kind`. Returns n, or 0 on bad kind. */
+size_t lzb_datagen(int kind, uint64_t seed, uint8_t* buf, size_t n) {
+    if (kind < 0 || kind > LZB_DATA_BINARY) return 0;
+    pthread_once(&g_vocab_once, vocab_once);
+    size_t nseg = (n + SEG - 1) / SEG;
+    int threads = nseg < 16 ? (int)nseg : 16;
+    if (threads <= 1) {
+        seg_job j = { kind, seed, buf, n, 0, nseg };
+        seg_worker(&j);
+        return n;
+    }
+    pthread_t th[16];
+    seg_job jobs[16];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (seg_job){ kind, seed, buf, n, nseg * (size_t)t / (size_t)threads, nseg * (size_t)(t + 1) / (size_t)threads };
+        pthread_create(&th[t], NULL, seg_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    return n;
 }

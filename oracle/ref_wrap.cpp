@@ -14,6 +14,7 @@
  */
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <vector>
 #include "lz4.h"
@@ -96,22 +97,24 @@ int64_t ref_compress_chunks_mt(int codec, int level, const uint8_t* in, size_t n
     size_t nchunks = (n + chunk - 1) / chunk;
     if (threads < 1) threads = 1;
     if ((size_t)threads > nchunks) threads = nchunks ? (int)nchunks : 1;
-    std::vector<std::vector<uint8_t>> stage((size_t)threads);
+    std::vector<std::unique_ptr<uint8_t[]>> stage((size_t)threads);
+    std::vector<size_t> stage_cap((size_t)threads);
     std::vector<int64_t> res((size_t)threads, 0);
     std::vector<std::thread> th;
     for (int t = 0; t < threads; t++) {
         size_t c0 = nchunks * (size_t)t / (size_t)threads, c1 = nchunks * (size_t)(t + 1) / (size_t)threads;
         size_t span = (c1 - c0) * chunk;
-        stage[(size_t)t].resize(REF_COMPRESS_BOUND(span) + 64);
+        stage_cap[(size_t)t] = REF_COMPRESS_BOUND(span) + 64;
+        stage[(size_t)t].reset(new uint8_t[stage_cap[(size_t)t]]);   /* no zero fill */
         th.emplace_back([&, t, c0, c1]() {
-            res[(size_t)t] = range_compress(codec, level, in, n, chunk, c0, c1, stage[(size_t)t].data(),
-                                            stage[(size_t)t].size(), csizes);
+            res[(size_t)t] = range_compress(codec, level, in, n, chunk, c0, c1, stage[(size_t)t].get(),
+                                            stage_cap[(size_t)t], csizes);
         });
     }
     int64_t sum = 0;
     for (int t = 0; t < threads; t++) {
         th[(size_t)t].join();
-        memcpy(out + sum, stage[(size_t)t].data(), (size_t)res[(size_t)t]);
+        memcpy(out + sum, stage[(size_t)t].get(), (size_t)res[(size_t)t]);
         sum += res[(size_t)t];
     }
     return sum;

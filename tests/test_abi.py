@@ -1,0 +1,90 @@
+"""CPU: the C-ABI library loads and exports every symbol include/lzbench_hip.h declares; host
+logic of the Python mirror; the product never touches the oracle.  No GPU compute calls."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import lzbench_amd as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "lzbench_hip.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lz[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    names = header_functions()
+    for must in ("lzbench_hip_lz4_compress", "lzbench_hip_lz4_decompress", "lzbench_hip_snappy_compress",
+                 "lzbench_hip_snappy_decompress", "lzbench_hip_compress_batch", "lzbench_hip_decompress_batch",
+                 "lzh_compress_async", "lzh_decompress_async"):
+        assert must in names
+
+
+def test_library_exports_every_header_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(line.split()[-1] for line in out.splitlines() if line.strip())
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+
+
+def test_python_signatures_cover_header_and_load():
+    lib = L.lib()                      # loads the .so and binds every signature
+    assert set(header_functions()) == set(L.SIGNATURES)
+    assert b"gfx950" in lib.lzh_version()
+
+
+def test_size_helpers():
+    lib = L.lib()
+    assert lib.lzh_num_chunks(1 << 30, 65536) == 16384
+    assert lib.lzh_num_chunks(65537, 65536) == 2
+    assert lib.lzh_num_chunks(0, 65536) == 1
+    s = lib.lzh_stage_stride(0, 65536)
+    assert s % 256 == 0 and s >= 65536 + 65536 // 255 + 16       # >= LZ4_compressBound
+    assert lib.lzh_stage_stride(1, 65536) >= 32 + 65536 + 65536 // 6  # >= MaxCompressedLength
+    assert lib.lzh_compress_temp_bytes(0, 1 << 30, 65536) >= 16384 * s
+    assert lib.lzh_max_packed_bytes(0, 1 << 20, 65536) >= 16 * (65536 + 65536 // 255 + 16)
+
+
+def test_comp_desc_table_mirrors_lzbench():
+    assert L.COMP_DESC[0].name == "memcpy"                   # lzbench.cpp:609, :695
+    assert L.find_compressor("lz4").name == "hip_lz4"
+    assert L.find_compressor("snappy").name == "hip_snappy"
+    assert (L.find_compressor("lz4fast").first_level, L.find_compressor("lz4fast").last_level) == (1, 99)
+    with pytest.raises(KeyError):
+        L.find_compressor("zling")
+    syms = set(L.SIGNATURES)
+    for d in L.COMP_DESC[1:]:
+        for f in (d.compress, d.decompress, d.init, d.deinit, d.compress_batch, d.decompress_batch):
+            assert f in syms
+
+
+def test_chunk_list_like_lzbench():
+    cs = L.chunk_sizes_for(200_000, 65536)                   # lzbench.cpp:366-373
+    assert cs.tolist() == [65536, 65536, 65536, 3392]
+    assert L.chunk_sizes_for(131072, 65536).tolist() == [65536, 65536]
+    assert L.get_compress_bound(600) == 600 + 100 + 16384
+
+
+def test_datagen_deterministic_and_segmented():
+    a = L.datagen("text", 40 << 20, seed=3)
+    b = L.datagen("text", 40 << 20, seed=3)
+    assert (a == b).all()
+    c = L.datagen("text", 20 << 20, seed=3)                   # same prefix regardless of length
+    assert (a[: 20 << 20] == c).all()
+    assert set(np.unique(L.datagen("text", 1 << 16, seed=1))) <= set(b"abcdefghijklmnopqrstuvwxyz \n")
+
+
+def test_product_sources_never_reference_the_oracle():
+    for d, _, files in os.walk(os.path.join(ROOT, "lzbench_amd")):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".c", ".h")):
+                txt = open(os.path.join(d, f)).read()
+                for bad in ("liboracle", "libref", "oracle_lib", "import oracle", "oracle/"):
+                    assert bad not in txt, (f, bad)

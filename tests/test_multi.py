@@ -1,0 +1,70 @@
+"""CPU, world_size 2 over gloo: the chunk-sharded multi-rank path gathers to a
+result byte-identical to the single-process lzbench chunk loop.  Each rank's codec here is the
+CPU checker (no GPU in this container); on the GPU box the same protocol runs with the HIP codec
+(tests/test_gpu_parity.py covers that codec bit for bit)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import oracle_lib as O
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, codec, chunk, n, q):
+    import torch.distributed as dist
+    import lzbench_amd as L
+    from lzbench_amd.shard import sharded_compress
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    data = L.datagen("json", n, seed=77)
+    res = sharded_compress(data, chunk, rank, world, lambda shard: O.compress_chunks(shard, codec, chunk))
+    # max-over-ranks timing reduction of bench.py's control plane
+    import torch
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        q.put((res[0].tobytes(), res[1].tolist(), float(t.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("codec,chunk", [("lz4", 65536), ("snappy", 262144)])
+def test_two_rank_shard_gather_equals_single(codec, chunk):
+    import lzbench_amd as L
+    n = 3 * chunk + 12345                       # ragged tail, uneven split across ranks
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, codec, chunk, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    packed, cs, tmax = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    data = L.datagen("json", n, seed=77)
+    ep, ec = O.compress_chunks(data, codec, chunk)
+    assert np.frombuffer(packed, np.uint8).tobytes() == ep.tobytes()
+    assert cs == ec.tolist()
+    assert tmax == 2.0
+
+
+def test_shard_ranges_cover_all_chunks():
+    from lzbench_amd.shard import shard_range, shard_bytes
+    for k in (1, 2, 7, 16384):
+        for w in (1, 2, 3, 8):
+            rs = [shard_range(k, r, w) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == k
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+    assert shard_bytes(200_000, 65536, 1, 2) == (131072, 200_000)
