@@ -96,3 +96,8 @@ __device__ __forceinline__ void copy_span(const Bytes& src, int s0, const Bytes&
     const int tail0 = head + 4 * nd;
     if (t < len - tail0) dst.st8(d0 + tail0 + t, src.b(s0 + tail0 + t));
 }
+
+// LDS pointers must carry address space 3: a generic pointer to __shared__ memory compiles to
+// flat_load/flat_store (vector-memory pipe, vmcnt waits) instead of ds_read/ds_write.
+#define LDSA __attribute__((address_space(3)))
+__device__ __forceinline__ void lds_zero16(LDSA uint32_t* p) { p[0] = 0; p[1] = 0; p[2] = 0; p[3] = 0; }

@@ -42,13 +42,13 @@ __device__ __forceinline__ void probe_sched(int k, int64_t a64, int64_t& off, in
 // compiler must neither forward a lane's own store nor cache a slot in a register
 template <bool kSmall>
 struct Lz4Table {
-    uint32_t* raw;   // 16 KiB of LDS
+    LDSA uint32_t* raw;   // 16 KiB of LDS
     __device__ __forceinline__ uint32_t get(uint32_t h) const {
-        if (kSmall) return ((volatile const uint16_t*)raw)[h];
-        return ((volatile const uint32_t*)raw)[h];
+        if (kSmall) return ((volatile const LDSA uint16_t*)raw)[h];
+        return ((volatile const LDSA uint32_t*)raw)[h];
     }
     __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
-        if (kSmall) ((volatile uint16_t*)raw)[h] = (uint16_t)v; else ((volatile uint32_t*)raw)[h] = v;
+        if (kSmall) ((volatile LDSA uint16_t*)raw)[h] = (uint16_t)v; else ((volatile LDSA uint32_t*)raw)[h] = v;
     }
 };
 
@@ -80,7 +80,7 @@ __device__ __forceinline__ void write_run(const Bytes& out, int dst, int count, 
 }
 
 template <bool kSmall>
-__device__ void lz4_compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, uint32_t* lds,
+__device__ void lz4_compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* lds,
                                    uint32_t* out_size) {
     const int lane = threadIdx.x;
     Lz4Table<kSmall> T{lds};
@@ -93,9 +93,9 @@ __device__ void lz4_compress_chunk(const Bytes& in, int n, const Bytes& out, int
     }
     // zero the table: 16 KiB = 64 lanes x 16 x 16 B
     {
-        uint4* t4 = (uint4*)lds;
+        LDSA uint32_t* t4 = (LDSA uint32_t*)lds;
 #pragma unroll
-        for (int i = 0; i < 16; i++) t4[i * LZH_WAVE + lane] = make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
         wave_lds_fence();
     }
     if (n >= kMinLength) {
@@ -272,8 +272,8 @@ lzh_lz4_compress_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readabl
     Bytes rin, rout;
     rin.init(in + off, readable);
     rout.init(stage + chunk * stride, stride);
-    if (n < 65547) lz4_compress_chunk<true>(rin, n, rout, acc, lds, csizes + chunk);
-    else lz4_compress_chunk<false>(rin, n, rout, acc, lds, csizes + chunk);
+    if (n < 65547) lz4_compress_chunk<true>(rin, n, rout, acc, (LDSA uint32_t*)lds, csizes + chunk);
+    else lz4_compress_chunk<false>(rin, n, rout, acc, (LDSA uint32_t*)lds, csizes + chunk);
 }
 
 #include "launch.h"

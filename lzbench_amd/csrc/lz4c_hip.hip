@@ -1,0 +1,417 @@
+// lzbench_amd/csrc/lz4c_hip.hip -- LZ4 block compressor (v3) for gfx950, bit-exact with lz4 1.9.3.
+//
+// Same greedy parse as the reference (lz4/lz4.c:851-1240) and as the v1 kernel
+// (lz4_hip.hip), organised so that one sequence costs one batch of ~150 wave instructions and
+// one dependent global-memory round trip:
+//
+//   * input ring: 1 KiB of the chunk around the parse front lives in LDS, filled ahead of
+//     the front by LDS-DMA (buffer_load ... lds).  Probe hashing, the ip-2 insert, ip-side
+//     catch-up / match-length bytes and literal bytes read LDS.
+//   * speculative candidate window: the 4-byte candidate compare loads 24 bytes
+//     [cand-4, cand+20) per lane; the hit lane's window (parked in 32 B of LDS) answers
+//     catch-up (<= 4 bytes, lz4.c:1019) and the first 12 bytes of LZ4_count (lz4.c:603-626)
+//     lane-parallel, without a second round trip.
+//   * deferred, branch-free emission: a sequence's bytes are stored while the next batch's
+//     candidate loads are in flight.
+//   * fast probe plan: with acceleration 1 the first 65 probes of a search step by 1, so a
+//     batch that starts a search (or re-tests a match end) is simply positions base+lane.
+// Long catch-ups / matches / literal runs beyond the windows take lane-parallel slow paths.
+#include "common.h"
+
+namespace lz4v3 {
+
+// optional per-kernel event counters (debug builds of the launch only; nullptr in production)
+#define LZ_STAT(i, v) do { if (stats && lane == 0) atomicAdd(&stats[i], (unsigned long long)(v)); } while (0)
+
+constexpr int kMinMatch = 4;
+constexpr int kMfLimit = 12;
+constexpr int kLastLiterals = 5;
+constexpr int kMinLength = 13;
+constexpr int kRing = 1024;           // bytes of LDS input ring per wave
+constexpr int kAhead = 704;           // keep the ring filled this far past the batch front
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ int64_t step_prefix(int64_t M) {
+    int64_t q = M >> 6, r = M & 63;
+    return 32 * q * (q - 1) + r * q;
+}
+
+template <bool kSmall>
+struct Table {
+    LDSA uint32_t* raw;
+    __device__ __forceinline__ uint32_t get(uint32_t h) const {
+        if (kSmall) return ((volatile const LDSA uint16_t*)raw)[h];
+        return ((volatile const LDSA uint32_t*)raw)[h];
+    }
+    __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
+        if (kSmall) ((volatile LDSA uint16_t*)raw)[h] = (uint16_t)v; else ((volatile LDSA uint32_t*)raw)[h] = v;
+    }
+};
+
+template <bool kSmall>
+__device__ __forceinline__ uint32_t hash_of(uint32_t w32, uint32_t b4) {
+    if (kSmall) return (w32 * 2654435761u) >> 19;
+    const uint64_t v = (uint64_t)w32 | ((uint64_t)b4 << 32);
+    return (uint32_t)(((v << 24) * 889523592379ull) >> 52);
+}
+
+// LDS ring over descriptor offsets X = p + sh: holds [fill - kRing, fill).
+struct Ring {
+    LDSA uint32_t* w;
+    int sh;
+    int fill;
+    __device__ __forceinline__ bool has(int p0, int p1) const { return p0 + sh >= fill - kRing && p1 + sh <= fill; }
+    __device__ __forceinline__ uint32_t dword(int a) const {
+        return ((volatile const LDSA uint32_t*)w)[(a >> 2) & (kRing / 4 - 1)];
+    }
+    __device__ __forceinline__ uint32_t u32(int p) const {
+        const int X = p + sh, a = X & ~3;
+        return __builtin_amdgcn_alignbyte(dword(a + 4), dword(a), (uint32_t)X & 3u);
+    }
+    __device__ __forceinline__ uint32_t byte(int p) const {
+        return ((volatile const LDSA uint8_t*)w)[(p + sh) & (kRing - 1)];
+    }
+    __device__ __forceinline__ void refill(rsrc_t r, int lane) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(w + ((fill & (kRing - 1)) >> 2)), 4, fill + 4 * lane,
+                                                 0, 0, 0);
+        fill += 256;
+    }
+};
+
+__device__ __forceinline__ int ext_len_bytes(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+
+// Emit one sequence (has_match) or the final literal run at op. Each lane computes its
+// byte of the sequence without branching; literal bytes come from the ring when it holds
+// them. Returns the new op.
+__device__ __forceinline__ int emit_seq(const Bytes& in, const Ring& R, const Bytes& out, int op, int anchor, int lit,
+                                        bool has_match, int off, int ml, int lane) {
+    const int lx = ext_len_bytes(lit);
+    const int mx = has_match ? ext_len_bytes(ml) : 0;
+    const int lit0 = 1 + lx, lit1 = lit0 + lit;            // literal bytes at [lit0, lit1)
+    const int total = lit1 + (has_match ? 2 + mx : 0);
+    const uint32_t token = ((uint32_t)min(lit, 15) << 4) | (has_match ? (uint32_t)min(ml, 15) : 0u);
+    const uint32_t lrem = (uint32_t)((lit - 15) % 255), mrem = (uint32_t)((ml - 15) % 255);
+    const bool lit_in_ring = R.has(anchor, anchor + lit);
+    if (!lit_in_ring && lit > 2 * LZH_WAVE) {
+        // long literal run: header, bulk copy, trailer
+        if (lane == 0) out.st8(op, token);
+        for (int b = lane; b < lx; b += LZH_WAVE) out.st8(op + 1 + b, b == lx - 1 ? lrem : 255u);
+        copy_span(in, anchor, out, op + lit0, lit, lane, LZH_WAVE);
+        if (has_match) {
+            if (lane < 2) out.st8(op + lit1 + lane, lane ? ((uint32_t)off >> 8) : ((uint32_t)off & 0xffu));
+            for (int b = lane; b < mx; b += LZH_WAVE) out.st8(op + lit1 + 2 + b, b == mx - 1 ? mrem : 255u);
+        }
+        return op + total;
+    }
+    for (int base = 0; base < total; base += LZH_WAVE) {
+        const int t = base + lane;
+        const int lp = anchor + t - lit0;
+        const bool inlit = t >= lit0 && t < lit1;
+        uint32_t lb = 0;
+        if (lit_in_ring) lb = R.byte(lp);
+        else if (inlit) lb = in.b(lp);
+        const int u = t - (lit1 + 2);
+        uint32_t v = token;
+        v = (t >= 1 && t < lit0) ? (t == lx ? lrem : 255u) : v;
+        v = inlit ? lb : v;
+        v = t == lit1 ? ((uint32_t)off & 0xffu) : v;
+        v = t == lit1 + 1 ? ((uint32_t)off >> 8) : v;
+        v = (u >= 0) ? (u == mx - 1 ? mrem : 255u) : v;
+        if (t < total) out.st8(op + t, v);
+    }
+    return op + total;
+}
+
+template <bool kSmall>
+__device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab, LDSA uint32_t* ringw,
+                               LDSA uint32_t* specw, uint32_t* out_size, unsigned long long* stats) {
+    const int lane = threadIdx.x;
+    Table<kSmall> T{tab};
+    if (n <= 0) {
+        if (lane == 0) out.st8(0, 0);
+        if (lane == 0) *out_size = 1;
+        return;
+    }
+    {
+        LDSA uint32_t* t4 = (LDSA uint32_t*)tab;
+#pragma unroll
+        for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
+    }
+    Ring R{ringw, in.sh, 0};
+    const int endX = n + in.sh + 8;
+    for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
+    wait_vm();
+    wave_lds_fence();
+
+    int op = 0, anchor = 0;
+    bool pend = false;                       // deferred sequence
+    int p_anchor = 0, p_lit = 0, p_off = 0, p_ml = 0;
+
+    if (n >= kMinLength) {
+        const int mfl1 = n - kMfLimit + 1;
+        const int mlimit = n - kLastLiterals;
+        const int64_t a64 = (int64_t)acc << 6;
+        const int hb = kSmall ? 4 : 5;
+
+        {
+            const uint32_t h0 = hash_of<kSmall>(R.u32(0), R.byte(4));
+            if (lane == 0) T.put(h0, 0);
+            wave_lds_fence();
+        }
+        int ip = 1, s = 1, k0 = 0;
+        bool retest = false;
+
+        for (int guard = 0; guard < 4 * n + 64; guard++) {
+            // ---- probe plan: lane -> position p, validity (forwardIp <= mflimitPlusOne)
+            int p;
+            bool valid;
+            if (acc == 1 && k0 == 0) {
+                // retest: lane 0 = ip, lanes j>=1 = search from ip+1 probe j-1 (step 1) -> ip + j;
+                // fresh search: s + j.  Either way base + lane with step 1.
+                p = (retest ? ip : s) + lane;
+                valid = p + 1 <= mfl1;
+            } else {
+                int64_t pp, nxt;
+                if (retest && lane == 0) {
+                    pp = ip;
+                    nxt = (int64_t)ip + 1;
+                } else {
+                    const int k = retest ? lane - 1 : k0 + lane;
+                    const int64_t o = k == 0 ? 0 : 1 + step_prefix(a64 + k - 1) - step_prefix(a64);
+                    const int64_t st = k == 0 ? 1 : (a64 + k - 1) >> 6;
+                    pp = (int64_t)s + o;
+                    nxt = pp + st;
+                }
+                valid = nxt <= mfl1;
+                p = valid ? (int)pp : 0;
+            }
+            const int pos = valid ? p : 0;
+            const uint64_t vmask = ballot(valid);
+            LZ_STAT(0, 1);
+            LZ_STAT(2, (acc == 1 && k0 == 0) ? 1 : 0);
+            const int front = rdlanei(pos, 0);
+            const int pmax = vmask ? rdlanei(pos, 63 - __builtin_clzll(vmask)) : front;
+
+            // ---- hash probe positions (ring when it covers the batch)
+            uint32_t pw, b4 = 0;
+            if (vmask && R.has(front - 4, pmax + hb + 8)) {
+                pw = R.u32(pos);
+                if (!kSmall) b4 = R.byte(pos + 4);
+            } else if (kSmall) {
+                LZ_STAT(9, 1);
+                pw = in.w32(pos);
+            } else {
+                const uint64_t v = in.w40(pos);
+                pw = (uint32_t)v;
+                b4 = (uint32_t)(v >> 32);
+            }
+            const uint32_t h = hash_of<kSmall>(pw, b4);
+            const uint32_t old = T.get(h);
+            if (valid) T.put(h, (uint32_t)pos);
+            wave_lds_fence();
+            const uint32_t back = T.get(h);
+            const uint64_t dup = ballot(valid && back != (uint32_t)pos);
+            uint32_t cand = old;
+            uint64_t grp = 1ull << lane;
+            if (dup) {
+                LZ_STAT(1, 1);
+                // exact in-batch collision resolution (rare)
+                wave_lds_fence();
+                if (valid) T.put(h, old);
+                wave_lds_fence();
+                uint64_t pending = dup;
+                int prev = -1;
+                for (int it = 0; it < LZH_WAVE && pending; it++) {
+                    const int l = ffs64(pending);
+                    const uint32_t hv = rdlane(h, l);
+                    const bool mine = valid && h == hv;
+                    const uint64_t m = ballot(mine);
+                    pending &= ~m;
+                    if (mine) {
+                        grp = m;
+                        const uint64_t below = m & ((1ull << lane) - 1ull);
+                        if (below) prev = 63 - __builtin_clzll(below);
+                    }
+                }
+                const uint32_t ppos = lane_gather((uint32_t)pos, prev < 0 ? lane : prev);
+                if (prev >= 0) cand = ppos;
+            }
+            // ---- speculative candidate window [cand-4, cand+20): one dwordx4 + one dwordx2
+            const int cX = (valid ? (int)cand : 0) + in.sh;
+            const int cA = (cX & ~3) - 4;
+            const uint32_t d0 = ld_b32(in.r, cA), d1 = ld_b32(in.r, cA + 4), d2 = ld_b32(in.r, cA + 8),
+                           d3 = ld_b32(in.r, cA + 12), d4 = ld_b32(in.r, cA + 16), d5 = ld_b32(in.r, cA + 20);
+            // ---- deferred emission of the previous sequence (stores overlap the loads above)
+            if (pend) {
+                op = emit_seq(in, R, out, op, p_anchor, p_lit, true, p_off, p_ml, lane);
+                pend = false;
+            }
+            // ---- keep the ring ahead of the batch front
+            {
+                const int target = min(front + in.sh + kAhead, endX + 256);
+                for (int r = 0; r < 4 && R.fill < target; r++) { R.refill(in.r, lane); LZ_STAT(12, 1); }
+            }
+            wait_vm();
+            wave_lds_fence();
+
+            const uint32_t cw = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)cX & 3u);
+            bool ok = valid && cw == pw;
+            if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)pos);
+            const uint64_t hits = ballot(ok);
+            const int fh = ffs64(hits), fi = ffs64(~vmask);
+            const bool found = hits != 0;
+            const int L = found ? fh : fi - 1;
+            if (!dup) {
+                if (valid && lane > L) T.put(h, old);
+            } else if (valid && lane <= L) {
+                const uint64_t upto = (L >= 63) ? ~0ull : ((2ull << L) - 1ull);
+                const uint64_t later = grp & ~((2ull << lane) - 1ull) & upto;
+                if (!later) T.put(h, (uint32_t)pos);
+            }
+            if (!found) {
+                wave_lds_fence();
+                if (~vmask) break;
+                if (retest) { retest = false; s = ip + 1; k0 = LZH_WAVE - 1; }
+                else k0 += LZH_WAVE;
+                continue;
+            }
+            // ---- park the hit lane's candidate window in LDS (byte i = descriptor cA_hit + i)
+            if (lane == fh) {
+                volatile LDSA uint32_t* sw = specw;
+                sw[0] = d0; sw[1] = d1; sw[2] = d2; sw[3] = d3; sw[4] = d4; sw[5] = d5;
+            }
+            wave_lds_fence();
+            int P = rdlanei(pos, fh);
+            int M = rdlanei((int)cand, fh);
+            LZ_STAT(3, 1);
+            LZ_STAT(4, fh);
+            const int sbase = ((M + in.sh) & 3) + 4;          // spec index of byte M
+            auto spec = [&](int idx) -> uint32_t { return ((volatile const LDSA uint8_t*)specw)[idx & 31]; };
+
+            // ---- catch-up: lanes 0..3 compare P-1-j with M-1-j
+            int bk;
+            {
+                const int maxb = min(P - anchor, M);
+                const int lim = min(maxb, 4);
+                const bool rb = R.has(P - 4, P);
+                const uint32_t pb = lane < lim ? (rb ? R.byte(P - 1 - lane) : in.b(P - 1 - lane)) : 0u;
+                const bool eq = lane < lim && pb == spec(sbase - 1 - lane);
+                bk = ffs64(ballot(!eq));
+                if (bk > lim) bk = lim;
+                if (bk == 4 && maxb > 4) {
+                    LZ_STAT(5, 1);
+                    int ip2 = P - 4, m2 = M - 4;
+                    for (int it = 0; it < (1 << 12); it++) {
+                        const int mb2 = min(ip2 - anchor, m2);
+                        if (mb2 <= 0) break;
+                        const bool e2 = lane < mb2 && in.b(ip2 - 1 - lane) == in.b(m2 - 1 - lane);
+                        const int b = ffs64(ballot(!e2));
+                        ip2 -= b;
+                        m2 -= b;
+                        if (b < LZH_WAVE) break;
+                    }
+                    bk = P - ip2;
+                }
+            }
+            P -= bk;
+            M -= bk;
+            const int lit = P - anchor;
+            const int offset = P - M;
+
+            // ---- match length LZ4_count(P+4, M+4, matchlimit): 12 bytes from the windows
+            const int a = P + kMinMatch;
+            int len;
+            {
+                const bool fast = bk <= 4;
+                const bool rf = R.has(a, a + 12);
+                const int si = sbase + 4 - bk + lane;           // spec index of byte M+4+lane
+                const bool in12 = lane < 12;
+                const uint32_t pb = (fast && in12) ? (rf ? R.byte(a + lane) : in.b(a + lane)) : 0u;
+                const bool eq = fast && in12 && si < 24 && pb == spec(si);
+                len = ffs64(ballot(!eq));
+                if (len >= 12 || !fast) {
+                    LZ_STAT(6, 1);
+                    len = fast ? 12 : 0;
+                    for (int it = 0; it < (1 << 10) && a + len < mlimit; it++) {
+                        const int o = len + 4 * lane;
+                        const uint32_t x = in.w32(a + o) ^ in.w32(M + kMinMatch + o);
+                        const uint64_t ne = ballot(x != 0);
+                        if (ne) {
+                            const int l = ffs64(ne);
+                            len += 4 * l + (__builtin_ctz(rdlane(x, l)) >> 3);
+                            break;
+                        }
+                        len += 4 * LZH_WAVE;
+                    }
+                }
+            }
+            const int ml = min(len, mlimit - a);
+
+            LZ_STAT(7, bk > 0 ? 1 : 0);
+            LZ_STAT(10, lit);
+            LZ_STAT(11, ml);
+            LZ_STAT(8, R.has(anchor, anchor + lit) ? 0 : 1);
+            pend = true;
+            p_anchor = anchor; p_lit = lit; p_off = offset; p_ml = ml;
+
+            ip = a + ml;
+            anchor = ip;
+            if (ip >= mfl1) break;
+            {   // fill table at ip-2; the re-test of ip is lane 0 of the next batch
+                uint32_t w, bb = 0;
+                if (R.has(ip - 6, ip + 8)) { w = R.u32(ip - 2); if (!kSmall) bb = R.byte(ip + 2); }
+                else { const uint64_t v = in.w40(ip - 2); w = (uint32_t)v; bb = (uint32_t)(v >> 32); }
+                const uint32_t hm2 = hash_of<kSmall>(w, bb);
+                if (lane == 0) T.put(hm2, (uint32_t)(ip - 2));
+                wave_lds_fence();
+            }
+            retest = true;
+            s = ip + 1;
+            k0 = 0;
+        }
+    }
+    if (pend) op = emit_seq(in, R, out, op, p_anchor, p_lit, true, p_off, p_ml, lane);
+    op = emit_seq(in, R, out, op, anchor, n - anchor, false, 0, 0, lane);
+    if (lane == 0) *out_size = (uint32_t)op;
+}
+
+}  // namespace lz4v3
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
+                           uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t chunk0,
+                           unsigned long long* stats) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + 256 + 8];
+    const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
+    const uint64_t off = chunk * chunk_size;
+    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
+    const int n = (int)min(chunk_size, n_total - off);
+    const uint64_t readable = min<uint64_t>(in_readable - off, (uint64_t)n + 64);
+    Bytes rin, rout;
+    rin.init(in + off, readable);
+    rout.init(stage + chunk * stride, stride);
+    if (n < 65547) lz4v3::compress_chunk<true>(rin, n, rout, acc, (LDSA uint32_t*)lds, (LDSA uint32_t*)lds + 4096, (LDSA uint32_t*)lds + 4096 + 256, csizes + chunk, stats);
+    else lz4v3::compress_chunk<false>(rin, n, rout, acc, (LDSA uint32_t*)lds, (LDSA uint32_t*)lds + 4096, (LDSA uint32_t*)lds + 4096 + 256, csizes + chunk, stats);
+}
+
+#include "launch.h"
+hipError_t lzh_launch_lz4_compress_v2(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                                      int acc, uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
+                                      hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(lzh_lz4_compress_v2_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable,
+                       chunk_size, acc, stage, stride, csizes, 0u, (unsigned long long*)nullptr);
+    return hipGetLastError();
+}
+
+// debug: run the v2 kernel with event counters (16 x u64 device buffer)
+extern "C" int lzh_debug_lz4_stats(const void* d_in, uint64_t n, uint64_t in_readable, uint64_t chunk_size, int acc,
+                                   void* d_stage, uint32_t* d_csizes, unsigned long long* d_stats, void* stream) {
+    const uint64_t k = (n + chunk_size - 1) / chunk_size;
+    const uint64_t stride = ((chunk_size + chunk_size / 255 + 16 + 16) + 255) / 256 * 256;
+    hipLaunchKernelGGL(lzh_lz4_compress_v2_kernel, dim3((unsigned)k), dim3(64), 0, (hipStream_t)stream,
+                       (const uint8_t*)d_in, n, in_readable, chunk_size, acc, (uint8_t*)d_stage, stride, d_csizes, 0u,
+                       d_stats);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -15,9 +15,9 @@
 namespace {
 
 struct SnTable {
-    uint16_t* t;
-    __device__ __forceinline__ uint32_t get(uint32_t h) const { return ((volatile const uint16_t*)t)[h]; }
-    __device__ __forceinline__ void put(uint32_t h, uint32_t v) const { ((volatile uint16_t*)t)[h] = (uint16_t)v; }
+    LDSA uint16_t* t;
+    __device__ __forceinline__ uint32_t get(uint32_t h) const { return ((volatile const LDSA uint16_t*)t)[h]; }
+    __device__ __forceinline__ void put(uint32_t h, uint32_t v) const { ((volatile LDSA uint16_t*)t)[h] = (uint16_t)v; }
 };
 
 __device__ __forceinline__ int log2floor_u(uint32_t v) { return 31 - __builtin_clz(v); }
@@ -93,15 +93,15 @@ __device__ __forceinline__ int emit_copy(const Bytes& out, int op, uint32_t off,
 }
 
 // CompressFragment over in[0..fn) (in is the fragment's own descriptor); writes at op.
-__device__ int sn_compress_fragment(const Bytes& in, int fn, const Bytes& out, int op, uint16_t* lds) {
+__device__ int sn_compress_fragment(const Bytes& in, int fn, const Bytes& out, int op, LDSA uint16_t* lds) {
     const int lane = threadIdx.x;
     SnTable T{lds};
     const uint32_t tsize = sn_table_size((uint32_t)fn);
     const int shift = 32 - log2floor_u(tsize);
     {
-        uint4* t4 = (uint4*)lds;
+        LDSA uint32_t* t4 = (LDSA uint32_t*)lds;
         const int nvec = (int)(tsize * 2 / 16);
-        for (int i = lane; i < nvec; i += LZH_WAVE) t4[i] = make_uint4(0, 0, 0, 0);
+        for (int i = lane; i < nvec; i += LZH_WAVE) lds_zero16(t4 + 4 * i);
         wave_lds_fence();
     }
     int next_emit = 0;
@@ -271,7 +271,7 @@ lzh_snappy_compress_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_read
         const uint64_t readable = min<uint64_t>(in_readable - off - fpos, (uint64_t)fn + 64);
         Bytes rin;
         rin.init(in + off + fpos, readable);
-        op = sn_compress_fragment(rin, fn, rout, op, lds);
+        op = sn_compress_fragment(rin, fn, rout, op, (LDSA uint16_t*)lds);
     }
     if (lane == 0) csizes[chunk] = (uint32_t)op;
 }

@@ -1,0 +1,23 @@
+"""tools/lz4_stats.py -- event counters of the LZ4 compress kernel (debug launch)."""
+import ctypes as C, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch, lzbench_amd as L
+lib = L.lib()
+f = lib.lzh_debug_lz4_stats
+f.restype = C.c_int
+f.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+names = ["batches", "dup_batches", "fast_plan", "found", "sum_fh", "catchup_slow", "count_slow", "bk>0",
+         "lit_not_in_ring", "hash_ring_miss", "sum_lit", "sum_ml", "refills", "-", "-", "-"]
+for corpus in sys.argv[1:] or ["text", "json"]:
+    n = 64 << 20
+    host = L.datagen(corpus, n, seed=12345)
+    d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda"); d_in[:n].copy_(torch.from_numpy(host))
+    dc = L.DeviceCodec("lz4", n, 65536)
+    st = torch.zeros(16, dtype=torch.int64, device="cuda")
+    assert f(d_in.data_ptr(), n, d_in.numel(), 65536, 1, dc.ctemp.data_ptr(), dc.csizes.data_ptr(), st.data_ptr(),
+             torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    v = st.cpu().tolist()
+    k = n // 65536
+    print(corpus, {names[i]: round(v[i] / k, 2) for i in range(13)}, "per chunk")
