@@ -46,10 +46,32 @@ struct Win {
         const uint32_t v = d < 64 ? rdlane(w0, d) : rdlane(w1, d - 64);
         return (v >> (8 * (x & 3))) & 0xffu;
     }
+    __device__ __forceinline__ bool covers(int p0, int p1) const { return p0 + sh >= wb && p1 + sh <= wb + 512; }
+    // per-lane byte at stream position pos (inside the window) via cross-lane permute
+    __device__ __forceinline__ uint32_t lane_byte(int pos) const {
+        const int x = pos + sh;
+        const int d = (x - wb) >> 2;
+        const uint32_t a = lane_gather(w0, d & 63), b = lane_gather(w1, d & 63);
+        return ((d < 64 ? a : b) >> (8 * (x & 3))) & 0xffu;
+    }
 };
 
 __device__ __forceinline__ void copy_in_out(const Bytes& in, int src, const Bytes& out, int dst, int len, int lane) {
     copy_span(in, src, out, dst, len, lane, LZH_WAVE);
+}
+
+// literal run in[src, src+len) -> out[dst..]: straight from the register window when it holds
+// the run (no memory round trip), else through memory
+__device__ __forceinline__ void copy_lit(const Win& w, const Bytes& in, int src, const Bytes& out, int dst, int len,
+                                         int lane) {
+    if (len <= 2 * LZH_WAVE && w.covers(src, src + len)) {
+        for (int base = 0; base < len; base += LZH_WAVE) {
+            const uint32_t v = w.lane_byte(src + base + lane);
+            if (base + lane < len) out.st8(dst + base + lane, v);
+        }
+        return;
+    }
+    copy_in_out(in, src, out, dst, len, lane);
 }
 
 // out[op + t] = out[op - off + (t mod off)] for t < len; all sources precede op
@@ -94,11 +116,11 @@ __device__ int lz4_decode(const Bytes& in, int cs, const Bytes& out, int cap, in
         }
         if (op + lit > cap - 12 || ip + lit > cs - 8) {
             if (ip + lit != cs || op + lit > cap) return -ip - 1;
-            copy_in_out(in, ip, out, op, lit, lane);
+            copy_lit(w, in, ip, out, op, lit, lane);
             op += lit;
             break;
         }
-        copy_in_out(in, ip, out, op, lit, lane);
+        copy_lit(w, in, ip, out, op, lit, lane);
         ip += lit;
         op += lit;
         w.ensure(ip, lane);
@@ -160,7 +182,7 @@ __device__ int snappy_decode(const Bytes& in, int cs, const Bytes& out, int cap,
                 ip += nb;
             }
             if ((int64_t)ip + len > cs || (int64_t)op + len > ul) return -1;
-            copy_in_out(in, ip, out, op, len, lane);
+            copy_lit(w, in, ip, out, op, len, lane);
             ip += len;
             op += len;
         } else {

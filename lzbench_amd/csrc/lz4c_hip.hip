@@ -123,9 +123,23 @@ __device__ __forceinline__ int emit_seq(const Bytes& in, const Ring& R, const By
     return op + total;
 }
 
+// M-side byte of the hit lane's window: spec index si (0..23) of the six uniform dwords
+__device__ __forceinline__ uint32_t spec_byte(int si, uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t e4,
+                                              uint32_t e5) {
+    const int q = si >> 2;
+    uint32_t v = e0;
+    v = q == 1 ? e1 : v;
+    v = q == 2 ? e2 : v;
+    v = q == 3 ? e3 : v;
+    v = q == 4 ? e4 : v;
+    v = q == 5 ? e5 : v;
+    return (v >> (8 * (si & 3))) & 0xffu;
+}
+
 template <bool kSmall>
 __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab, LDSA uint32_t* ringw,
                                LDSA uint32_t* specw, uint32_t* out_size, unsigned long long* stats) {
+    (void)specw;
     const int lane = threadIdx.x;
     Table<kSmall> T{tab};
     if (n <= 0) {
@@ -163,14 +177,17 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         bool retest = false;
 
         for (int guard = 0; guard < 4 * n + 64; guard++) {
-            // ---- probe plan: lane -> position p, validity (forwardIp <= mflimitPlusOne)
+            // ---- probe plan: lane -> position, validity (forwardIp <= mflimitPlusOne)
+            const bool fast = acc == 1 && k0 == 0;
+            // in a fast re-test batch lane 63 carries the ip-2 table fill (lz4.c:1146) instead of
+            // a probe; it is written before any probe reads the table
+            const bool ins63 = fast && retest;
             int p;
             bool valid;
-            if (acc == 1 && k0 == 0) {
-                // retest: lane 0 = ip, lanes j>=1 = search from ip+1 probe j-1 (step 1) -> ip + j;
-                // fresh search: s + j.  Either way base + lane with step 1.
-                p = (retest ? ip : s) + lane;
+            if (fast) {
+                p = (retest ? ip : s) + lane;            // re-test ip, then search ip+1.. step 1
                 valid = p + 1 <= mfl1;
+                if (ins63 && lane == 63) { p = ip - 2; valid = false; }
             } else {
                 int64_t pp, nxt;
                 if (retest && lane == 0) {
@@ -186,62 +203,41 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 valid = nxt <= mfl1;
                 p = valid ? (int)pp : 0;
             }
-            const int pos = valid ? p : 0;
             const uint64_t vmask = ballot(valid);
+            const int front = ins63 ? ip - 2 : rdlanei(p, 0);
+            const int pmax = vmask ? rdlanei(p, 63 - __builtin_clzll(vmask)) : front;
             LZ_STAT(0, 1);
-            LZ_STAT(2, (acc == 1 && k0 == 0) ? 1 : 0);
-            const int front = rdlanei(pos, 0);
-            const int pmax = vmask ? rdlanei(pos, 63 - __builtin_clzll(vmask)) : front;
+            LZ_STAT(2, fast ? 1 : 0);
 
-            // ---- hash probe positions (ring when it covers the batch)
+            // ---- hash (ring when it covers the batch)
             uint32_t pw, b4 = 0;
-            if (vmask && R.has(front - 4, pmax + hb + 8)) {
-                pw = R.u32(pos);
-                if (!kSmall) b4 = R.byte(pos + 4);
+            if (R.has(front - 4, pmax + hb + 8)) {
+                pw = R.u32(p);
+                if (!kSmall) b4 = R.byte(p + 4);
             } else if (kSmall) {
                 LZ_STAT(9, 1);
-                pw = in.w32(pos);
+                pw = in.w32(p);
             } else {
-                const uint64_t v = in.w40(pos);
+                const uint64_t v = in.w40(p);
                 pw = (uint32_t)v;
                 b4 = (uint32_t)(v >> 32);
             }
             const uint32_t h = hash_of<kSmall>(pw, b4);
+            if (ins63 && lane == 63) T.put(h, (uint32_t)(ip - 2));
+            else if (retest && !fast) {   // general plan: the ip-2 fill happened before the batch
+            }
             const uint32_t old = T.get(h);
-            if (valid) T.put(h, (uint32_t)pos);
+            if (valid) T.put(h, (uint32_t)p);
             wave_lds_fence();
             const uint32_t back = T.get(h);
-            const uint64_t dup = ballot(valid && back != (uint32_t)pos);
+            // lanes whose table write lost to another lane of the batch (same slot)
+            const uint64_t losers = ballot(valid && back != (uint32_t)p);
             uint32_t cand = old;
-            uint64_t grp = 1ull << lane;
-            if (dup) {
-                LZ_STAT(1, 1);
-                // exact in-batch collision resolution (rare)
-                wave_lds_fence();
-                if (valid) T.put(h, old);
-                wave_lds_fence();
-                uint64_t pending = dup;
-                int prev = -1;
-                for (int it = 0; it < LZH_WAVE && pending; it++) {
-                    const int l = ffs64(pending);
-                    const uint32_t hv = rdlane(h, l);
-                    const bool mine = valid && h == hv;
-                    const uint64_t m = ballot(mine);
-                    pending &= ~m;
-                    if (mine) {
-                        grp = m;
-                        const uint64_t below = m & ((1ull << lane) - 1ull);
-                        if (below) prev = 63 - __builtin_clzll(below);
-                    }
-                }
-                const uint32_t ppos = lane_gather((uint32_t)pos, prev < 0 ? lane : prev);
-                if (prev >= 0) cand = ppos;
-            }
-            // ---- speculative candidate window [cand-4, cand+20): one dwordx4 + one dwordx2
-            const int cX = (valid ? (int)cand : 0) + in.sh;
-            const int cA = (cX & ~3) - 4;
-            const uint32_t d0 = ld_b32(in.r, cA), d1 = ld_b32(in.r, cA + 4), d2 = ld_b32(in.r, cA + 8),
-                           d3 = ld_b32(in.r, cA + 12), d4 = ld_b32(in.r, cA + 16), d5 = ld_b32(in.r, cA + 20);
+            // ---- speculative candidate window [cand-4, cand+20)
+            int cX = (valid ? (int)cand : 0) + in.sh;
+            int cA = (cX & ~3) - 4;
+            uint32_t d0 = ld_b32(in.r, cA), d1 = ld_b32(in.r, cA + 4), d2 = ld_b32(in.r, cA + 8),
+                     d3 = ld_b32(in.r, cA + 12), d4 = ld_b32(in.r, cA + 16), d5 = ld_b32(in.r, cA + 20);
             // ---- deferred emission of the previous sequence (stores overlap the loads above)
             if (pend) {
                 op = emit_seq(in, R, out, op, p_anchor, p_lit, true, p_off, p_ml, lane);
@@ -255,110 +251,153 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             wait_vm();
             wave_lds_fence();
 
-            const uint32_t cw = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)cX & 3u);
-            bool ok = valid && cw == pw;
-            if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)pos);
-            const uint64_t hits = ballot(ok);
-            const int fh = ffs64(hits), fi = ffs64(~vmask);
-            const bool found = hits != 0;
-            const int L = found ? fh : fi - 1;
-            if (!dup) {
-                if (valid && lane > L) T.put(h, old);
-            } else if (valid && lane <= L) {
-                const uint64_t upto = (L >= 63) ? ~0ull : ((2ull << L) - 1ull);
-                const uint64_t later = grp & ~((2ull << lane) - 1ull) & upto;
-                if (!later) T.put(h, (uint32_t)pos);
+            bool ok = valid && __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)cX & 3u) == pw;
+            if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
+            uint64_t hits = ballot(ok);
+            const int fi = ffs64(~vmask);
+            int fh = ffs64(hits);
+            bool found = hits != 0;
+            int L = found ? fh : fi - 1;
+            uint64_t upto = L < 0 ? 0ull : (L >= 63 ? ~0ull : ((2ull << L) - 1ull));
+            // exact resolution is needed only if two lanes <= L share a slot; any such pair has
+            // a loser <= L, and for small L the pair test is a few cross-lane compares
+            bool exact = false;
+            if (losers & upto) {
+                if (L <= 7) {
+                    bool pr = false;
+#pragma unroll
+                    for (int d = 1; d <= 7; d++) {
+                        const uint32_t hv = lane_gather(h, lane >= d ? lane - d : lane);
+                        pr = pr || (d <= lane && lane <= L && hv == h);
+                    }
+                    exact = ballot(pr) != 0;
+                } else {
+                    exact = true;
+                }
+            }
+            if (!exact) {
+                // keep writes of lanes <= L: winners above L restore, then lanes <= L re-assert
+                if (valid && lane > L && back == (uint32_t)p) T.put(h, old);
+                if (losers & upto) {
+                    wave_lds_fence();
+                    if (lane <= L) T.put(h, (uint32_t)p);
+                }
+            } else {
+                LZ_STAT(1, 1);
+                if (valid) T.put(h, old);
+                wave_lds_fence();
+                uint64_t pending = losers;
+                uint64_t grp = 1ull << lane;
+                int prev = -1;
+                for (int it = 0; it < LZH_WAVE && pending; it++) {
+                    const int l = ffs64(pending);
+                    const uint32_t hv = rdlane(h, l);
+                    const bool mine = valid && h == hv;
+                    const uint64_t m = ballot(mine);
+                    pending &= ~m;
+                    if (mine) {
+                        grp = m;
+                        const uint64_t below = m & ((1ull << lane) - 1ull);
+                        if (below) prev = 63 - __builtin_clzll(below);
+                    }
+                }
+                const uint32_t ppos = lane_gather((uint32_t)p, prev < 0 ? lane : prev);
+                if (prev >= 0) cand = ppos;
+                cX = (valid ? (int)cand : 0) + in.sh;
+                cA = (cX & ~3) - 4;
+                d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
+                d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
+                ok = valid && __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)cX & 3u) == pw;
+                if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
+                hits = ballot(ok);
+                fh = ffs64(hits);
+                found = hits != 0;
+                L = found ? fh : fi - 1;
+                upto = L < 0 ? 0ull : (L >= 63 ? ~0ull : ((2ull << L) - 1ull));
+                if (valid && lane <= L) {
+                    const uint64_t later = grp & ~((2ull << lane) - 1ull) & upto;
+                    if (!later) T.put(h, (uint32_t)p);
+                }
             }
             if (!found) {
                 wave_lds_fence();
-                if (~vmask) break;
-                if (retest) { retest = false; s = ip + 1; k0 = LZH_WAVE - 1; }
+                if (~vmask & ~(ins63 ? (1ull << 63) : 0ull)) break;     // ran past mflimit
+                if (retest) { retest = false; s = ip + 1; k0 = ins63 ? LZH_WAVE - 2 : LZH_WAVE - 1; }
                 else k0 += LZH_WAVE;
                 continue;
             }
-            // ---- park the hit lane's candidate window in LDS (byte i = descriptor cA_hit + i)
-            if (lane == fh) {
-                volatile LDSA uint32_t* sw = specw;
-                sw[0] = d0; sw[1] = d1; sw[2] = d2; sw[3] = d3; sw[4] = d4; sw[5] = d5;
-            }
             wave_lds_fence();
-            int P = rdlanei(pos, fh);
-            int M = rdlanei((int)cand, fh);
+
+            // ---- hit at P with candidate M; one lane-parallel compare answers catch-up
+            // (lanes 0..3: P-1-j vs M-1-j, lz4.c:1019) and the match length from P+4 (lanes 4..:
+            // P+4+k vs M+4+k, LZ4_count lz4.c:603-626).  Catch-up back bk moves both starts but
+            // not the match end: count(P-bk+4) = bk + count(P+4).
+            const int P = rdlanei(p, fh);
+            const int M = rdlanei((int)cand, fh);
+            const uint32_t e0 = rdlane(d0, fh), e1 = rdlane(d1, fh), e2 = rdlane(d2, fh), e3 = rdlane(d3, fh),
+                           e4 = rdlane(d4, fh), e5 = rdlane(d5, fh);
             LZ_STAT(3, 1);
             LZ_STAT(4, fh);
-            const int sbase = ((M + in.sh) & 3) + 4;          // spec index of byte M
-            auto spec = [&](int idx) -> uint32_t { return ((volatile const LDSA uint8_t*)specw)[idx & 31]; };
-
-            // ---- catch-up: lanes 0..3 compare P-1-j with M-1-j
-            int bk;
-            {
-                const int maxb = min(P - anchor, M);
-                const int lim = min(maxb, 4);
-                const bool rb = R.has(P - 4, P);
-                const uint32_t pb = lane < lim ? (rb ? R.byte(P - 1 - lane) : in.b(P - 1 - lane)) : 0u;
-                const bool eq = lane < lim && pb == spec(sbase - 1 - lane);
-                bk = ffs64(ballot(!eq));
-                if (bk > lim) bk = lim;
-                if (bk == 4 && maxb > 4) {
-                    LZ_STAT(5, 1);
-                    int ip2 = P - 4, m2 = M - 4;
-                    for (int it = 0; it < (1 << 12); it++) {
-                        const int mb2 = min(ip2 - anchor, m2);
-                        if (mb2 <= 0) break;
-                        const bool e2 = lane < mb2 && in.b(ip2 - 1 - lane) == in.b(m2 - 1 - lane);
-                        const int b = ffs64(ballot(!e2));
-                        ip2 -= b;
-                        m2 -= b;
-                        if (b < LZH_WAVE) break;
+            const int sbase = ((M + in.sh) & 3) + 4;           // window index of byte M
+            const int kmax = 20 - sbase;                        // count bytes the window holds (13..16)
+            const int maxb = min(P - anchor, M);
+            const int blim = min(maxb, 4);
+            int qpos, si;
+            bool act;
+            if (lane < 4) { qpos = P - 1 - lane; si = sbase - 1 - lane; act = lane < blim; }
+            else { const int k = lane - 4; qpos = P + 4 + k; si = sbase + 4 + k; act = k < kmax; }
+            const bool rok = R.has(P - 4, P + 4 + 16);
+            uint32_t pb = 0;
+            if (rok) pb = R.byte(qpos);
+            else if (act) pb = in.b(qpos);
+            const bool eq = act && pb == spec_byte(si & 31, e0, e1, e2, e3, e4, e5);
+            const uint64_t em = ballot(eq);
+            int bk = ffs64(~em & 0xfull);
+            if (bk > blim) bk = blim;
+            int cnt = ffs64((~(em >> 4) & ((1ull << kmax) - 1ull)) | (1ull << kmax));
+            if (bk == 4 && maxb > 4) {
+                LZ_STAT(5, 1);
+                int ip2 = P - 4, m2 = M - 4;
+                for (int it = 0; it < (1 << 12); it++) {
+                    const int mb2 = min(ip2 - anchor, m2);
+                    if (mb2 <= 0) break;
+                    const bool e2b = lane < mb2 && in.b(ip2 - 1 - lane) == in.b(m2 - 1 - lane);
+                    const int b = ffs64(ballot(!e2b));
+                    ip2 -= b;
+                    m2 -= b;
+                    if (b < LZH_WAVE) break;
+                }
+                bk = P - ip2;
+            }
+            const int a = P + kMinMatch;                        // count start before catch-up
+            if (cnt >= kmax && a + cnt < mlimit) {
+                LZ_STAT(6, 1);
+                for (int it = 0; it < (1 << 10) && a + cnt < mlimit; it++) {
+                    const int o = cnt + 4 * lane;
+                    const uint32_t x = in.w32(a + o) ^ in.w32(M + kMinMatch + o);
+                    const uint64_t ne = ballot(x != 0);
+                    if (ne) {
+                        const int l = ffs64(ne);
+                        cnt += 4 * l + (__builtin_ctz(rdlane(x, l)) >> 3);
+                        break;
                     }
-                    bk = P - ip2;
+                    cnt += 4 * LZH_WAVE;
                 }
             }
-            P -= bk;
-            M -= bk;
-            const int lit = P - anchor;
-            const int offset = P - M;
-
-            // ---- match length LZ4_count(P+4, M+4, matchlimit): 12 bytes from the windows
-            const int a = P + kMinMatch;
-            int len;
-            {
-                const bool fast = bk <= 4;
-                const bool rf = R.has(a, a + 12);
-                const int si = sbase + 4 - bk + lane;           // spec index of byte M+4+lane
-                const bool in12 = lane < 12;
-                const uint32_t pb = (fast && in12) ? (rf ? R.byte(a + lane) : in.b(a + lane)) : 0u;
-                const bool eq = fast && in12 && si < 24 && pb == spec(si);
-                len = ffs64(ballot(!eq));
-                if (len >= 12 || !fast) {
-                    LZ_STAT(6, 1);
-                    len = fast ? 12 : 0;
-                    for (int it = 0; it < (1 << 10) && a + len < mlimit; it++) {
-                        const int o = len + 4 * lane;
-                        const uint32_t x = in.w32(a + o) ^ in.w32(M + kMinMatch + o);
-                        const uint64_t ne = ballot(x != 0);
-                        if (ne) {
-                            const int l = ffs64(ne);
-                            len += 4 * l + (__builtin_ctz(rdlane(x, l)) >> 3);
-                            break;
-                        }
-                        len += 4 * LZH_WAVE;
-                    }
-                }
-            }
-            const int ml = min(len, mlimit - a);
-
+            cnt = min(cnt, mlimit - a);
+            const int P2 = P - bk;
+            const int lit = P2 - anchor;
+            const int ml = bk + cnt;
             LZ_STAT(7, bk > 0 ? 1 : 0);
             LZ_STAT(10, lit);
             LZ_STAT(11, ml);
-            LZ_STAT(8, R.has(anchor, anchor + lit) ? 0 : 1);
             pend = true;
-            p_anchor = anchor; p_lit = lit; p_off = offset; p_ml = ml;
+            p_anchor = anchor; p_lit = lit; p_off = P - M; p_ml = ml;
 
-            ip = a + ml;
+            ip = a + cnt;                                       // = P2 + 4 + ml
             anchor = ip;
             if (ip >= mfl1) break;
-            {   // fill table at ip-2; the re-test of ip is lane 0 of the next batch
+            if (acc != 1) {   // general plan: fill table at ip-2 now (fast plan: lane 63 next batch)
                 uint32_t w, bb = 0;
                 if (R.has(ip - 6, ip + 8)) { w = R.u32(ip - 2); if (!kSmall) bb = R.byte(ip + 2); }
                 else { const uint64_t v = in.w40(ip - 2); w = (uint32_t)v; bb = (uint32_t)(v >> 32); }
