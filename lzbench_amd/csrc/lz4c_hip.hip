@@ -29,6 +29,7 @@ constexpr int kLastLiterals = 5;
 constexpr int kMinLength = 13;
 constexpr int kRing = 1024;           // bytes of LDS input ring per wave
 constexpr int kAhead = 704;           // keep the ring filled this far past the batch front
+constexpr int kRT = 16;               // probe lanes of a re-test batch
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -182,12 +183,16 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             // in a fast re-test batch lane 63 carries the ip-2 table fill (lz4.c:1146) instead of
             // a probe; it is written before any probe reads the table
             const bool ins63 = fast && retest;
+            // a re-test batch probes only kRT lanes: the first hit after a match is almost always
+            // within a few positions, and idle lanes issue no candidate loads
             int p;
-            bool valid;
+            bool valid, term;
             if (fast) {
                 p = (retest ? ip : s) + lane;            // re-test ip, then search ip+1.. step 1
-                valid = p + 1 <= mfl1;
-                if (ins63 && lane == 63) { p = ip - 2; valid = false; }
+                const bool act = !retest || lane < kRT;
+                valid = act && p + 1 <= mfl1;
+                term = act && p + 1 > mfl1;
+                if (ins63 && lane == 63) { p = ip - 2; valid = false; term = false; }
             } else {
                 int64_t pp, nxt;
                 if (retest && lane == 0) {
@@ -201,9 +206,11 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     nxt = pp + st;
                 }
                 valid = nxt <= mfl1;
+                term = !valid;
                 p = valid ? (int)pp : 0;
             }
             const uint64_t vmask = ballot(valid);
+            const uint64_t tmask = ballot(term);
             const int front = ins63 ? ip - 2 : rdlanei(p, 0);
             const int pmax = vmask ? rdlanei(p, 63 - __builtin_clzll(vmask)) : front;
             LZ_STAT(0, 1);
@@ -236,8 +243,11 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             // ---- speculative candidate window [cand-4, cand+20)
             int cX = (valid ? (int)cand : 0) + in.sh;
             int cA = (cX & ~3) - 4;
-            uint32_t d0 = ld_b32(in.r, cA), d1 = ld_b32(in.r, cA + 4), d2 = ld_b32(in.r, cA + 8),
-                     d3 = ld_b32(in.r, cA + 12), d4 = ld_b32(in.r, cA + 16), d5 = ld_b32(in.r, cA + 20);
+            uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0, d5 = 0;
+            if (valid) {
+                d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
+                d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
+            }
             // ---- deferred emission of the previous sequence (stores overlap the loads above)
             if (pend) {
                 op = emit_seq(in, R, out, op, p_anchor, p_lit, true, p_off, p_ml, lane);
@@ -254,7 +264,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             bool ok = valid && __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)cX & 3u) == pw;
             if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
             uint64_t hits = ballot(ok);
-            const int fi = ffs64(~vmask);
+            const int fi = ffs64(tmask);
             int fh = ffs64(hits);
             bool found = hits != 0;
             int L = found ? fh : fi - 1;
@@ -305,8 +315,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 if (prev >= 0) cand = ppos;
                 cX = (valid ? (int)cand : 0) + in.sh;
                 cA = (cX & ~3) - 4;
-                d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
-                d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
+                if (valid) {
+                    d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
+                    d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
+                }
                 ok = valid && __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)cX & 3u) == pw;
                 if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
                 hits = ballot(ok);
@@ -321,8 +333,8 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             }
             if (!found) {
                 wave_lds_fence();
-                if (~vmask & ~(ins63 ? (1ull << 63) : 0ull)) break;     // ran past mflimit
-                if (retest) { retest = false; s = ip + 1; k0 = ins63 ? LZH_WAVE - 2 : LZH_WAVE - 1; }
+                if (tmask) break;                                      // ran past mflimit
+                if (retest) { retest = false; s = ip + 1; k0 = fast ? kRT - 1 : LZH_WAVE - 1; }
                 else k0 += LZH_WAVE;
                 continue;
             }
