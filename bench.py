@@ -69,6 +69,13 @@ def cpu_baseline(sample: np.ndarray, codec: str, chunk: int, level: int, iters: 
     }, packed, cs
 
 
+def kernel_name(codec):
+    """Compressor kernel the C-ABI launches for `codec` (api.cpp lzh_compress_kernel_only)."""
+    if codec == "snappy":
+        return "lzh_snappy_compress_kernel" if os.environ.get("LZH_SNAPPY_V1", "0") != "0" else "lzh_snappy_compress_v2_kernel"
+    return "lzh_lz4_compress_kernel" if os.environ.get("LZH_LZ4_V1", "0") != "0" else "lzh_lz4_compress_v2_kernel"
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -199,7 +206,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": None,
-            "kernel": "lzh_lz4_compress_kernel" if args.codec != "snappy" else "lzh_snappy_compress_kernel",
+            "kernel": kernel_name(args.codec),
             "kernel_ms": round(k_ms, 3),
             "algorithmic_bytes_per_launch": int(algo_bytes),
         },

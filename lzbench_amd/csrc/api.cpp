@@ -83,8 +83,13 @@ int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, s
             LZH_CHECK(lzh_launch_lz4_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, level < 1 ? 1 : level,
                                                  (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
     } else if (codec == LZH_CODEC_SNAPPY) {
-        LZH_CHECK(lzh_launch_snappy_compress((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
-                                             stride, d_csizes, (uint32_t)k, s));
+        static const bool use_v1 = getenv("LZH_SNAPPY_V1") && atoi(getenv("LZH_SNAPPY_V1")) != 0;
+        if (use_v1)
+            LZH_CHECK(lzh_launch_snappy_compress((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
+                                                 stride, d_csizes, (uint32_t)k, s));
+        else
+            LZH_CHECK(lzh_launch_snappy_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size,
+                                                    (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
     } else {
         return LZH_EARG;
     }

@@ -13,6 +13,9 @@ hipError_t lzh_launch_lz4_compress_v2(const uint8_t* in, uint64_t n_total, uint6
 hipError_t lzh_launch_snappy_compress(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                                       uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
                                       hipStream_t s);
+hipError_t lzh_launch_snappy_compress_v2(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                                         uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
+                                         hipStream_t s);
 hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                  const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                  int32_t* status, uint32_t nchunks, hipStream_t s);

@@ -22,6 +22,8 @@ namespace lz4v3 {
 
 // optional per-kernel event counters (debug builds of the launch only; nullptr in production)
 #define LZ_STAT(i, v) do { if (stats && lane == 0) atomicAdd(&stats[i], (unsigned long long)(v)); } while (0)
+// debug-only phase clock (s_memtime) accumulated per wave
+#define LZ_T(k) do { if (stats) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ph[k] += t_ - tlast; tlast = t_; } } while (0)
 
 constexpr int kMinMatch = 4;
 constexpr int kMfLimit = 12;
@@ -176,8 +178,11 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         }
         int ip = 1, s = 1, k0 = 0;
         bool retest = false;
+        uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+        uint64_t tlast = stats ? __builtin_amdgcn_s_memtime() : 0;
 
         for (int guard = 0; guard < 4 * n + 64; guard++) {
+            LZ_T(5);
             // ---- probe plan: lane -> position, validity (forwardIp <= mflimitPlusOne)
             const bool fast = acc == 1 && k0 == 0;
             // in a fast re-test batch lane 63 carries the ip-2 table fill (lz4.c:1146) instead of
@@ -240,6 +245,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             // lanes whose table write lost to another lane of the batch (same slot)
             const uint64_t losers = ballot(valid && back != (uint32_t)p);
             uint32_t cand = old;
+            LZ_T(0);
             // ---- speculative candidate window [cand-4, cand+20)
             int cX = (valid ? (int)cand : 0) + in.sh;
             int cA = (cX & ~3) - 4;
@@ -258,8 +264,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 const int target = min(front + in.sh + kAhead, endX + 256);
                 for (int r = 0; r < 4 && R.fill < target; r++) { R.refill(in.r, lane); LZ_STAT(12, 1); }
             }
+            LZ_T(1);
             wait_vm();
             wave_lds_fence();
+            LZ_T(2);
 
             bool ok = valid && __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)cX & 3u) == pw;
             if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
@@ -344,6 +352,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             // (lanes 0..3: P-1-j vs M-1-j, lz4.c:1019) and the match length from P+4 (lanes 4..:
             // P+4+k vs M+4+k, LZ4_count lz4.c:603-626).  Catch-up back bk moves both starts but
             // not the match end: count(P-bk+4) = bk + count(P+4).
+            LZ_T(3);
             const int P = rdlanei(p, fh);
             const int M = rdlanei((int)cand, fh);
             const uint32_t e0 = rdlane(d0, fh), e1 = rdlane(d1, fh), e2 = rdlane(d2, fh), e3 = rdlane(d3, fh),
@@ -417,10 +426,12 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 if (lane == 0) T.put(hm2, (uint32_t)(ip - 2));
                 wave_lds_fence();
             }
+            LZ_T(4);
             retest = true;
             s = ip + 1;
             k0 = 0;
         }
+        for (int k = 0; k < 6; k++) LZ_STAT(16 + k, ph[k]);
     }
     if (pend) op = emit_seq(in, R, out, op, p_anchor, p_lit, true, p_off, p_ml, lane);
     op = emit_seq(in, R, out, op, anchor, n - anchor, false, 0, 0, lane);

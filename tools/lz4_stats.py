@@ -14,10 +14,14 @@ for corpus in sys.argv[1:] or ["text", "json"]:
     host = L.datagen(corpus, n, seed=12345)
     d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda"); d_in[:n].copy_(torch.from_numpy(host))
     dc = L.DeviceCodec("lz4", n, 65536)
-    st = torch.zeros(16, dtype=torch.int64, device="cuda")
+    st = torch.zeros(24, dtype=torch.int64, device="cuda")
     assert f(d_in.data_ptr(), n, d_in.numel(), 65536, 1, dc.ctemp.data_ptr(), dc.csizes.data_ptr(), st.data_ptr(),
              torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
     v = st.cpu().tolist()
     k = n // 65536
     print(corpus, {names[i]: round(v[i] / k, 2) for i in range(13)}, "per chunk")
+    ph = v[16:22]
+    tot = sum(ph) or 1
+    print("  phase clocks per batch (s_memtime ticks):", {n_: round(ph[i] / max(v[0], 1), 1) for i, n_ in
+          enumerate(["plan+hash+table", "spec_issue+emit+prefetch", "wait_vm", "hit+commit", "catchup+count+book", "loop_top"])})
