@@ -21,9 +21,7 @@
 namespace lz4v3 {
 
 // optional per-kernel event counters (debug builds of the launch only; nullptr in production)
-#define LZ_STAT(i, v) do { if (stats && lane == 0) atomicAdd(&stats[i], (unsigned long long)(v)); } while (0)
-// debug-only phase clock (s_memtime) accumulated per wave
-#define LZ_T(k) do { if (stats) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ph[k] += t_ - tlast; tlast = t_; } } while (0)
+#define LZ_STAT(i, v) do { if (kStats && lane == 0) atomicAdd(&stats[i], (unsigned long long)(v)); } while (0)
 
 constexpr int kMinMatch = 4;
 constexpr int kMfLimit = 12;
@@ -31,7 +29,7 @@ constexpr int kLastLiterals = 5;
 constexpr int kMinLength = 13;
 constexpr int kRing = 1024;           // bytes of LDS input ring per wave
 constexpr int kAhead = 704;           // keep the ring filled this far past the batch front
-constexpr int kRT = 16;               // probe lanes of a re-test batch
+constexpr int kOut = 512;             // bytes of LDS output ring per wave
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -84,65 +82,262 @@ struct Ring {
 
 __device__ __forceinline__ int ext_len_bytes(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
 
-// Emit one sequence (has_match) or the final literal run at op. Each lane computes its
-// byte of the sequence without branching; literal bytes come from the ring when it holds
-// them. Returns the new op.
-__device__ __forceinline__ int emit_seq(const Bytes& in, const Ring& R, const Bytes& out, int op, int anchor, int lit,
-                                        bool has_match, int off, int ml, int lane) {
-    const int lx = ext_len_bytes(lit);
-    const int mx = has_match ? ext_len_bytes(ml) : 0;
-    const int lit0 = 1 + lx, lit1 = lit0 + lit;            // literal bytes at [lit0, lit1)
-    const int total = lit1 + (has_match ? 2 + mx : 0);
-    const uint32_t token = ((uint32_t)min(lit, 15) << 4) | (has_match ? (uint32_t)min(ml, 15) : 0u);
-    const uint32_t lrem = (uint32_t)((lit - 15) % 255), mrem = (uint32_t)((ml - 15) % 255);
-    const bool lit_in_ring = R.has(anchor, anchor + lit);
-    if (!lit_in_ring && lit > 2 * LZH_WAVE) {
-        // long literal run: header, bulk copy, trailer
-        if (lane == 0) out.st8(op, token);
-        for (int b = lane; b < lx; b += LZH_WAVE) out.st8(op + 1 + b, b == lx - 1 ? lrem : 255u);
-        copy_span(in, anchor, out, op + lit0, lit, lane, LZH_WAVE);
-        if (has_match) {
-            if (lane < 2) out.st8(op + lit1 + lane, lane ? ((uint32_t)off >> 8) : ((uint32_t)off & 0xffu));
-            for (int b = lane; b < mx; b += LZH_WAVE) out.st8(op + lit1 + 2 + b, b == mx - 1 ? mrem : 255u);
-        }
-        return op + total;
+// LDS output ring (kOut bytes) indexed by the output descriptor offset X = pos + sh, so ring
+// dwords line up with global dwords: sequences are assembled here with ds_write_b8 and leave
+// for HBM as aligned dword stores once 256 bytes are pending (no store in the batch's vmcnt
+// wait; one store instruction per 256 output bytes instead of one per sequence).
+struct OutRing {
+    LDSA uint8_t* b;
+    int sh;
+    int flushed;          // output bytes [0, flushed) are in global memory
+    __device__ __forceinline__ void put(int pos, uint32_t v) const {
+        ((volatile LDSA uint8_t*)b)[(pos + sh) & (kOut - 1)] = (uint8_t)v;
     }
-    for (int base = 0; base < total; base += LZH_WAVE) {
-        const int t = base + lane;
-        const int lp = anchor + t - lit0;
-        const bool inlit = t >= lit0 && t < lit1;
-        uint32_t lb = 0;
-        if (lit_in_ring) lb = R.byte(lp);
-        else if (inlit) lb = in.b(lp);
+    __device__ __forceinline__ uint32_t dword(int X) const {
+        return ((volatile const LDSA uint32_t*)b)[(X & (kOut - 1)) >> 2];
+    }
+    // global <- ring bytes [flushed, upto): aligned dwords, bytewise partial dwords at the ends
+    __device__ __forceinline__ void flush(const Bytes& out, int upto, int lane) {
+        const int fx = flushed + sh, ux = upto + sh;
+        wave_lds_fence();
+        for (int D0 = fx & ~3; D0 < ux; D0 += 4 * LZH_WAVE) {
+            const int D = D0 + 4 * lane;
+            const uint32_t w = dword(D);
+            if (D >= fx && D + 4 <= ux) {
+                st_b32(out.r, D, w);
+            } else if (D + 4 > fx && D < ux) {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (D + k >= fx && D + k < ux) st_u8(out.r, D + k, (w >> (8 * k)) & 0xffu);
+            }
+        }
+        flushed = upto;
+    }
+};
+
+// byte t of a sequence (token, literal-length bytes, literals, offset, match-length bytes)
+struct SeqLayout {
+    int lx, mx, lit0, lit1, total;
+    uint32_t token, lrem, mrem;
+    __device__ __forceinline__ SeqLayout(int lit, bool has_match, int ml) {
+        lx = ext_len_bytes(lit);
+        mx = has_match ? ext_len_bytes(ml) : 0;
+        lit0 = 1 + lx;
+        lit1 = lit0 + lit;
+        total = lit1 + (has_match ? 2 + mx : 0);
+        token = ((uint32_t)min(lit, 15) << 4) | (has_match ? (uint32_t)min(ml, 15) : 0u);
+        lrem = (uint32_t)(lit - 15) % 255u;
+        mrem = (uint32_t)(ml - 15) % 255u;
+    }
+    __device__ __forceinline__ uint32_t byte(int t, uint32_t lb, int off) const {
         const int u = t - (lit1 + 2);
         uint32_t v = token;
         v = (t >= 1 && t < lit0) ? (t == lx ? lrem : 255u) : v;
-        v = inlit ? lb : v;
+        v = (t >= lit0 && t < lit1) ? lb : v;
         v = t == lit1 ? ((uint32_t)off & 0xffu) : v;
         v = t == lit1 + 1 ? ((uint32_t)off >> 8) : v;
         v = (u >= 0) ? (u == mx - 1 ? mrem : 255u) : v;
-        if (t < total) out.st8(op + t, v);
+        return v;
     }
-    return op + total;
+};
+
+// Emit one sequence (has_match) or the final literal run at op; returns the new op.
+// Common case (<= 256 bytes, literals in the input ring): assembled in the output ring.
+__device__ __forceinline__ int emit_seq(const Bytes& in, const Ring& R, const Bytes& out, OutRing& O, int op,
+                                        int anchor, int lit, bool has_match, int off, int ml, int lane) {
+    const SeqLayout S(lit, has_match, ml);
+    const bool lit_in_ring = R.has(anchor, anchor + lit);
+    if (S.total <= 4 * LZH_WAVE && (lit_in_ring || lit <= 2 * LZH_WAVE)) {
+        for (int base = 0; base < S.total; base += LZH_WAVE) {
+            const int t = base + lane;
+            const int lp = anchor + t - S.lit0;
+            uint32_t lb = 0;
+            if (lit_in_ring) lb = R.byte(lp);
+            else if (t >= S.lit0 && t < S.lit1) lb = in.b(lp);
+            if (t < S.total) O.put(op + t, S.byte(t, lb, off));
+        }
+        op += S.total;
+        if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
+        return op;
+    }
+    // long sequence: drain the ring, then write straight to global memory
+    O.flush(out, op, lane);
+    if (lane == 0) out.st8(op, S.token);
+    for (int b = lane; b < S.lx; b += LZH_WAVE) out.st8(op + 1 + b, b == S.lx - 1 ? S.lrem : 255u);
+    if (lit_in_ring) {
+        for (int base = 0; base < lit; base += LZH_WAVE)
+            if (base + lane < lit) out.st8(op + S.lit0 + base + lane, R.byte(anchor + base + lane));
+    } else {
+        copy_span(in, anchor, out, op + S.lit0, lit, lane, LZH_WAVE);
+    }
+    if (has_match) {
+        if (lane < 2) out.st8(op + S.lit1 + lane, lane ? ((uint32_t)off >> 8) : ((uint32_t)off & 0xffu));
+        for (int b = lane; b < S.mx; b += LZH_WAVE) out.st8(op + S.lit1 + 2 + b, b == S.mx - 1 ? S.mrem : 255u);
+    }
+    op += S.total;
+    O.flushed = op;
+    return op;
 }
 
-// M-side byte of the hit lane's window: spec index si (0..23) of the six uniform dwords
-__device__ __forceinline__ uint32_t spec_byte(int si, uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t e4,
-                                              uint32_t e5) {
-    const int q = si >> 2;
-    uint32_t v = e0;
-    v = q == 1 ? e1 : v;
-    v = q == 2 ? e2 : v;
-    v = q == 3 ? e3 : v;
-    v = q == 4 ? e4 : v;
-    v = q == 5 ? e5 : v;
-    return (v >> (8 * (si & 3))) & 0xffu;
+// Per-lane match evaluation of probe p against candidate c, from 28 bytes around each:
+//   P side  [p-4, p+24) from the input ring (or global memory),
+//   M side  [c-4, c+24) loaded speculatively for every lane in one 32-byte window.
+// ok  : the 4-byte seed matches (LZ4_read32(match) == LZ4_read32(ip), lz4.c:1005)
+// bkr : bytes of backward match p-1.. vs c-1.., capped at 4 (catch-up, lz4.c:1017-1020)
+// len : bytes of forward match p+4.. vs c+4.., capped at 20 (LZ4_count, lz4.c:603-626)
+struct PSide {
+    uint32_t m4, w, q0, q1, q2, q3, q4;       // words at p-4, p, p+4, .., p+20
+};
+
+__device__ __forceinline__ PSide p_side_ring(const Ring& R, int p) {
+    const int X = p - 4 + R.sh, A = X & ~3;
+    const uint32_t s = (uint32_t)X & 3u;
+    const uint32_t a0 = R.dword(A), a1 = R.dword(A + 4), a2 = R.dword(A + 8), a3 = R.dword(A + 12),
+                   a4 = R.dword(A + 16), a5 = R.dword(A + 20), a6 = R.dword(A + 24), a7 = R.dword(A + 28);
+    PSide v;
+    v.m4 = __builtin_amdgcn_alignbyte(a1, a0, s);
+    v.w = __builtin_amdgcn_alignbyte(a2, a1, s);
+    v.q0 = __builtin_amdgcn_alignbyte(a3, a2, s);
+    v.q1 = __builtin_amdgcn_alignbyte(a4, a3, s);
+    v.q2 = __builtin_amdgcn_alignbyte(a5, a4, s);
+    v.q3 = __builtin_amdgcn_alignbyte(a6, a5, s);
+    v.q4 = __builtin_amdgcn_alignbyte(a7, a6, s);
+    return v;
 }
 
-template <bool kSmall>
-__device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab, LDSA uint32_t* ringw,
-                               LDSA uint32_t* specw, uint32_t* out_size, unsigned long long* stats) {
-    (void)specw;
+__device__ __forceinline__ PSide p_side_global(const Bytes& in, int p) {
+    const int X = p - 4 + in.sh, A = X & ~3;
+    const uint32_t s = (uint32_t)X & 3u;
+    // a0 (bytes A..A+3) matters only when A >= 0; its own clamped offset keeps it out of the
+    // wide load of a1..a7, whose range check would otherwise fail as a whole at A = -4
+    const uint32_t a0 = ld_b32(in.r, max(A, 0)), a1 = ld_b32(in.r, A + 4), a2 = ld_b32(in.r, A + 8),
+                   a3 = ld_b32(in.r, A + 12), a4 = ld_b32(in.r, A + 16), a5 = ld_b32(in.r, A + 20),
+                   a6 = ld_b32(in.r, A + 24), a7 = ld_b32(in.r, A + 28);
+    PSide v;
+    v.m4 = __builtin_amdgcn_alignbyte(a1, a0, s);
+    v.w = __builtin_amdgcn_alignbyte(a2, a1, s);
+    v.q0 = __builtin_amdgcn_alignbyte(a3, a2, s);
+    v.q1 = __builtin_amdgcn_alignbyte(a4, a3, s);
+    v.q2 = __builtin_amdgcn_alignbyte(a5, a4, s);
+    v.q3 = __builtin_amdgcn_alignbyte(a6, a5, s);
+    v.q4 = __builtin_amdgcn_alignbyte(a7, a6, s);
+    return v;
+}
+
+struct MWin {
+    uint32_t d0, d1, d2, d3, d4, d5, d6, d7;
+    int sm;
+    __device__ __forceinline__ void load(const Bytes& in, uint32_t c, bool valid) {
+        const int X = (valid ? (int)c : 0) + in.sh;
+        const int A = (X & ~3) - 4;
+        sm = X & 3;
+        d0 = d1 = d2 = d3 = d4 = d5 = d6 = d7 = 0;
+        if (valid) {
+            // d0 (bytes before the candidate) matters only when A >= 0: clamped, separate load
+            // (a merged wide load starting at offset -4 would fail its range check as a whole)
+            d0 = ld_b32(in.r, max(A, 0)); d1 = ld_b32(in.r, A + 4); d2 = ld_b32(in.r, A + 8); d3 = ld_b32(in.r, A + 12);
+            d4 = ld_b32(in.r, A + 16); d5 = ld_b32(in.r, A + 20); d6 = ld_b32(in.r, A + 24); d7 = ld_b32(in.r, A + 28);
+        }
+    }
+};
+
+__device__ __forceinline__ uint32_t byte_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x) >> 3; }
+
+// returns ok; sets bkr (0..4) and len (0..20)
+__device__ __forceinline__ bool eval_lane(const PSide& P, const MWin& W, bool valid, int& bkr, int& len) {
+    const uint32_t s = (uint32_t)W.sm;
+    const uint32_t mm4 = __builtin_amdgcn_alignbyte(W.d1, W.d0, s);
+    const uint32_t mw = __builtin_amdgcn_alignbyte(W.d2, W.d1, s);
+    const uint32_t x0 = P.q0 ^ __builtin_amdgcn_alignbyte(W.d3, W.d2, s);
+    const uint32_t x1 = P.q1 ^ __builtin_amdgcn_alignbyte(W.d4, W.d3, s);
+    const uint32_t x2 = P.q2 ^ __builtin_amdgcn_alignbyte(W.d5, W.d4, s);
+    const uint32_t x3 = P.q3 ^ __builtin_amdgcn_alignbyte(W.d6, W.d5, s);
+    const uint32_t x4 = P.q4 ^ __builtin_amdgcn_alignbyte(W.d7, W.d6, s);
+    int l = 20;
+    l = x4 ? 16 + (int)byte_ctz(x4) : l;
+    l = x3 ? 12 + (int)byte_ctz(x3) : l;
+    l = x2 ? 8 + (int)byte_ctz(x2) : l;
+    l = x1 ? 4 + (int)byte_ctz(x1) : l;
+    l = x0 ? (int)byte_ctz(x0) : l;
+    len = l;
+    const uint32_t y = P.m4 ^ mm4;
+    bkr = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
+    return valid && mw == P.w;
+}
+
+// Finish the match at P (candidate M) from the hit lane's bkr/len: catch-up bounded by the
+// anchor and the block start (lz4.c:1017-1020), count bounded by matchlimit (lz4.c:1055-1100);
+// runs past the precomputed windows continue lane-parallel from global memory.
+// Returns bk; cnt = bytes matched past P+4.
+template <bool kStats>
+__device__ __forceinline__ int finish_match(const Bytes& in, int P, int M, int bkr, int len, int anchor, int mlimit,
+                                            int& cnt_out, int lane, unsigned long long* stats) {
+    const int maxb = min(P - anchor, M);
+    int bk = min(bkr, maxb);
+    if (bkr == 4 && maxb > 4) {
+        LZ_STAT(5, 1);
+        int ip2 = P - 4, m2 = M - 4;
+        for (int it = 0; it < (1 << 12); it++) {
+            const int mb2 = min(ip2 - anchor, m2);
+            if (mb2 <= 0) break;
+            const bool e2b = lane < mb2 && in.b(ip2 - 1 - lane) == in.b(m2 - 1 - lane);
+            const int b = ffs64(ballot(!e2b));
+            ip2 -= b;
+            m2 -= b;
+            if (b < LZH_WAVE) break;
+        }
+        bk = P - ip2;
+    }
+    const int a = P + kMinMatch;
+    int cnt = len;
+    if (len == 20 && a + cnt < mlimit) {
+        LZ_STAT(6, 1);
+        for (int it = 0; it < (1 << 10) && a + cnt < mlimit; it++) {
+            const int o = cnt + 4 * lane;
+            const uint32_t x = in.w32(a + o) ^ in.w32(M + kMinMatch + o);
+            const uint64_t ne = ballot(x != 0);
+            if (ne) {
+                const int l = ffs64(ne);
+                cnt += 4 * l + (int)byte_ctz(rdlane(x, l));
+                break;
+            }
+            cnt += 4 * LZH_WAVE;
+        }
+    }
+    cnt_out = min(cnt, mlimit - a);
+    return bk;
+}
+
+__device__ __forceinline__ uint64_t lane_bits(int lo, int hi) {   // bits lo..hi (0 <= lo <= hi <= 63)
+    const uint64_t top = hi >= 63 ? ~0ull : ((2ull << hi) - 1ull);
+    return top & ~((1ull << lo) - 1ull);
+}
+
+// Group lanes by table slot (one ballot per slot that has a collision): grp = lanes sharing
+// this lane's slot; prev = the closest earlier lane in it (-1 if none).
+__device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t losers, uint64_t& grp, int& prev,
+                                            int lane) {
+    uint64_t pending = losers;
+    grp = 1ull << lane;
+    prev = -1;
+    for (int it = 0; it < LZH_WAVE && pending; it++) {
+        const int l = ffs64(pending);
+        const uint32_t hv = rdlane(h, l);
+        const bool mine = valid && h == hv;
+        const uint64_t m = ballot(mine);
+        pending &= ~m;
+        if (mine) {
+            grp = m;
+            const uint64_t below = m & ((1ull << lane) - 1ull);
+            if (below) prev = 63 - __builtin_clzll(below);
+        }
+    }
+}
+
+template <bool kSmall, bool kStats>
+__device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab,
+                               LDSA uint32_t* ringw, LDSA uint8_t* outb, uint32_t* out_size,
+                               unsigned long long* stats) {
     const int lane = threadIdx.x;
     Table<kSmall> T{tab};
     if (n <= 0) {
@@ -156,53 +351,54 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
     }
     Ring R{ringw, in.sh, 0};
+    OutRing O{outb, out.sh, 0};
     const int endX = n + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
     wait_vm();
     wave_lds_fence();
 
     int op = 0, anchor = 0;
-    bool pend = false;                       // deferred sequence
+    bool pend = false;                       // one sequence waits to be emitted
     int p_anchor = 0, p_lit = 0, p_off = 0, p_ml = 0;
 
     if (n >= kMinLength) {
         const int mfl1 = n - kMfLimit + 1;
         const int mlimit = n - kLastLiterals;
         const int64_t a64 = (int64_t)acc << 6;
-        const int hb = kSmall ? 4 : 5;
 
-        {
+        {   // position 0 enters the table before the first search (lz4.c:922-923)
             const uint32_t h0 = hash_of<kSmall>(R.u32(0), R.byte(4));
             if (lane == 0) T.put(h0, 0);
             wave_lds_fence();
         }
-        int ip = 1, s = 1, k0 = 0;
-        bool retest = false;
-        uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
-        uint64_t tlast = stats ? __builtin_amdgcn_s_memtime() : 0;
+        // Parse state.  Run batches (acceleration 1, a search in its first 64 probes): lanes
+        // are positions base..base+63; the next probe is q, probes step by 1 up to qlim (the
+        // re-test at a match end, then 64 step-1 search probes, lz4.c:955-969 / :1148-1200);
+        // pins = a pending ip-2 table fill (lz4.c:1145-1146) sitting at base.  Stride batches
+        // (any other schedule): one sequence per batch, the search from s with k0 probes done.
+        bool runb = acc == 1, retest = false, go = true;
+        int base = 1, q = 1, qlim = 64, pins = -1;
+        int s = 1, k0 = 0;
 
-        for (int guard = 0; guard < 4 * n + 64; guard++) {
-            LZ_T(5);
-            // ---- probe plan: lane -> position, validity (forwardIp <= mflimitPlusOne)
-            const bool fast = acc == 1 && k0 == 0;
-            // in a fast re-test batch lane 63 carries the ip-2 table fill (lz4.c:1146) instead of
-            // a probe; it is written before any probe reads the table
-            const bool ins63 = fast && retest;
-            // a re-test batch probes only kRT lanes: the first hit after a match is almost always
-            // within a few positions, and idle lanes issue no candidate loads
+        for (int guard = 0; go && guard < 4 * n + 64; guard++) {
+            runb = unii(runb) != 0; retest = unii(retest) != 0;
+            base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
+            op = unii(op); anchor = unii(anchor); pend = unii(pend) != 0;
+            p_anchor = unii(p_anchor); p_lit = unii(p_lit); p_off = unii(p_off); p_ml = unii(p_ml);
+            R.fill = unii(R.fill); O.flushed = unii(O.flushed);
+            LZ_STAT(0, 1);
+
+            // ---- lanes -> positions
             int p;
-            bool valid, term;
-            if (fast) {
-                p = (retest ? ip : s) + lane;            // re-test ip, then search ip+1.. step 1
-                const bool act = !retest || lane < kRT;
-                valid = act && p + 1 <= mfl1;
-                term = act && p + 1 > mfl1;
-                if (ins63 && lane == 63) { p = ip - 2; valid = false; term = false; }
+            bool valid;
+            if (runb) {
+                p = base + lane;
+                valid = p + 1 <= mfl1;        // forwardIp <= mflimitPlusOne (lz4.c:969)
             } else {
                 int64_t pp, nxt;
                 if (retest && lane == 0) {
-                    pp = ip;
-                    nxt = (int64_t)ip + 1;
+                    pp = s - 1;
+                    nxt = s;
                 } else {
                     const int k = retest ? lane - 1 : k0 + lane;
                     const int64_t o = k == 0 ? 0 : 1 + step_prefix(a64 + k - 1) - step_prefix(a64);
@@ -211,123 +407,139 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     nxt = pp + st;
                 }
                 valid = nxt <= mfl1;
-                term = !valid;
                 p = valid ? (int)pp : 0;
             }
             const uint64_t vmask = ballot(valid);
-            const uint64_t tmask = ballot(term);
-            const int front = ins63 ? ip - 2 : rdlanei(p, 0);
+            const int front = rdlanei(p, 0);
             const int pmax = vmask ? rdlanei(p, 63 - __builtin_clzll(vmask)) : front;
-            LZ_STAT(0, 1);
-            LZ_STAT(2, fast ? 1 : 0);
 
-            // ---- hash (ring when it covers the batch)
-            uint32_t pw, b4 = 0;
-            if (R.has(front - 4, pmax + hb + 8)) {
-                pw = R.u32(p);
-                if (!kSmall) b4 = R.byte(p + 4);
-            } else if (kSmall) {
-                LZ_STAT(9, 1);
-                pw = in.w32(p);
+            // ---- P-side bytes (ring when it covers the batch), hash, table read / claim / read back
+            PSide ps;
+            uint32_t b4 = 0;
+            if (R.has(front - 4, pmax + 28)) {
+                ps = p_side_ring(R, p);
             } else {
-                const uint64_t v = in.w40(p);
-                pw = (uint32_t)v;
-                b4 = (uint32_t)(v >> 32);
+                LZ_STAT(9, 1);
+                ps = p_side_global(in, p);
             }
-            const uint32_t h = hash_of<kSmall>(pw, b4);
-            if (ins63 && lane == 63) T.put(h, (uint32_t)(ip - 2));
-            else if (retest && !fast) {   // general plan: the ip-2 fill happened before the batch
-            }
+            if (!kSmall) b4 = ps.q0 & 0xffu;
+            const uint32_t h = hash_of<kSmall>(ps.w, b4);
             const uint32_t old = T.get(h);
             if (valid) T.put(h, (uint32_t)p);
             wave_lds_fence();
             const uint32_t back = T.get(h);
-            // lanes whose table write lost to another lane of the batch (same slot)
             const uint64_t losers = ballot(valid && back != (uint32_t)p);
             uint32_t cand = old;
-            LZ_T(0);
-            // ---- speculative candidate window [cand-4, cand+20)
-            int cX = (valid ? (int)cand : 0) + in.sh;
-            int cA = (cX & ~3) - 4;
-            uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0, d5 = 0;
-            if (valid) {
-                d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
-                d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
-            }
-            // ---- deferred emission of the previous sequence (stores overlap the loads above)
+            MWin W;
+            W.load(in, cand, valid);
+            // ---- deferred emission (LDS work under the loads above)
             if (pend) {
-                op = emit_seq(in, R, out, op, p_anchor, p_lit, true, p_off, p_ml, lane);
+                op = emit_seq(in, R, out, O, op, p_anchor, p_lit, true, p_off, p_ml, lane);
                 pend = false;
             }
-            // ---- keep the ring ahead of the batch front
             {
                 const int target = min(front + in.sh + kAhead, endX + 256);
                 for (int r = 0; r < 4 && R.fill < target; r++) { R.refill(in.r, lane); LZ_STAT(12, 1); }
             }
-            LZ_T(1);
             wait_vm();
             wave_lds_fence();
-            LZ_T(2);
-
-            bool ok = valid && __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)cX & 3u) == pw;
+            int bkr, len;
+            bool ok = eval_lane(ps, W, valid, bkr, len);
             if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
+
+            if (runb) {
+                // ================= run batch: resolve every sequence that starts in the batch
+                const uint64_t okm = ballot(ok);
+                // a lane with an earlier lane in its slot sees that lane's write if it was
+                // inserted: probes are resolved only below the first such lane C
+                uint64_t grp = 1ull << lane;
+                int C = LZH_WAVE;
+                if (losers) {
+                    LZ_STAT(1, 1);
+                    int prev;
+                    slot_groups(h, valid, losers, grp, prev, lane);
+                    C = ffs64(ballot(prev >= 0));
+                }
+                uint64_t I = pins >= 0 ? (1ull << (pins - base)) : 0ull;   // lanes left in the table
+                pins = -1;
+                bool next_stride = false;
+                for (int it = 0; it < LZH_WAVE + 1; it++) {
+                    const int lo = q - base;
+                    const int hi = min(min(qlim - base, LZH_WAVE - 1), C - 1);
+                    if (lo > hi) break;                                // batch (or clean prefix) done
+                    const uint64_t rm = lane_bits(lo, hi);
+                    const uint64_t hm = okm & rm, tm = ~vmask & rm;
+                    const int fh = ffs64(hm), ft = ffs64(tm);
+                    if (ft < fh) { go = false; break; }               // ran past mflimit (lz4.c:969)
+                    if (!hm) {                                         // no match up to hi
+                        I |= rm;
+                        q = base + hi + 1;
+                        if (hi == qlim - base) {                       // step 1 exhausted: stride batches
+                            next_stride = true;
+                            s = qlim - 63;
+                            k0 = LZH_WAVE;
+                            retest = false;
+                        }
+                        break;
+                    }
+                    I |= lane_bits(lo, fh);
+                    LZ_STAT(3, 1);
+                    const int P = base + fh;
+                    const int M = rdlanei((int)cand, fh);
+                    int cnt;
+                    const int bk = finish_match<kStats>(in, P, M, rdlanei(bkr, fh), rdlanei(len, fh), anchor, mlimit,
+                                                        cnt, lane, stats);
+                    if (pend) op = emit_seq(in, R, out, O, op, p_anchor, p_lit, true, p_off, p_ml, lane);
+                    pend = true;
+                    p_anchor = anchor; p_lit = P - bk - anchor; p_off = P - M; p_ml = bk + cnt;
+                    const int ip = P + kMinMatch + cnt;
+                    anchor = ip;
+                    if (ip >= mfl1) { go = false; break; }             // lz4.c:1142
+                    if (ip - 2 - base < LZH_WAVE) I |= 1ull << (ip - 2 - base);
+                    else pins = ip - 2;
+                    q = ip;                                            // re-test, then search from ip+1
+                    qlim = ip + LZH_WAVE;
+                }
+                if (go) {
+                    // table: the last inserted lane of each slot, or the slot's old value
+                    const bool inI = (I >> lane) & 1ull;
+                    if (!losers) {
+                        if (valid && !inI) T.put(h, old);
+                    } else {
+                        const uint64_t gi = grp & I;
+                        const bool wr = valid && (gi == 0 || (inI && (gi & ~((2ull << lane) - 1ull)) == 0));
+                        if (wr) T.put(h, inI ? (uint32_t)p : old);
+                    }
+                    wave_lds_fence();
+                    if (next_stride) runb = false;
+                    else base = pins >= 0 ? pins : q;
+                }
+                continue;
+            }
+
+            // ================= stride batch: first sequence only
             uint64_t hits = ballot(ok);
+            const uint64_t tmask = ballot(!valid);
             const int fi = ffs64(tmask);
             int fh = ffs64(hits);
             bool found = hits != 0;
             int L = found ? fh : fi - 1;
             uint64_t upto = L < 0 ? 0ull : (L >= 63 ? ~0ull : ((2ull << L) - 1ull));
-            // exact resolution is needed only if two lanes <= L share a slot; any such pair has
-            // a loser <= L, and for small L the pair test is a few cross-lane compares
-            bool exact = false;
-            if (losers & upto) {
-                if (L <= 7) {
-                    bool pr = false;
-#pragma unroll
-                    for (int d = 1; d <= 7; d++) {
-                        const uint32_t hv = lane_gather(h, lane >= d ? lane - d : lane);
-                        pr = pr || (d <= lane && lane <= L && hv == h);
-                    }
-                    exact = ballot(pr) != 0;
-                } else {
-                    exact = true;
-                }
-            }
-            if (!exact) {
-                // keep writes of lanes <= L: winners above L restore, then lanes <= L re-assert
+            if (!(losers & upto)) {
                 if (valid && lane > L && back == (uint32_t)p) T.put(h, old);
-                if (losers & upto) {
-                    wave_lds_fence();
-                    if (lane <= L) T.put(h, (uint32_t)p);
-                }
             } else {
+                // lanes up to L sharing a slot: each sees the previous lane of its slot
                 LZ_STAT(1, 1);
                 if (valid) T.put(h, old);
                 wave_lds_fence();
-                uint64_t pending = losers;
-                uint64_t grp = 1ull << lane;
-                int prev = -1;
-                for (int it = 0; it < LZH_WAVE && pending; it++) {
-                    const int l = ffs64(pending);
-                    const uint32_t hv = rdlane(h, l);
-                    const bool mine = valid && h == hv;
-                    const uint64_t m = ballot(mine);
-                    pending &= ~m;
-                    if (mine) {
-                        grp = m;
-                        const uint64_t below = m & ((1ull << lane) - 1ull);
-                        if (below) prev = 63 - __builtin_clzll(below);
-                    }
-                }
+                uint64_t grp;
+                int prev;
+                slot_groups(h, valid, losers, grp, prev, lane);
                 const uint32_t ppos = lane_gather((uint32_t)p, prev < 0 ? lane : prev);
                 if (prev >= 0) cand = ppos;
-                cX = (valid ? (int)cand : 0) + in.sh;
-                cA = (cX & ~3) - 4;
-                if (valid) {
-                    d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
-                    d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
-                }
-                ok = valid && __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)cX & 3u) == pw;
+                W.load(in, cand, valid);
+                wait_vm();
+                ok = eval_lane(ps, W, valid, bkr, len);
                 if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
                 hits = ballot(ok);
                 fh = ffs64(hits);
@@ -339,102 +551,47 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     if (!later) T.put(h, (uint32_t)p);
                 }
             }
-            if (!found) {
-                wave_lds_fence();
-                if (tmask) break;                                      // ran past mflimit
-                if (retest) { retest = false; s = ip + 1; k0 = fast ? kRT - 1 : LZH_WAVE - 1; }
-                else k0 += LZH_WAVE;
-                continue;
-            }
             wave_lds_fence();
-
-            // ---- hit at P with candidate M; one lane-parallel compare answers catch-up
-            // (lanes 0..3: P-1-j vs M-1-j, lz4.c:1019) and the match length from P+4 (lanes 4..:
-            // P+4+k vs M+4+k, LZ4_count lz4.c:603-626).  Catch-up back bk moves both starts but
-            // not the match end: count(P-bk+4) = bk + count(P+4).
-            LZ_T(3);
-            const int P = rdlanei(p, fh);
-            const int M = rdlanei((int)cand, fh);
-            const uint32_t e0 = rdlane(d0, fh), e1 = rdlane(d1, fh), e2 = rdlane(d2, fh), e3 = rdlane(d3, fh),
-                           e4 = rdlane(d4, fh), e5 = rdlane(d5, fh);
-            LZ_STAT(3, 1);
-            LZ_STAT(4, fh);
-            const int sbase = ((M + in.sh) & 3) + 4;           // window index of byte M
-            const int kmax = 20 - sbase;                        // count bytes the window holds (13..16)
-            const int maxb = min(P - anchor, M);
-            const int blim = min(maxb, 4);
-            int qpos, si;
-            bool act;
-            if (lane < 4) { qpos = P - 1 - lane; si = sbase - 1 - lane; act = lane < blim; }
-            else { const int k = lane - 4; qpos = P + 4 + k; si = sbase + 4 + k; act = k < kmax; }
-            const bool rok = R.has(P - 4, P + 4 + 16);
-            uint32_t pb = 0;
-            if (rok) pb = R.byte(qpos);
-            else if (act) pb = in.b(qpos);
-            const bool eq = act && pb == spec_byte(si & 31, e0, e1, e2, e3, e4, e5);
-            const uint64_t em = ballot(eq);
-            int bk = ffs64(~em & 0xfull);
-            if (bk > blim) bk = blim;
-            int cnt = ffs64((~(em >> 4) & ((1ull << kmax) - 1ull)) | (1ull << kmax));
-            if (bk == 4 && maxb > 4) {
-                LZ_STAT(5, 1);
-                int ip2 = P - 4, m2 = M - 4;
-                for (int it = 0; it < (1 << 12); it++) {
-                    const int mb2 = min(ip2 - anchor, m2);
-                    if (mb2 <= 0) break;
-                    const bool e2b = lane < mb2 && in.b(ip2 - 1 - lane) == in.b(m2 - 1 - lane);
-                    const int b = ffs64(ballot(!e2b));
-                    ip2 -= b;
-                    m2 -= b;
-                    if (b < LZH_WAVE) break;
-                }
-                bk = P - ip2;
-            }
-            const int a = P + kMinMatch;                        // count start before catch-up
-            if (cnt >= kmax && a + cnt < mlimit) {
-                LZ_STAT(6, 1);
-                for (int it = 0; it < (1 << 10) && a + cnt < mlimit; it++) {
-                    const int o = cnt + 4 * lane;
-                    const uint32_t x = in.w32(a + o) ^ in.w32(M + kMinMatch + o);
-                    const uint64_t ne = ballot(x != 0);
-                    if (ne) {
-                        const int l = ffs64(ne);
-                        cnt += 4 * l + (__builtin_ctz(rdlane(x, l)) >> 3);
-                        break;
-                    }
-                    cnt += 4 * LZH_WAVE;
+            if (!found) {
+                if (tmask) go = false;                                 // ran past mflimit
+                else if (retest) { retest = false; k0 = LZH_WAVE - 1; }
+                else k0 += LZH_WAVE;
+            } else {
+                LZ_STAT(3, 1);
+                const int P = rdlanei(p, fh);
+                const int M = rdlanei((int)cand, fh);
+                int cnt;
+                const int bk = finish_match<kStats>(in, P, M, rdlanei(bkr, fh), rdlanei(len, fh), anchor, mlimit, cnt,
+                                                    lane, stats);
+                pend = true;
+                p_anchor = anchor; p_lit = P - bk - anchor; p_off = P - M; p_ml = bk + cnt;
+                const int ip = P + kMinMatch + cnt;
+                anchor = ip;
+                if (ip >= mfl1) {
+                    go = false;
+                } else if (acc == 1) {                                 // back to run batches
+                    runb = true;
+                    pins = ip - 2;
+                    base = ip - 2;
+                    q = ip;
+                    qlim = ip + LZH_WAVE;
+                } else {   // fill table at ip-2 (lz4.c:1146), then re-test ip as lane 0
+                    uint32_t w, bb = 0;
+                    if (R.has(ip - 6, ip + 8)) { w = R.u32(ip - 2); if (!kSmall) bb = R.byte(ip + 2); }
+                    else { const uint64_t v = in.w40(ip - 2); w = (uint32_t)v; bb = (uint32_t)(v >> 32); }
+                    const uint32_t hm2 = hash_of<kSmall>(w, bb);
+                    if (lane == 0) T.put(hm2, (uint32_t)(ip - 2));
+                    wave_lds_fence();
+                    retest = true;
+                    s = ip + 1;
+                    k0 = 0;
                 }
             }
-            cnt = min(cnt, mlimit - a);
-            const int P2 = P - bk;
-            const int lit = P2 - anchor;
-            const int ml = bk + cnt;
-            LZ_STAT(7, bk > 0 ? 1 : 0);
-            LZ_STAT(10, lit);
-            LZ_STAT(11, ml);
-            pend = true;
-            p_anchor = anchor; p_lit = lit; p_off = P - M; p_ml = ml;
-
-            ip = a + cnt;                                       // = P2 + 4 + ml
-            anchor = ip;
-            if (ip >= mfl1) break;
-            if (acc != 1) {   // general plan: fill table at ip-2 now (fast plan: lane 63 next batch)
-                uint32_t w, bb = 0;
-                if (R.has(ip - 6, ip + 8)) { w = R.u32(ip - 2); if (!kSmall) bb = R.byte(ip + 2); }
-                else { const uint64_t v = in.w40(ip - 2); w = (uint32_t)v; bb = (uint32_t)(v >> 32); }
-                const uint32_t hm2 = hash_of<kSmall>(w, bb);
-                if (lane == 0) T.put(hm2, (uint32_t)(ip - 2));
-                wave_lds_fence();
-            }
-            LZ_T(4);
-            retest = true;
-            s = ip + 1;
-            k0 = 0;
         }
-        for (int k = 0; k < 6; k++) LZ_STAT(16 + k, ph[k]);
     }
-    if (pend) op = emit_seq(in, R, out, op, p_anchor, p_lit, true, p_off, p_ml, lane);
-    op = emit_seq(in, R, out, op, anchor, n - anchor, false, 0, 0, lane);
+    if (pend) op = emit_seq(in, R, out, O, op, p_anchor, p_lit, true, p_off, p_ml, lane);
+    op = emit_seq(in, R, out, O, op, anchor, n - anchor, false, 0, 0, lane);
+    O.flush(out, op, lane);
     if (lane == 0) *out_size = (uint32_t)op;
 }
 
@@ -444,7 +601,8 @@ extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                            uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t chunk0,
                            unsigned long long* stats) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + 256 + 8];
+    // table 16 KiB | input ring 1 KiB | output ring 512 B  (17.5 KiB: 9 waves per CU)
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4];
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t off = chunk * chunk_size;
     if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
@@ -453,8 +611,32 @@ lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_read
     Bytes rin, rout;
     rin.init(in + off, readable);
     rout.init(stage + chunk * stride, stride);
-    if (n < 65547) lz4v3::compress_chunk<true>(rin, n, rout, acc, (LDSA uint32_t*)lds, (LDSA uint32_t*)lds + 4096, (LDSA uint32_t*)lds + 4096 + 256, csizes + chunk, stats);
-    else lz4v3::compress_chunk<false>(rin, n, rout, acc, (LDSA uint32_t*)lds, (LDSA uint32_t*)lds + 4096, (LDSA uint32_t*)lds + 4096 + 256, csizes + chunk, stats);
+    LDSA uint32_t* tab = (LDSA uint32_t*)lds;
+    LDSA uint32_t* ring = tab + 4096;
+    LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
+    if (n < 65547) lz4v3::compress_chunk<true, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats);
+    else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats);
+}
+
+// debug twin of the kernel above with event counters (tools/lz4_stats.py)
+extern "C" __global__ void __launch_bounds__(64)
+lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
+                              uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t chunk0,
+                              unsigned long long* stats) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4];
+    const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
+    const uint64_t off = chunk * chunk_size;
+    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
+    const int n = (int)min(chunk_size, n_total - off);
+    const uint64_t readable = min<uint64_t>(in_readable - off, (uint64_t)n + 64);
+    Bytes rin, rout;
+    rin.init(in + off, readable);
+    rout.init(stage + chunk * stride, stride);
+    LDSA uint32_t* tab = (LDSA uint32_t*)lds;
+    LDSA uint32_t* ring = tab + 4096;
+    LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
+    if (n < 65547) lz4v3::compress_chunk<true, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats);
+    else lz4v3::compress_chunk<false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats);
 }
 
 #include "launch.h"
@@ -472,7 +654,7 @@ extern "C" int lzh_debug_lz4_stats(const void* d_in, uint64_t n, uint64_t in_rea
                                    void* d_stage, uint32_t* d_csizes, unsigned long long* d_stats, void* stream) {
     const uint64_t k = (n + chunk_size - 1) / chunk_size;
     const uint64_t stride = ((chunk_size + chunk_size / 255 + 16 + 16) + 255) / 256 * 256;
-    hipLaunchKernelGGL(lzh_lz4_compress_v2_kernel, dim3((unsigned)k), dim3(64), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(lzh_lz4_compress_stats_kernel, dim3((unsigned)k), dim3(64), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, n, in_readable, chunk_size, acc, (uint8_t*)d_stage, stride, d_csizes, 0u,
                        d_stats);
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -7,8 +7,8 @@ lib = L.lib()
 f = lib.lzh_debug_lz4_stats
 f.restype = C.c_int
 f.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
-names = ["batches", "dup_batches", "fast_plan", "found", "sum_fh", "catchup_slow", "count_slow", "bk>0",
-         "lit_not_in_ring", "hash_ring_miss", "sum_lit", "sum_ml", "refills", "-", "-", "-"]
+names = ["batches", "collision_batches", "-", "sequences", "-", "catchup_slow", "count_slow", "-",
+         "-", "hash_ring_miss", "-", "-", "refills", "-", "-", "-"]
 for corpus in sys.argv[1:] or ["text", "json"]:
     n = 64 << 20
     host = L.datagen(corpus, n, seed=12345)
@@ -20,8 +20,4 @@ for corpus in sys.argv[1:] or ["text", "json"]:
     torch.cuda.synchronize()
     v = st.cpu().tolist()
     k = n // 65536
-    print(corpus, {names[i]: round(v[i] / k, 2) for i in range(13)}, "per chunk")
-    ph = v[16:22]
-    tot = sum(ph) or 1
-    print("  phase clocks per batch (s_memtime ticks):", {n_: round(ph[i] / max(v[0], 1), 1) for i, n_ in
-          enumerate(["plan+hash+table", "spec_issue+emit+prefetch", "wait_vm", "hit+commit", "catchup+count+book", "loop_top"])})
+    print(corpus, {names[i]: round(v[i] / k, 2) for i in range(13) if names[i] != '-'}, "per chunk")
