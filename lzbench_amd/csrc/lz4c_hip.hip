@@ -145,6 +145,19 @@ struct SeqLayout {
 // Common case (<= 256 bytes, literals in the input ring): assembled in the output ring.
 __device__ __forceinline__ int emit_seq(const Bytes& in, const Ring& R, const Bytes& out, OutRing& O, int op,
                                         int anchor, int lit, bool has_match, int off, int ml, int lane) {
+    // (ml counts match bytes beyond the 4-byte minimum, as the token does)
+    if (has_match && lit < 15 && ml < 15 && R.has(anchor, anchor + 16)) {
+        // short sequence (no length bytes): token, lit literals, 2-byte offset
+        const uint32_t lb = R.byte(anchor + lane - 1);
+        uint32_t v = ((uint32_t)lit << 4) | (uint32_t)ml;
+        v = (lane >= 1 && lane <= lit) ? lb : v;
+        v = lane == lit + 1 ? ((uint32_t)off & 0xffu) : v;
+        v = lane == lit + 2 ? ((uint32_t)off >> 8) : v;
+        if (lane < lit + 3) O.put(op + lane, v);
+        op += lit + 3;
+        if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
+        return op;
+    }
     const SeqLayout S(lit, has_match, ml);
     const bool lit_in_ring = R.has(anchor, anchor + lit);
     if (S.total <= 4 * LZH_WAVE && (lit_in_ring || lit <= 2 * LZH_WAVE)) {
@@ -309,8 +322,7 @@ __device__ __forceinline__ int finish_match(const Bytes& in, int P, int M, int b
 }
 
 __device__ __forceinline__ uint64_t lane_bits(int lo, int hi) {   // bits lo..hi (0 <= lo <= hi <= 63)
-    const uint64_t top = hi >= 63 ? ~0ull : ((2ull << hi) - 1ull);
-    return top & ~((1ull << lo) - 1ull);
+    return ((2ull << hi) - 1ull) & (~0ull << lo);                 // 2 << 63 wraps to 0: all ones
 }
 
 // Group lanes by table slot (one ballot per slot that has a collision): grp = lanes sharing
@@ -460,6 +472,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     slot_groups(h, valid, losers, grp, prev, lane);
                     C = ffs64(ballot(prev >= 0));
                 }
+                const int fv = __builtin_popcountll(vmask);           // first lane past mflimit
                 uint64_t I = pins >= 0 ? (1ull << (pins - base)) : 0ull;   // lanes left in the table
                 pins = -1;
                 bool next_stride = false;
@@ -468,10 +481,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     const int hi = min(min(qlim - base, LZH_WAVE - 1), C - 1);
                     if (lo > hi) break;                                // batch (or clean prefix) done
                     const uint64_t rm = lane_bits(lo, hi);
-                    const uint64_t hm = okm & rm, tm = ~vmask & rm;
-                    const int fh = ffs64(hm), ft = ffs64(tm);
-                    if (ft < fh) { go = false; break; }               // ran past mflimit (lz4.c:969)
+                    const uint64_t hm = okm & rm;
                     if (!hm) {                                         // no match up to hi
+                        if (hi >= fv) { go = false; break; }           // ran past mflimit (lz4.c:969)
                         I |= rm;
                         q = base + hi + 1;
                         if (hi == qlim - base) {                       // step 1 exhausted: stride batches
@@ -482,6 +494,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         }
                         break;
                     }
+                    const int fh = __builtin_ctzll(hm);               // valid lanes are a prefix: fh < fv
                     I |= lane_bits(lo, fh);
                     LZ_STAT(3, 1);
                     const int P = base + fh;
