@@ -462,26 +462,56 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             if (runb) {
                 // ================= run batch: resolve every sequence that starts in the batch
                 const uint64_t okm = ballot(ok);
-                // a lane with an earlier lane in its slot sees that lane's write if it was
-                // inserted: probes are resolved only below the first such lane C
+                // a probe whose slot holds an earlier lane of the batch sees that lane's position
+                // if it was inserted (probed or ip-2 filled), else the slot's old value: such
+                // "colliders" are re-evaluated per step against the in-batch candidate
                 uint64_t grp = 1ull << lane;
-                int C = LZH_WAVE;
+                uint64_t coll = 0;
                 if (losers) {
                     LZ_STAT(1, 1);
                     int prev;
                     slot_groups(h, valid, losers, grp, prev, lane);
-                    C = ffs64(ballot(prev >= 0));
+                    coll = ballot(prev >= 0);
                 }
+                const uint64_t below = (1ull << lane) - 1ull;
                 const int fv = __builtin_popcountll(vmask);           // first lane past mflimit
                 uint64_t I = pins >= 0 ? (1ull << (pins - base)) : 0ull;   // lanes left in the table
                 pins = -1;
                 bool next_stride = false;
                 for (int it = 0; it < LZH_WAVE + 1; it++) {
                     const int lo = q - base;
-                    const int hi = min(min(qlim - base, LZH_WAVE - 1), C - 1);
-                    if (lo > hi) break;                                // batch (or clean prefix) done
+                    const int hi = min(qlim - base, LZH_WAVE - 1);
+                    if (lo > hi) break;                                // batch done
                     const uint64_t rm = lane_bits(lo, hi);
-                    const uint64_t hm = okm & rm;
+                    uint64_t okx = okm;
+                    uint32_t ce = cand;
+                    int be = bkr, le = len;
+                    if (coll & rm) {
+                        // earlier slot members count as inserted if in I or probed in this step
+                        const uint64_t mk = grp & below & (I | (~0ull << lo));
+                        const int k = mk ? 63 - __builtin_clzll(mk) : lane;
+                        const uint32_t gm4 = lane_gather(ps.m4, k), gw = lane_gather(ps.w, k),
+                                       g0 = lane_gather(ps.q0, k), g1 = lane_gather(ps.q1, k),
+                                       g2 = lane_gather(ps.q2, k), g3 = lane_gather(ps.q3, k),
+                                       g4 = lane_gather(ps.q4, k);
+                        if (mk) {
+                            const uint32_t x0 = ps.q0 ^ g0, x1 = ps.q1 ^ g1, x2 = ps.q2 ^ g2, x3 = ps.q3 ^ g3,
+                                           x4 = ps.q4 ^ g4;
+                            int l = 20;
+                            l = x4 ? 16 + (int)byte_ctz(x4) : l;
+                            l = x3 ? 12 + (int)byte_ctz(x3) : l;
+                            l = x2 ? 8 + (int)byte_ctz(x2) : l;
+                            l = x1 ? 4 + (int)byte_ctz(x1) : l;
+                            l = x0 ? (int)byte_ctz(x0) : l;
+                            le = l;
+                            const uint32_t y = ps.m4 ^ gm4;
+                            be = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
+                            ce = (uint32_t)(base + k);
+                        }
+                        const bool okc = mk ? (valid && gw == ps.w) : ok;
+                        okx = ballot(okc);
+                    }
+                    const uint64_t hm = okx & rm;
                     if (!hm) {                                         // no match up to hi
                         if (hi >= fv) { go = false; break; }           // ran past mflimit (lz4.c:969)
                         I |= rm;
@@ -498,9 +528,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     I |= lane_bits(lo, fh);
                     LZ_STAT(3, 1);
                     const int P = base + fh;
-                    const int M = rdlanei((int)cand, fh);
+                    const int M = rdlanei((int)ce, fh);
                     int cnt;
-                    const int bk = finish_match<kStats>(in, P, M, rdlanei(bkr, fh), rdlanei(len, fh), anchor, mlimit,
+                    const int bk = finish_match<kStats>(in, P, M, rdlanei(be, fh), rdlanei(le, fh), anchor, mlimit,
                                                         cnt, lane, stats);
                     if (pend) op = emit_seq(in, R, out, O, op, p_anchor, p_lit, true, p_off, p_ml, lane);
                     pend = true;
