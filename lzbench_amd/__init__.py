@@ -27,7 +27,8 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblzbench_hip.so")
+# LZH_LIB: an alternative in-tree build of the same library (kernel experiments; tools/exp_build.sh)
+LIB_PATH = os.environ.get("LZH_LIB") or os.path.join(_HERE, "liblzbench_hip.so")
 DATAGEN_PATH = os.path.join(_HERE, "libdatagen.so")
 
 LZH_CODEC_LZ4, LZH_CODEC_SNAPPY, LZH_CODEC_MEMCPY = 0, 1, 2

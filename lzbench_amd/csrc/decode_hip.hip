@@ -209,6 +209,247 @@ __device__ int snappy_decode(const Bytes& in, int cs, const Bytes& out, int cap,
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------
+// v2: output through an LDS window.  The last kW decoded bytes of the chunk stay in LDS, so a
+// match whose source lies in them (most of them: median offsets are a few KiB) is an
+// LDS-to-LDS copy with no memory round trip; decoded bytes leave for global memory as aligned
+// dword stores once 256 are pending.  Far matches read the (already flushed) output with
+// L1-bypassing loads.
+namespace dec2 {
+
+constexpr int kW = 8192;
+
+struct Sink {
+    LDSA uint8_t* b;
+    Bytes out;
+    int flushed;      // output bytes [0, flushed) are in global memory
+    int ringlo;       // output bytes [ringlo, op) are in the window (bulk literal runs bypass it)
+    __device__ __forceinline__ void put(int pos, uint32_t v) const {
+        ((volatile LDSA uint8_t*)b)[(pos + out.sh) & (kW - 1)] = (uint8_t)v;
+    }
+    __device__ __forceinline__ uint32_t get(int pos) const {
+        return ((volatile const LDSA uint8_t*)b)[(pos + out.sh) & (kW - 1)];
+    }
+    __device__ __forceinline__ uint32_t dword(int X) const {
+        return ((volatile const LDSA uint32_t*)b)[(X & (kW - 1)) >> 2];
+    }
+    // global <- window bytes [flushed, upto)
+    __device__ __forceinline__ void flush(int upto, int lane) {
+        const int fx = flushed + out.sh, ux = upto + out.sh;
+        for (int D0 = fx & ~3; D0 < ux; D0 += 4 * LZH_WAVE) {
+            const int D = D0 + 4 * lane;
+            const uint32_t w = dword(D);
+            if (D >= fx && D + 4 <= ux) {
+                st_b32(out.r, D, w);
+            } else if (D + 4 > fx && D < ux) {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (D + k >= fx && D + k < ux) st_u8(out.r, D + k, (w >> (8 * k)) & 0xffu);
+            }
+        }
+        flushed = upto;
+    }
+    __device__ __forceinline__ void maybe_flush(int op, int lane) {
+        if (op - flushed >= 4 * LZH_WAVE) flush(((op + out.sh) & ~3) - out.sh, lane);
+    }
+
+    // literal run in[src, src+len) -> op
+    __device__ __forceinline__ void literals(const Win& w, const Bytes& in, int src, int op, int len, int lane) {
+        if (len > 8 * LZH_WAVE) {
+            // bulk: straight to global memory; the window restarts after the run
+            flush(op, lane);
+            copy_span(in, src, out, op, len, lane, LZH_WAVE);
+            flushed = op + len;
+            ringlo = op + len;
+            return;
+        }
+        for (int base = 0; base < len; base += LZH_WAVE) {
+            const int t = base + lane;
+            uint32_t v;
+            if (w.covers(src + base, src + base + LZH_WAVE)) v = w.lane_byte(src + t);
+            else v = in.b(src + t);
+            if (t < len) put(op + t, v);
+            maybe_flush(op + min(base + LZH_WAVE, len), lane);
+        }
+    }
+
+    // out[op + t] = out[op - off + t] for t < len (byte by byte semantics), 0 < off <= op
+    __device__ __forceinline__ void match(int op, int off, int len, int lane) {
+        const int src0 = op - off;
+        if (src0 >= ringlo && off <= kW - LZH_WAVE) {
+            for (int base = 0; base < len; base += LZH_WAVE) {
+                const int t = base + lane;
+                const int s = off >= LZH_WAVE ? src0 + t : src0 + (int)((uint32_t)t % (uint32_t)off);
+                const uint32_t v = get(s);
+                if (t < len) put(op + t, v);
+                maybe_flush(op + min(base + LZH_WAVE, len), lane);
+            }
+            return;
+        }
+        // far: the source is in global memory once every pending byte is flushed and stored
+        flush(op, lane);
+        for (int base = 0; base < len; base += LZH_WAVE) {
+            const int t = base + lane;
+            const int s = off >= LZH_WAVE ? src0 + t : src0 + (int)((uint32_t)t % (uint32_t)off);
+            if (off < len && base > 0) flush(op + base, lane);   // sources in this match's output
+            wait_vm();
+            const uint32_t v = t < len ? out.b_sc1(s) : 0u;
+            if (t < len) put(op + t, v);
+        }
+        maybe_flush(op + len, lane);
+    }
+};
+
+// returns decoded size or a negative error (same acceptance rules as lz4_decode above)
+__device__ int lz4_decode(const Bytes& in, int cs, Sink& O, int cap, int lane) {
+    if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
+    if (cs <= 0) return -1;
+    Win w;
+    w.bind(in);
+    w.load(0, lane);
+    int ip = 0, op = 0;
+    for (int guard = 0; guard <= cs; guard++) {
+        ip = unii(ip); op = unii(op);
+        if (ip >= cs) return -ip - 1;
+        w.ensure(ip, lane);
+        const uint32_t tok = w.byte(ip++);
+        int lit = (int)(tok >> 4);
+        if (lit == 15) {
+            if (ip >= cs - 15) return -ip - 1;
+            for (int it = 0; it <= cs; it++) {
+                w.ensure(ip, lane);
+                const uint32_t s = w.byte(ip++);
+                lit += (int)s;
+                if (ip >= cs - 15 || s != 255) break;
+            }
+        }
+        if (op + lit > cap - 12 || ip + lit > cs - 8) {
+            if (ip + lit != cs || op + lit > cap) return -ip - 1;
+            O.literals(w, in, ip, op, lit, lane);
+            op += lit;
+            break;
+        }
+        O.literals(w, in, ip, op, lit, lane);
+        ip += lit;
+        op += lit;
+        w.ensure(ip, lane);
+        const int off = (int)(w.byte(ip) | (w.byte(ip + 1) << 8));
+        ip += 2;
+        int ml = (int)(tok & 15u);
+        if (ml == 15) {
+            for (int it = 0; it <= cs; it++) {
+                w.ensure(ip, lane);
+                const uint32_t s = w.byte(ip++);
+                ml += (int)s;
+                if (ip >= cs - 4) return -ip - 1;
+                if (s != 255) break;
+            }
+        }
+        ml += 4;
+        if (off > op) return -ip - 1;
+        if (op + ml > cap - 5) return -ip - 1;
+        if (off == 0) {   // reference leaves zeros here; never produced by a compressor
+            for (int base = 0; base < ml; base += LZH_WAVE) {
+                if (base + lane < ml) O.put(op + base + lane, 0);
+                O.maybe_flush(op + min(base + LZH_WAVE, ml), lane);
+            }
+        } else {
+            O.match(op, off, ml, lane);
+        }
+        op += ml;
+    }
+    return op;
+}
+
+__device__ int snappy_decode(const Bytes& in, int cs, Sink& O, int cap, int lane) {
+    Win w;
+    w.bind(in);
+    w.load(0, lane);
+    int ip = 0;
+    uint32_t ulen = 0;
+    for (int shift = 0;; shift += 7) {
+        if (ip >= cs || shift >= 32) return -1;
+        const uint32_t c = w.byte(ip++);
+        const uint32_t val = c & 0x7fu;
+        if (shift == 28 && val > 15) return -1;
+        ulen |= val << shift;
+        if (c < 128) break;
+    }
+    if (ulen > (uint32_t)cap) return -1;
+    const int ul = (int)ulen;
+    int op = 0;
+    for (int guard = 0; guard <= cs && ip < cs; guard++) {
+        ip = unii(ip); op = unii(op);
+        w.ensure(ip, lane);
+        const uint32_t c = w.byte(ip++);
+        const uint32_t kind = c & 3u;
+        if (kind == 0) {
+            int len = (int)(c >> 2) + 1;
+            if (len > 60) {
+                const int nb = len - 60;
+                if (ip + nb > cs) return -1;
+                uint32_t v = 0;
+                for (int i = 0; i < nb; i++) v |= w.byte(ip + i) << (8 * i);
+                len = (int)v + 1;
+                if (v >= 0x7fffffffu) return -1;
+                ip += nb;
+            }
+            if ((int64_t)ip + len > cs || (int64_t)op + len > ul) return -1;
+            O.literals(w, in, ip, op, len, lane);
+            ip += len;
+            op += len;
+        } else {
+            const int extra = kind == 1 ? 1 : (kind == 2 ? 2 : 4);
+            if (ip + extra > cs) return -1;
+            int len;
+            uint32_t off;
+            if (kind == 1) {
+                len = (int)((c >> 2) & 7u) + 4;
+                off = ((c >> 5) << 8) | w.byte(ip);
+            } else {
+                len = (int)(c >> 2) + 1;
+                off = 0;
+                for (int i = 0; i < extra; i++) off |= w.byte(ip + i) << (8 * i);
+            }
+            ip += extra;
+            if (off == 0 || off > (uint32_t)op || op + len > ul) return -1;
+            O.match(op, (int)off, len, lane);
+            op += len;
+        }
+    }
+    return op == ul ? op : -1;
+}
+
+}  // namespace dec2
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                         const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
+                         int32_t* status, uint32_t chunk0) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[dec2::kW];
+    const int lane = threadIdx.x;
+    const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
+    const uint64_t ooff = chunk * chunk_size;
+    if (ooff >= n_total) return;
+    const int part = (int)min(chunk_size, n_total - ooff);
+    const uint64_t ioff = offsets[chunk];
+    const int cs = (int)csizes[chunk];
+    const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+    Bytes rin, rout;
+    rin.init(packed + ioff, readable);
+    rout.init(out + ooff, (uint64_t)part);
+    int r;
+    if (cs == part || codec == 2) {
+        copy_raw(rin, rout, part, lane);
+        r = part;
+    } else {
+        dec2::Sink O{(LDSA uint8_t*)win, rout, 0, 0};
+        r = codec == 0 ? dec2::lz4_decode(rin, cs, O, part, lane) : dec2::snappy_decode(rin, cs, O, part, lane);
+        if (r > 0) O.flush(r, lane);
+    }
+    if (lane == 0) status[chunk] = r;
+}
+
 // codec: 0 = lz4, 1 = snappy, 2 = raw copy only.  offsets[i] = byte offset of chunk i in
 // `packed`; a chunk whose csize equals its size was stored raw (lzbench.cpp:311-315).
 extern "C" __global__ void __launch_bounds__(64)
@@ -239,11 +480,17 @@ lzh_decompress_kernel(int codec, const uint8_t* packed, uint64_t packed_readable
 }
 
 #include "launch.h"
+#include <stdlib.h>
 hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                  const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                  int32_t* status, uint32_t nchunks, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(lzh_decompress_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
-                       offsets, csizes, n_total, chunk_size, out, status, 0u);
+    static const bool use_v2 = getenv("LZH_DEC_V2") && atoi(getenv("LZH_DEC_V2")) != 0;
+    if (!use_v2)
+        hipLaunchKernelGGL(lzh_decompress_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
+                           offsets, csizes, n_total, chunk_size, out, status, 0u);
+    else
+        hipLaunchKernelGGL(lzh_decompress_v2_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
+                           offsets, csizes, n_total, chunk_size, out, status, 0u);
     return hipGetLastError();
 }

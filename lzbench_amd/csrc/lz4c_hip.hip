@@ -145,6 +145,9 @@ struct SeqLayout {
 // Common case (<= 256 bytes, literals in the input ring): assembled in the output ring.
 __device__ __forceinline__ int emit_seq(const Bytes& in, const Ring& R, const Bytes& out, OutRing& O, int op,
                                         int anchor, int lit, bool has_match, int off, int ml, int lane) {
+#ifdef LZH_EXP_NOEMIT
+    if (has_match) return op + 3 + lit;
+#endif
     // (ml counts match bytes beyond the 4-byte minimum, as the token does)
     if (has_match && lit < 15 && ml < 15 && R.has(anchor, anchor + 16)) {
         // short sequence (no length bytes): token, lit literals, 2-byte offset

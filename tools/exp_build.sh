@@ -1,0 +1,19 @@
+#!/bin/bash
+# tools/exp_build.sh NAME "-DFLAG ..." -- build liblzbench_hip.so with extra defines into build/exp/NAME/
+# (kernel experiments; run with LZH_LIB=build/exp/NAME/liblzbench_hip.so)
+set -e
+name=$1; flags=$2
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/build/exp/$name
+mkdir -p $out
+cd $root/lzbench_amd/csrc
+objs=""
+for f in lz4_hip lz4c_hip snappy_hip snappyc_hip decode_hip pack_hip; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $flags -c $f.hip -o $out/$f.o &
+  objs="$objs $out/$f.o"
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $flags -x hip -c api.cpp -o $out/api.o &
+gcc -O2 -fPIC -c datagen.c -o $out/datagen.o &
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/liblzbench_hip.so $objs $out/api.o $out/datagen.o -lm -pthread
+echo built $out/liblzbench_hip.so
