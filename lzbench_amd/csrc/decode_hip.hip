@@ -47,6 +47,15 @@ struct Win {
         return (v >> (8 * (x & 3))) & 0xffu;
     }
     __device__ __forceinline__ bool covers(int p0, int p1) const { return p0 + sh >= wb && p1 + sh <= wb + 512; }
+    // per-lane 4 bytes at stream position pos (pos .. pos+3 inside the window)
+    __device__ __forceinline__ uint32_t lane_word(int pos) const {
+        const int x = pos + sh;
+        const int d = (x - wb) >> 2;
+        const uint32_t a0 = lane_gather(w0, d & 63), a1 = lane_gather(w1, d & 63);
+        const uint32_t b0 = lane_gather(w0, (d + 1) & 63), b1 = lane_gather(w1, (d + 1) & 63);
+        const uint32_t lo = d < 64 ? a0 : a1, hi = d + 1 < 64 ? b0 : b1;
+        return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)x & 3u);
+    }
     // per-lane byte at stream position pos (inside the window) via cross-lane permute
     __device__ __forceinline__ uint32_t lane_byte(int pos) const {
         const int x = pos + sh;
@@ -422,6 +431,170 @@ __device__ int snappy_decode(const Bytes& in, int cs, Sink& O, int cap, int lane
 
 }  // namespace dec2
 
+// ---------------------------------------------------------------------------------------
+// v3: LZ4 sequences decoded a group at a time.  Every lane parses "a token at ip + lane" from
+// the register window; a short scalar walk picks the real chain of short sequences (no
+// length bytes) and records them lane-indexed; then each lane assembles one output byte per
+// pass (its sequence found by a popcount over the sequence-start mask): literal bytes come
+// from the register window, match bytes from the LDS output window (byte-by-byte overlap
+// semantics through the source rule src = match_start - off + (k mod off)), in dependency
+// rounds when a source lies in the same pass.  Sequences the group path cannot take (length
+// bytes, the last sequence, any rule violation) run through the v2 per-sequence path, which
+// applies the reference acceptance rules.
+namespace dec3 {
+
+using dec2::kW;
+
+// decodes one sequence the v2 way; returns 0 = continue, 1 = done (last literals), <0 error
+__device__ __forceinline__ int lz4_one(const Bytes& in, int cs, dec2::Sink& O, Win& w, int cap, int& ip, int& op,
+                                       int lane) {
+    if (ip >= cs) return -ip - 1;
+    w.ensure(ip, lane);
+    const uint32_t tok = w.byte(ip++);
+    int lit = (int)(tok >> 4);
+    if (lit == 15) {
+        if (ip >= cs - 15) return -ip - 1;
+        for (int it = 0; it <= cs; it++) {
+            w.ensure(ip, lane);
+            const uint32_t s = w.byte(ip++);
+            lit += (int)s;
+            if (ip >= cs - 15 || s != 255) break;
+        }
+    }
+    if (op + lit > cap - 12 || ip + lit > cs - 8) {
+        if (ip + lit != cs || op + lit > cap) return -ip - 1;
+        O.literals(w, in, ip, op, lit, lane);
+        op += lit;
+        return 1;
+    }
+    O.literals(w, in, ip, op, lit, lane);
+    ip += lit;
+    op += lit;
+    w.ensure(ip, lane);
+    const int off = (int)(w.byte(ip) | (w.byte(ip + 1) << 8));
+    ip += 2;
+    int ml = (int)(tok & 15u);
+    if (ml == 15) {
+        for (int it = 0; it <= cs; it++) {
+            w.ensure(ip, lane);
+            const uint32_t s = w.byte(ip++);
+            ml += (int)s;
+            if (ip >= cs - 4) return -ip - 1;
+            if (s != 255) break;
+        }
+    }
+    ml += 4;
+    if (off > op) return -ip - 1;
+    if (op + ml > cap - 5) return -ip - 1;
+    if (off == 0) {
+        for (int base = 0; base < ml; base += LZH_WAVE) {
+            if (base + lane < ml) O.put(op + base + lane, 0);
+            O.maybe_flush(op + min(base + LZH_WAVE, ml), lane);
+        }
+    } else {
+        O.match(op, off, ml, lane);
+    }
+    op += ml;
+    return 0;
+}
+
+constexpr int kGroupOut = 4 * LZH_WAVE;      // output bytes per group (4 passes)
+
+__device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, int cap, int lane) {
+    if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
+    if (cs <= 0) return -1;
+    Win w;
+    w.bind(in);
+    w.load(0, lane);
+    int ip = 0, op = 0;
+    for (int guard = 0; guard <= cs; guard++) {
+        ip = unii(ip); op = unii(op);
+        O.flushed = unii(O.flushed); O.ringlo = unii(O.ringlo);
+        // ---- every lane parses a token at ip + lane
+        if (!w.covers(ip, ip + 2 * LZH_WAVE)) w.load(ip, lane);
+        const uint32_t tw = w.lane_word(ip + lane);
+        const uint32_t lit_l = (tw >> 4) & 15u, mlc_l = tw & 15u;
+        const uint32_t ow = w.lane_word(ip + lane + 1 + (int)lit_l);
+        const uint32_t info = (ow & 0xffffu) | (lit_l << 16) | (mlc_l << 20) |
+                              ((lit_l == 15u || mlc_l == 15u) ? (1u << 24) : 0u);
+        // ---- scalar walk over the chain of short sequences
+        uint32_t A = 0, B = 0;                  // lane k: sequence k (A: j | lit<<8 | mlc<<12, B: out start | off<<16)
+        uint64_t S0 = 0, S1 = 0, S2 = 0, S3 = 0;  // sequence starts in the group's output
+        int k = 0, o = 0, x = ip;
+        for (; k < LZH_WAVE; k++) {
+            const int j = x - ip;
+            if (j >= LZH_WAVE) break;
+            const uint32_t inf = rdlane(info, j);
+            const int lit = (int)((inf >> 16) & 15u), mlc = (int)((inf >> 20) & 15u), off = (int)(inf & 0xffffu);
+            if (inf >> 24) break;                                          // length bytes
+            const int opm = op + o + lit;
+            if (opm > cap - 12 || x + 1 + lit > cs - 8) break;             // last literals / malformed
+            if (off == 0 || off > opm || opm + mlc + 4 > cap - 5) break;   // left to the checked path
+            if (o + lit + mlc + 4 > kGroupOut) break;
+            A = (lane == k) ? ((uint32_t)j | ((uint32_t)lit << 8) | ((uint32_t)mlc << 12)) : A;
+            B = (lane == k) ? ((uint32_t)o | ((uint32_t)off << 16)) : B;
+            const uint64_t bit = 1ull << (o & 63);
+            if (o < 64) S0 |= bit; else if (o < 128) S1 |= bit; else if (o < 192) S2 |= bit; else S3 |= bit;
+            o += lit + mlc + 4;
+            x += 3 + lit;
+        }
+        if (k == 0) {
+            const int r = lz4_one(in, cs, O, w, cap, ip, op, lane);
+            if (r < 0) return r;
+            if (r == 1) break;
+            continue;
+        }
+        // ---- assemble the group's output, one byte per lane per pass
+        const int total = o;
+        int before = 0;                                 // sequence starts in earlier passes
+        for (int pass = 0; pass * LZH_WAVE < total; pass++) {
+            const uint64_t Sp = pass == 0 ? S0 : (pass == 1 ? S1 : (pass == 2 ? S2 : S3));
+            const int ob = pass * LZH_WAVE + lane;
+            const bool act = ob < total;
+            const int kk = before + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(Sp >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)Sp, 0u)) +
+                           (int)((Sp >> lane) & 1ull) - 1;
+            const uint32_t a = lane_gather(A, kk), b = lane_gather(B, kk);
+            const int jk = (int)(a & 255u), litk = (int)((a >> 8) & 15u);
+            const int ostart = (int)(b & 0xffffu), offk = (int)(b >> 16);
+            const int u = ob - ostart;
+            const bool is_lit = u < litk;
+            const uint32_t lb = w.lane_byte(ip + jk + 1 + (is_lit ? u : 0));
+            const int mu = u - litk;
+            const int mstart = op + ostart + litk;
+            const int src = mstart - offk + (mu < offk ? mu : (int)((uint32_t)mu % (uint32_t)max(offk, 1)));
+            const int pbase = op + pass * LZH_WAVE;
+            const bool near = !is_lit && src >= O.ringlo && src >= pbase + LZH_WAVE - kW;
+            const bool inpass = !is_lit && src >= pbase;
+            uint32_t v = is_lit ? lb : (near && !inpass ? O.get(src) : 0u);
+            bool done = is_lit || (near && !inpass);
+            const bool far = act && !is_lit && !near;
+            if (ballot(far)) {   // far sources were flushed long ago: their stores must be done
+                wait_vm();
+                if (far) v = O.out.b_sc1(src);
+                done = done || far;
+            }
+            if (act && done) O.put(op + ob, v);
+            uint64_t dm = ballot(act && done) | ~ballot(act);
+            for (int r = 0; r < LZH_WAVE && ~dm; r++) {
+                const bool pend = !((dm >> lane) & 1ull);
+                const int sl = src - pbase;
+                const bool ready = pend && ((dm >> (sl & 63)) & 1ull);
+                const uint32_t vv = O.get(src);
+                if (ready) O.put(op + ob, vv);
+                dm |= ballot(ready);
+            }
+            before += __builtin_popcountll(Sp);
+            O.maybe_flush(min(pbase + LZH_WAVE, op + total), lane);
+        }
+        op += total;
+        ip = x;
+    }
+    return op;
+}
+
+}  // namespace dec3
+
 extern "C" __global__ void __launch_bounds__(64)
 lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                          const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
@@ -444,7 +617,7 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
         r = part;
     } else {
         dec2::Sink O{(LDSA uint8_t*)win, rout, 0, 0};
-        r = codec == 0 ? dec2::lz4_decode(rin, cs, O, part, lane) : dec2::snappy_decode(rin, cs, O, part, lane);
+        r = codec == 0 ? dec3::lz4_decode(rin, cs, O, part, lane) : dec2::snappy_decode(rin, cs, O, part, lane);
         if (r > 0) O.flush(r, lane);
     }
     if (lane == 0) status[chunk] = r;
@@ -485,8 +658,8 @@ hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t pack
                                  const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                  int32_t* status, uint32_t nchunks, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
-    static const bool use_v2 = getenv("LZH_DEC_V2") && atoi(getenv("LZH_DEC_V2")) != 0;
-    if (!use_v2)
+    static const bool use_v1 = getenv("LZH_DEC_V1") && atoi(getenv("LZH_DEC_V1")) != 0;
+    if (use_v1)
         hipLaunchKernelGGL(lzh_decompress_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
                            offsets, csizes, n_total, chunk_size, out, status, 0u);
     else
