@@ -226,7 +226,10 @@ __device__ int snappy_decode(const Bytes& in, int cs, const Bytes& out, int cap,
 // L1-bypassing loads.
 namespace dec2 {
 
-constexpr int kW = 8192;
+#ifndef LZH_DEC_KW
+#define LZH_DEC_KW 8192
+#endif
+constexpr int kW = LZH_DEC_KW;   // LDS output window bytes (power of two)
 
 struct Sink {
     LDSA uint8_t* b;

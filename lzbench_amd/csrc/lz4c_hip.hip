@@ -21,7 +21,12 @@
 namespace lz4v3 {
 
 // optional per-kernel event counters (debug builds of the launch only; nullptr in production)
-#define LZ_STAT(i, v) do { if (kStats && lane == 0) atomicAdd(&stats[i], (unsigned long long)(v)); } while (0)
+// (counted per wave in registers, flushed once at the end: per-event atomics would serialize the run)
+#define LZ_STAT(i, v) do { if (kStats) ctr[i] += (uint32_t)(v); } while (0)
+constexpr int kCtr = 13;
+// phase clocks (stats build only): time since the previous mark is charged to phase i
+#define LZ_CLK(i) do { if (kStats) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); clk[i] += t_ - clk_last; clk_last = t_; } } while (0)
+constexpr int kClk = 10;
 
 constexpr int kMinMatch = 4;
 constexpr int kMfLimit = 12;
@@ -195,6 +200,63 @@ __device__ __forceinline__ int emit_seq(const Bytes& in, const Ring& R, const By
     return op;
 }
 
+// Wave-wide inclusive prefix sum (DPP row shifts + row broadcasts, no LDS round trip).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// Sequences found by one batch, one per member lane (the lane of the sequence's match start):
+// anchor, literal count, offset, match length - 4, first output byte within the batch's
+// output.  Emitted lane-parallel under the NEXT batch's candidate loads.  Plain locals (a
+// struct here ends up in scratch memory).
+#define RECS_DECL                                                                                  \
+    uint32_t rc_anc = 0, rc_lit = 0, rc_off = 0, rc_mlx = 0, rc_st = 0;                            \
+    uint64_t rc_m = 0;                                                                             \
+    int rc_tot = 0
+#define RECS_EMIT() op = emit_recs(in, R, out, O, op, rc_anc, rc_lit, rc_off, rc_mlx, rc_st, rc_m, rc_tot, lane)
+
+// Emit the records at op (returns the new op).  Common case (<= 256 bytes, literals in the
+// input ring): output byte t of the batch is lane t of pass t/64; its sequence is the last
+// member whose start is <= t.  Else sequence by sequence.
+__device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const Bytes& out, OutRing& O, int op,
+                                         uint32_t anc, uint32_t lit, uint32_t off, uint32_t mlx, uint32_t st,
+                                         uint64_t mem, int tot, int lane) {
+    if (mem == 0) return op;
+    const int first = __builtin_ctzll(mem), last = 63 - __builtin_clzll(mem);
+    const int a0 = rdlanei((int)anc, first), a1 = rdlanei((int)anc, last) + rdlanei((int)lit, last);
+    if (tot <= 4 * LZH_WAVE && R.has(a0, a1)) {
+        for (int pass = 0; pass * LZH_WAVE < tot; pass++) {
+            const int ob = pass * LZH_WAVE + lane;
+            int k = first;
+            for (uint64_t mm = mem & (mem - 1); mm; mm &= mm - 1) {
+                const int m = __builtin_ctzll(mm);
+                k = ob >= rdlanei((int)st, m) ? m : k;
+            }
+            const int a = (int)lane_gather(anc, k), l = (int)lane_gather(lit, k);
+            const int o = (int)lane_gather(off, k), m = (int)lane_gather(mlx, k);
+            const int t = ob - (int)lane_gather(st, k);
+            const SeqLayout S(l, true, m);
+            const uint32_t lb = R.byte(a + t - S.lit0);
+            if (ob < tot) O.put(op + ob, S.byte(t, lb, o));
+        }
+        op += tot;
+        if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
+        return op;
+    }
+    for (uint64_t mm = mem; mm; mm &= mm - 1) {
+        const int k = __builtin_ctzll(mm);
+        op = emit_seq(in, R, out, O, op, rdlanei((int)anc, k), rdlanei((int)lit, k), true, rdlanei((int)off, k),
+                      rdlanei((int)mlx, k), lane);
+    }
+    return op;
+}
+
 // Per-lane match evaluation of probe p against candidate c, from 28 bytes around each:
 //   P side  [p-4, p+24) from the input ring (or global memory),
 //   M side  [c-4, c+24) loaded speculatively for every lane in one 32-byte window.
@@ -287,7 +349,7 @@ __device__ __forceinline__ bool eval_lane(const PSide& P, const MWin& W, bool va
 // Returns bk; cnt = bytes matched past P+4.
 template <bool kStats>
 __device__ __forceinline__ int finish_match(const Bytes& in, int P, int M, int bkr, int len, int anchor, int mlimit,
-                                            int& cnt_out, int lane, unsigned long long* stats) {
+                                            int& cnt_out, int lane, uint32_t* ctr) {
     const int maxb = min(P - anchor, M);
     int bk = min(bkr, maxb);
     if (bkr == 4 && maxb > 4) {
@@ -324,6 +386,43 @@ __device__ __forceinline__ int finish_match(const Bytes& in, int P, int M, int b
     return bk;
 }
 
+// catch-up past the 4-byte window (lz4.c:1017-1020): bytes matched backwards from P / M,
+// bounded by the anchor and the block start; lane-parallel compare, 64 bytes per step
+__device__ __forceinline__ int slow_catchup(const Bytes& in, int P, int M, int anchor, int lane) {
+    int ip2 = P - 4, m2 = M - 4;
+    for (int it = 0; it < (1 << 12); it++) {
+        const int mb2 = min(ip2 - anchor, m2);
+        if (mb2 <= 0) break;
+        const bool e2b = lane < mb2 && in.b(ip2 - 1 - lane) == in.b(m2 - 1 - lane);
+        const int b = ffs64(ballot(!e2b));
+        ip2 -= b;
+        m2 -= b;
+        if (b < LZH_WAVE) break;
+    }
+    return P - ip2;
+}
+
+// LZ4_count past the 20-byte window (lz4.c:603-626): bytes matched after P+4 / M+4, from 20 on,
+// capped at matchlimit; lane-parallel compare, 256 bytes per step
+__device__ __forceinline__ int slow_count(const Bytes& in, int P, int M, int mlimit, int lane) {
+    const int a = P + kMinMatch;
+    int cnt = 20;
+    for (int it = 0; it < (1 << 10) && a + cnt < mlimit; it++) {
+        const int o = cnt + 4 * lane;
+        const uint32_t x = in.w32(a + o) ^ in.w32(M + kMinMatch + o);
+        const uint64_t ne = ballot(x != 0);
+        if (ne) {
+            const int l = ffs64(ne);
+            cnt += 4 * l + (int)byte_ctz(rdlane(x, l));
+            break;
+        }
+        cnt += 4 * LZH_WAVE;
+    }
+    return min(cnt, mlimit - a);
+}
+
+__device__ __forceinline__ int ctz64v(uint64_t x) { return x ? __builtin_ctzll(x) : 64; }
+
 __device__ __forceinline__ uint64_t lane_bits(int lo, int hi) {   // bits lo..hi (0 <= lo <= hi <= 63)
     return ((2ull << hi) - 1ull) & (~0ull << lo);                 // 2 << 63 wraps to 0: all ones
 }
@@ -355,6 +454,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                                unsigned long long* stats) {
     const int lane = threadIdx.x;
     Table<kSmall> T{tab};
+    uint64_t clk[kClk] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t ctr[kCtr] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t clk_last = kStats ? __builtin_amdgcn_s_memtime() : 0;
     if (n <= 0) {
         if (lane == 0) out.st8(0, 0);
         if (lane == 0) *out_size = 1;
@@ -373,8 +475,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
     wave_lds_fence();
 
     int op = 0, anchor = 0;
-    bool pend = false;                       // one sequence waits to be emitted
-    int p_anchor = 0, p_lit = 0, p_off = 0, p_ml = 0;
+    RECS_DECL;                               // sequences waiting to be emitted
 
     if (n >= kMinLength) {
         const int mfl1 = n - kMfLimit + 1;
@@ -398,10 +499,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         for (int guard = 0; go && guard < 4 * n + 64; guard++) {
             runb = unii(runb) != 0; retest = unii(retest) != 0;
             base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
-            op = unii(op); anchor = unii(anchor); pend = unii(pend) != 0;
-            p_anchor = unii(p_anchor); p_lit = unii(p_lit); p_off = unii(p_off); p_ml = unii(p_ml);
+            op = unii(op); anchor = unii(anchor); rc_tot = unii(rc_tot);
             R.fill = unii(R.fill); O.flushed = unii(O.flushed);
             LZ_STAT(0, 1);
+            LZ_CLK(9);                                                 // (loop overhead / uncharged)
 
             // ---- lanes -> positions
             int p;
@@ -439,6 +540,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             }
             if (!kSmall) b4 = ps.q0 & 0xffu;
             const uint32_t h = hash_of<kSmall>(ps.w, b4);
+            LZ_CLK(0);                                                 // lanes -> positions, P side, hash
             const uint32_t old = T.get(h);
             if (valid) T.put(h, (uint32_t)p);
             wave_lds_fence();
@@ -447,57 +549,142 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             uint32_t cand = old;
             MWin W;
             W.load(in, cand, valid);
+            LZ_CLK(1);                                                 // table read/claim/read back, loads issued
             // ---- deferred emission (LDS work under the loads above)
-            if (pend) {
-                op = emit_seq(in, R, out, O, op, p_anchor, p_lit, true, p_off, p_ml, lane);
-                pend = false;
-            }
+            RECS_EMIT();
+            rc_m = 0;
+            rc_tot = 0;
             {
                 const int target = min(front + in.sh + kAhead, endX + 256);
                 for (int r = 0; r < 4 && R.fill < target; r++) { R.refill(in.r, lane); LZ_STAT(12, 1); }
             }
+            LZ_CLK(2);                                                 // deferred emission + refill
             wait_vm();
             wave_lds_fence();
+            LZ_CLK(3);                                                 // exposed load wait
             int bkr, len;
             bool ok = eval_lane(ps, W, valid, bkr, len);
             if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
 
             if (runb) {
                 // ================= run batch: resolve every sequence that starts in the batch
-                const uint64_t okm = ballot(ok);
                 // a probe whose slot holds an earlier lane of the batch sees that lane's position
                 // if it was inserted (probed or ip-2 filled), else the slot's old value: such
                 // "colliders" are re-evaluated per step against the in-batch candidate
                 uint64_t grp = 1ull << lane;
                 uint64_t coll = 0;
+                int prev = -1;
+                bool okp = false;                                      // evaluation against lane prev
+                int bep = 0, lep = 0;
                 if (losers) {
                     LZ_STAT(1, 1);
-                    int prev;
                     slot_groups(h, valid, losers, grp, prev, lane);
                     coll = ballot(prev >= 0);
+                    // a collider's candidate is usually its closest earlier slot member: evaluate
+                    // that pair once per batch (the per-step test below then only selects)
+                    const int k = prev >= 0 ? prev : lane;
+                    const uint32_t gm4 = lane_gather(ps.m4, k), gw = lane_gather(ps.w, k),
+                                   g0 = lane_gather(ps.q0, k), g1 = lane_gather(ps.q1, k),
+                                   g2 = lane_gather(ps.q2, k), g3 = lane_gather(ps.q3, k),
+                                   g4 = lane_gather(ps.q4, k);
+                    const uint32_t x0 = ps.q0 ^ g0, x1 = ps.q1 ^ g1, x2 = ps.q2 ^ g2, x3 = ps.q3 ^ g3,
+                                   x4 = ps.q4 ^ g4;
+                    int l = 20;
+                    l = x4 ? 16 + (int)byte_ctz(x4) : l;
+                    l = x3 ? 12 + (int)byte_ctz(x3) : l;
+                    l = x2 ? 8 + (int)byte_ctz(x2) : l;
+                    l = x1 ? 4 + (int)byte_ctz(x1) : l;
+                    l = x0 ? (int)byte_ctz(x0) : l;
+                    lep = l;
+                    const uint32_t y = ps.m4 ^ gm4;
+                    bep = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
+                    okp = valid && gw == ps.w;
                 }
+                LZ_CLK(4);                                             // eval + slot groups
                 const uint64_t below = (1ull << lane) - 1ull;
                 const int fv = __builtin_popcountll(vmask);           // first lane past mflimit
-                uint64_t I = pins >= 0 ? (1ull << (pins - base)) : 0ull;   // lanes left in the table
-                pins = -1;
-                bool next_stride = false;
-                for (int it = 0; it < LZH_WAVE + 1; it++) {
-                    const int lo = q - base;
-                    const int hi = min(qlim - base, LZH_WAVE - 1);
-                    if (lo > hi) break;                                // batch done
-                    const uint64_t rm = lane_bits(lo, hi);
-                    uint64_t okx = okm;
-                    uint32_t ce = cand;
-                    int be = bkr, le = len;
-                    if (coll & rm) {
-                        // earlier slot members count as inserted if in I or probed in this step
-                        const uint64_t mk = grp & below & (I | (~0ull << lo));
-                        const int k = mk ? 63 - __builtin_clzll(mk) : lane;
+                const uint64_t I0 = pins >= 0 ? (1ull << (pins - base)) : 0ull;
+                const int lo = q - base, hi0 = min(qlim - base, LZH_WAVE - 1);
+                // Each lane's candidate: the latest earlier slot member that is inserted when the
+                // lane is probed (ak; -1 = the slot's old value).  Assume prev, resolve the batch,
+                // check the assumption against the resolved inserted set; repeat with corrected
+                // candidates until consistent (each round fixes a prefix of the batch).
+                int ak = prev;
+                bool oke = prev >= 0 ? okp : ok;
+                uint32_t ce = prev >= 0 ? (uint32_t)(base + prev) : cand;
+                int be = prev >= 0 ? bep : bkr, le = prev >= 0 ? lep : len;
+                uint64_t Mm = 0, I = I0;                               // member lanes (sequence starts)
+                int cn = 0, e = 0;                                     // per lane: match count, end lane
+                int eL = 0;                                            // end lane of the last member
+                bool endp = false;                                     // the parse ends in this batch
+                for (int round = 0; round <= LZH_WAVE; round++) {
+                    const uint64_t A = ballot(oke);
+                    // if lane l starts a sequence: match count, end lane, next hit at or after the end
+                    cn = min(le, mlimit - (p + kMinMatch));
+                    const bool lng = oke && le == 20 && p + kMinMatch + 20 < mlimit;
+                    e = lane + kMinMatch + cn;
+                    int f = ctz64v(e < LZH_WAVE ? (A & (~0ull << e)) : 0ull);
+                    // chain walk (lz4.c:1142-1200: match end -> re-test -> search from ip+1)
+                    Mm = 0;
+                    endp = false;
+                    uint64_t E;                                        // probed lanes
+                    const uint64_t r0 = A & lane_bits(lo, hi0);
+                    if (!r0) {
+                        E = lane_bits(lo, hi0);
+                        endp = hi0 >= fv;                              // ran past mflimit (lz4.c:969)
+                    } else {
+                        int sl = __builtin_ctzll(r0);
+                        bool endip = false;                            // a match ended past mflimit
+                        for (int it = 0; it < LZH_WAVE; it++) {
+                            Mm |= 1ull << sl;
+                            int es, fs;
+                            if (rdlane((uint32_t)lng, sl)) {           // match runs past the window
+                                LZ_STAT(6, 1);
+                                const int c = slow_count(in, base + sl, rdlanei((int)ce, sl), mlimit, lane);
+                                es = sl + kMinMatch + c;
+                                cn = lane == sl ? c : cn;
+                                e = lane == sl ? es : e;
+                                fs = ctz64v(es < LZH_WAVE ? (A & (~0ull << es)) : 0ull);
+                            } else {
+                                es = rdlanei(e, sl);
+                                fs = rdlanei(f, sl);
+                            }
+                            eL = es;
+                            if (base + es >= mfl1) { endip = true; break; }  // lz4.c:1142
+                            if (fs >= LZH_WAVE) break;
+                            sl = fs;
+                        }
+                        // lanes strictly inside a member's match are not probed; ip-2 is inserted
+                        const uint64_t mle = Mm & (below | (1ull << lane));
+                        const int j = mle ? 63 - __builtin_clzll(mle) : lane;
+                        const int ej = (int)lane_gather((uint32_t)e, j);
+                        const bool inside = mle && lane > j && lane < ej;
+                        E = ballot(lane >= lo && !inside && (!endip || lane < eL));
+                        I = ballot(mle && lane == ej - 2);             // lz4.c:1146
+                        endp = endip || (eL < LZH_WAVE && LZH_WAVE - 1 >= fv);   // or the search ran past mflimit
+                    }
+                    I |= I0 | E;
+                    if (!(coll & E)) break;
+                    const uint64_t mk = grp & below & I;
+                    const int kt = mk ? 63 - __builtin_clzll(mk) : -1;
+                    const bool fix = ((E >> lane) & 1ull) && kt != ak;
+                    if (!ballot(fix)) break;
+                    LZ_STAT(2, 1);
+                    const bool far = fix && kt >= 0 && kt != prev;
+                    if (fix) {
+                        ak = kt;
+                        oke = kt < 0 ? ok : okp;
+                        ce = kt < 0 ? cand : (uint32_t)(base + kt);
+                        be = kt < 0 ? bkr : bep;
+                        le = kt < 0 ? len : lep;
+                    }
+                    if (ballot(far)) {                                 // an older member than prev
+                        const int k = far ? kt : lane;
                         const uint32_t gm4 = lane_gather(ps.m4, k), gw = lane_gather(ps.w, k),
                                        g0 = lane_gather(ps.q0, k), g1 = lane_gather(ps.q1, k),
                                        g2 = lane_gather(ps.q2, k), g3 = lane_gather(ps.q3, k),
                                        g4 = lane_gather(ps.q4, k);
-                        if (mk) {
+                        if (far) {
                             const uint32_t x0 = ps.q0 ^ g0, x1 = ps.q1 ^ g1, x2 = ps.q2 ^ g2, x3 = ps.q3 ^ g3,
                                            x4 = ps.q4 ^ g4;
                             int l = 20;
@@ -509,44 +696,60 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                             le = l;
                             const uint32_t y = ps.m4 ^ gm4;
                             be = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
-                            ce = (uint32_t)(base + k);
+                            oke = valid && gw == ps.w;
                         }
-                        const bool okc = mk ? (valid && gw == ps.w) : ok;
-                        okx = ballot(okc);
                     }
-                    const uint64_t hm = okx & rm;
-                    if (!hm) {                                         // no match up to hi
-                        if (hi >= fv) { go = false; break; }           // ran past mflimit (lz4.c:969)
-                        I |= rm;
-                        q = base + hi + 1;
-                        if (hi == qlim - base) {                       // step 1 exhausted: stride batches
-                            next_stride = true;
-                            s = qlim - 63;
-                            k0 = LZH_WAVE;
-                            retest = false;
-                        }
-                        break;
-                    }
-                    const int fh = __builtin_ctzll(hm);               // valid lanes are a prefix: fh < fv
-                    I |= lane_bits(lo, fh);
-                    LZ_STAT(3, 1);
-                    const int P = base + fh;
-                    const int M = rdlanei((int)ce, fh);
-                    int cnt;
-                    const int bk = finish_match<kStats>(in, P, M, rdlanei(be, fh), rdlanei(le, fh), anchor, mlimit,
-                                                        cnt, lane, stats);
-                    if (pend) op = emit_seq(in, R, out, O, op, p_anchor, p_lit, true, p_off, p_ml, lane);
-                    pend = true;
-                    p_anchor = anchor; p_lit = P - bk - anchor; p_off = P - M; p_ml = bk + cnt;
-                    const int ip = P + kMinMatch + cnt;
-                    anchor = ip;
-                    if (ip >= mfl1) { go = false; break; }             // lz4.c:1142
-                    if (ip - 2 - base < LZH_WAVE) I |= 1ull << (ip - 2 - base);
-                    else pins = ip - 2;
-                    q = ip;                                            // re-test, then search from ip+1
-                    qlim = ip + LZH_WAVE;
                 }
-                if (go) {
+                LZ_CLK(5);                                             // chain resolve
+                // ---- records of the members (emitted under the next batch's loads)
+                if (Mm) {
+                    LZ_STAT(3, __builtin_popcountll(Mm));
+                    const bool mem = (Mm >> lane) & 1ull;
+                    const uint64_t mb = Mm & below;
+                    const int jp = mb ? 63 - __builtin_clzll(mb) : lane;
+                    const int ep = (int)lane_gather((uint32_t)e, jp);
+                    const int anc = mb ? base + ep : anchor;           // previous match end (or anchor)
+                    const int maxb = min(p - anc, (int)ce);
+                    int bk = min(be, maxb);
+                    const bool scu = mem && be == 4 && maxb > 4;       // catch-up past the window
+                    for (uint64_t sm = ballot(scu); sm; sm &= sm - 1) {
+                        LZ_STAT(5, 1);
+                        const int k = __builtin_ctzll(sm);
+                        const int b = slow_catchup(in, base + k, rdlanei((int)ce, k), rdlanei(anc, k), lane);
+                        bk = lane == k ? b : bk;
+                    }
+                    const int lit = p - bk - anc, mlx = bk + cn;
+                    const int L = mem ? 3 + lit + ext_len_bytes(lit) + ext_len_bytes(mlx) : 0;
+                    const int incl = wave_incl_scan(L);
+                    rc_anc = (uint32_t)anc;
+                    rc_lit = (uint32_t)lit;
+                    rc_off = (uint32_t)(p - (int)ce);
+                    rc_mlx = (uint32_t)mlx;
+                    rc_st = (uint32_t)(incl - L);
+                    rc_m = Mm;
+                    rc_tot = rdlanei(incl, 63);
+                }
+                LZ_CLK(6);                                             // records
+                if (endp) {
+                    go = false;
+                    if (Mm) anchor = base + eL;
+                } else {
+                    if (Mm) {
+                        const int ip = base + eL;
+                        anchor = ip;
+                        if (eL < LZH_WAVE) {                           // searched to the batch end
+                            q = base + LZH_WAVE;
+                            qlim = ip + LZH_WAVE;
+                            pins = -1;
+                        } else {                                       // re-test in a later batch
+                            q = ip;
+                            qlim = ip + LZH_WAVE;
+                            pins = eL - 2 >= LZH_WAVE ? ip - 2 : -1;
+                        }
+                    } else {
+                        q = base + hi0 + 1;
+                        pins = -1;
+                    }
                     // table: the last inserted lane of each slot, or the slot's old value
                     const bool inI = (I >> lane) & 1ull;
                     if (!losers) {
@@ -557,9 +760,16 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         if (wr) T.put(h, inI ? (uint32_t)p : old);
                     }
                     wave_lds_fence();
-                    if (next_stride) runb = false;
-                    else base = pins >= 0 ? pins : q;
+                    if (!Mm && hi0 == qlim - base) {                   // step 1 exhausted: stride batches
+                        runb = false;
+                        s = qlim - 63;
+                        k0 = LZH_WAVE;
+                        retest = false;
+                    } else {
+                        base = pins >= 0 ? pins : q;
+                    }
                 }
+                LZ_CLK(8);                                             // table restore
                 continue;
             }
 
@@ -608,9 +818,17 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 const int M = rdlanei((int)cand, fh);
                 int cnt;
                 const int bk = finish_match<kStats>(in, P, M, rdlanei(bkr, fh), rdlanei(len, fh), anchor, mlimit, cnt,
-                                                    lane, stats);
-                pend = true;
-                p_anchor = anchor; p_lit = P - bk - anchor; p_off = P - M; p_ml = bk + cnt;
+                                                    lane, ctr);
+                {
+                    const int lit = P - bk - anchor, mlx = bk + cnt;
+                    rc_anc = (uint32_t)anchor;
+                    rc_lit = (uint32_t)lit;
+                    rc_off = (uint32_t)(P - M);
+                    rc_mlx = (uint32_t)mlx;
+                    rc_st = 0;
+                    rc_m = 1;
+                    rc_tot = 3 + lit + ext_len_bytes(lit) + ext_len_bytes(mlx);
+                }
                 const int ip = P + kMinMatch + cnt;
                 anchor = ip;
                 if (ip >= mfl1) {
@@ -635,10 +853,14 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             }
         }
     }
-    if (pend) op = emit_seq(in, R, out, O, op, p_anchor, p_lit, true, p_off, p_ml, lane);
+    RECS_EMIT();
     op = emit_seq(in, R, out, O, op, anchor, n - anchor, false, 0, 0, lane);
     O.flush(out, op, lane);
     if (lane == 0) *out_size = (uint32_t)op;
+    if (kStats && lane == 0) {
+        for (int i = 0; i < kCtr; i++) atomicAdd(&stats[i], (unsigned long long)ctr[i]);
+        for (int i = 0; i < kClk; i++) atomicAdd(&stats[13 + i], (unsigned long long)clk[i]);
+    }
 }
 
 }  // namespace lz4v3

@@ -7,10 +7,10 @@ lib = L.lib()
 f = lib.lzh_debug_lz4_stats
 f.restype = C.c_int
 f.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
-names = ["batches", "collision_batches", "-", "sequences", "-", "catchup_slow", "count_slow", "-",
+names = ["batches", "collision_batches", "slow_colliders", "sequences", "-", "catchup_slow", "count_slow", "-",
          "-", "hash_ring_miss", "-", "-", "refills", "-", "-", "-"]
 for corpus in sys.argv[1:] or ["text", "json"]:
-    n = 64 << 20
+    n = int(os.environ.get("STATS_MIB", "512")) << 20
     host = L.datagen(corpus, n, seed=12345)
     d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda"); d_in[:n].copy_(torch.from_numpy(host))
     dc = L.DeviceCodec("lz4", n, 65536)
@@ -21,3 +21,7 @@ for corpus in sys.argv[1:] or ["text", "json"]:
     v = st.cpu().tolist()
     k = n // 65536
     print(corpus, {names[i]: round(v[i] / k, 2) for i in range(13) if names[i] != '-'}, "per chunk")
+    clk = ["probe+hash", "table+loads", "defer_emit+refill", "load_wait", "eval+groups", "coll_reeval",
+           "finish_match", "inbatch_emit", "table_restore", "other(stride,loop)"]
+    tot = sum(v[13:23]) or 1
+    print("  clocks/chunk %.0f:" % (tot / k), {clk[i]: "%.1f%%" % (100 * v[13 + i] / tot) for i in range(10)})
