@@ -227,7 +227,7 @@ __device__ int snappy_decode(const Bytes& in, int cs, const Bytes& out, int cap,
 namespace dec2 {
 
 #ifndef LZH_DEC_KW
-#define LZH_DEC_KW 8192
+#define LZH_DEC_KW 4096
 #endif
 constexpr int kW = LZH_DEC_KW;   // LDS output window bytes (power of two)
 
@@ -598,11 +598,153 @@ __device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, int cap, int l
 
 }  // namespace dec3
 
+// ---------------------------------------------------------------------------------------
+// v4: LZ4 groups resolved lane-parallel.  Every lane parses "a sequence at ip + lane" in full
+// (token, one literal-length byte, offset, one match-length byte) from the register window; a
+// scalar walk over the per-lane next-token links picks the real chain (a few instructions per
+// sequence); the reference acceptance rules are checked per member lane against a DPP prefix
+// sum of the output lengths, and the chain is cut before the first member that fails them (it,
+// the last sequence and sequences with 255-run lengths go through the checked v2 path).  Output
+// bytes are assembled one per lane per pass: the owning sequence is found from per-pass start
+// marks in LDS, literal bytes come from the register window, match bytes from the LDS output
+// window (or global memory for far sources) in dependency rounds.
+namespace dec4 {
+
+using dec2::kW;
+
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+__device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
+    if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
+    if (cs <= 0) return -1;
+    Win w;
+    w.bind(in);
+    w.load(0, lane);
+    int ip = 0, op = 0;
+    for (int guard = 0; guard <= cs; guard++) {
+        ip = unii(ip); op = unii(op);
+        O.flushed = unii(O.flushed); O.ringlo = unii(O.ringlo);
+        if (!w.covers(ip, ip + 2 * LZH_WAVE)) w.load(ip, lane);
+        // ---- every lane parses a whole sequence at x = ip + lane (lz4.c:1707-1729, :1929-2151)
+        const int x = ip + lane;
+        const uint32_t tw = w.lane_word(x);
+        const int ln = (int)((tw >> 4) & 15u), mc = (int)(tw & 15u), b1 = (int)((tw >> 8) & 255u);
+        const int lit = ln == 15 ? 15 + b1 : ln;
+        const int p1 = x + 1 + (ln == 15 ? 1 : 0);                // first literal byte
+        const int po = p1 + lit;                                    // offset bytes
+        const bool inwin = w.covers(po, po + 4);
+        const uint32_t ow = w.lane_word(inwin ? po : x);
+        const int off = (int)(ow & 0xffffu), b2 = (int)((ow >> 16) & 255u);
+        const int ml = mc == 15 ? 19 + b2 : mc + 4;
+        const int pe = po + 2 + (mc == 15 ? 1 : 0);                 // next token
+        const bool cplx = !inwin || (ln == 15 && b1 == 255) || (mc == 15 && b2 == 255);
+        const int link = cplx ? 255 : pe - ip;
+        // ---- the real chain from lane 0
+        uint64_t M = 0;
+        int j = 0;
+        for (int it = 0; it < LZH_WAVE; it++) {
+            const int nj = rdlanei(link, j);
+            if (nj == 255) break;
+            M |= 1ull << j;
+            if (nj >= LZH_WAVE) break;
+            j = nj;
+        }
+        // ---- acceptance rules per member (as lz4_one); the chain ends before the first failure
+        const bool mem = (M >> lane) & 1ull;
+        const int L = mem ? lit + ml : 0;
+        const int incl = wave_incl_scan(L);
+        const int excl = incl - L;
+        const int opm = op + excl + lit;
+        const bool bad = mem && (x >= cs || (ln == 15 && x + 1 >= cs - 15) || opm > cap - 12 || p1 + lit > cs - 8 ||
+                                 (mc == 15 && po + 3 >= cs - 4) || off == 0 || off > opm || opm + ml > cap - 5);
+        const uint64_t badm = ballot(bad);
+        const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
+        if (!keep) {
+            const int r = dec3::lz4_one(in, cs, O, w, cap, ip, op, lane);
+            if (r < 0) return r;
+            if (r == 1) break;
+            continue;
+        }
+        const int lastk = 63 - __builtin_clzll(keep);
+        const int total = rdlanei(incl, lastk);
+        const int ip_next = ip + rdlanei(pe - ip, lastk);
+        // member data, packed for the per-byte gathers
+        const uint32_t pA = (uint32_t)lit | ((uint32_t)ml << 16);
+        const uint32_t pB = (uint32_t)(p1 - ip) | ((uint32_t)off << 16);
+        const bool kmem = (keep >> lane) & 1ull;
+        // ---- assemble the group's output, one byte per lane per pass
+        int carry = lastk;                                          // (pass 0 always has a start at 0)
+        for (int pass = 0; pass * LZH_WAVE < total; pass++) {
+            const int pb = pass * LZH_WAVE;
+            mark[lane] = 0xff;
+            wave_lds_fence();
+            if (kmem && excl >= pb && excl < pb + LZH_WAVE) mark[excl - pb] = (uint8_t)lane;
+            wave_lds_fence();
+            const int mv = (int)mark[lane];
+            const uint64_t S = ballot(mv != 0xff);
+            const uint64_t le = S & ((2ull << lane) - 1ull);
+            const int js = le ? 63 - __builtin_clzll(le) : lane;
+            const int own_here = (int)lane_gather((uint32_t)mv, js);
+            const int k = le ? own_here : carry;
+            carry = rdlanei(k, 63);
+            const uint32_t a = lane_gather(pA, k), b = lane_gather(pB, k);
+            const int ek = (int)lane_gather((uint32_t)excl, k);
+            const int litk = (int)(a & 0xffffu), offk = (int)(b >> 16);
+            const int ob = pb + lane;
+            const bool act = ob < total;
+            const int u = ob - ek;
+            const bool is_lit = u < litk;
+            const uint32_t lb = w.lane_byte(ip + (int)(b & 0xffffu) + (is_lit ? u : 0));
+            const int mu = u - litk;
+            const int mstart = op + ek + litk;
+            int src = mstart - offk + mu;
+            if (ballot(act && !is_lit && mu >= offk)) {              // overlapping copy: period offk
+                if (!is_lit && mu >= offk) src = mstart - offk + (int)((uint32_t)mu % (uint32_t)max(offk, 1));
+            }
+            const int pbase = op + pb;
+            const bool near = !is_lit && src >= O.ringlo && src >= pbase + LZH_WAVE - kW;
+            const bool inpass = !is_lit && src >= pbase;
+            uint32_t v = is_lit ? lb : (near && !inpass ? O.get(src) : 0u);
+            bool done = is_lit || (near && !inpass);
+            const bool far = act && !is_lit && !near;
+            if (ballot(far)) {   // far sources were flushed long ago: their stores must be done
+                wait_vm();
+                if (far) v = O.out.b_sc1(src);
+                done = done || far;
+            }
+            if (act && done) O.put(op + ob, v);
+            uint64_t dm = ballot(act && done) | ~ballot(act);
+            for (int r = 0; r < LZH_WAVE && ~dm; r++) {
+                const bool pend = !((dm >> lane) & 1ull);
+                const int sl = src - pbase;
+                const bool ready = pend && ((dm >> (sl & 63)) & 1ull);
+                const uint32_t vv = O.get(src);
+                if (ready) O.put(op + ob, vv);
+                dm |= ballot(ready);
+            }
+            O.maybe_flush(min(pbase + LZH_WAVE, op + total), lane);
+        }
+        op += total;
+        ip = ip_next;
+    }
+    return op;
+}
+
+}  // namespace dec4
+
 extern "C" __global__ void __launch_bounds__(64)
 lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                          const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                          int32_t* status, uint32_t chunk0) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[dec2::kW];
+    __shared__ __attribute__((aligned(16))) uint8_t win[dec2::kW + LZH_WAVE];   // output window | start marks
     const int lane = threadIdx.x;
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t ooff = chunk * chunk_size;
@@ -620,7 +762,12 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
         r = part;
     } else {
         dec2::Sink O{(LDSA uint8_t*)win, rout, 0, 0};
+#ifdef LZH_DEC_V3
         r = codec == 0 ? dec3::lz4_decode(rin, cs, O, part, lane) : dec2::snappy_decode(rin, cs, O, part, lane);
+#else
+        r = codec == 0 ? dec4::lz4_decode(rin, cs, O, (LDSA uint8_t*)win + dec2::kW, part, lane)
+                       : dec2::snappy_decode(rin, cs, O, part, lane);
+#endif
         if (r > 0) O.flush(r, lane);
     }
     if (lane == 0) status[chunk] = r;

@@ -25,7 +25,7 @@ namespace lz4v3 {
 #define LZ_STAT(i, v) do { if (kStats) ctr[i] += (uint32_t)(v); } while (0)
 constexpr int kCtr = 13;
 // phase clocks (stats build only): time since the previous mark is charged to phase i
-#define LZ_CLK(i) do { if (kStats) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); clk[i] += t_ - clk_last; clk_last = t_; } } while (0)
+#define LZ_CLK(i) do { if (!kStats) asm volatile("; LZMARK " #i ::: "memory"); if (kStats) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); clk[i] += t_ - clk_last; clk_last = t_; } } while (0)
 constexpr int kClk = 10;
 
 constexpr int kMinMatch = 4;
