@@ -63,11 +63,14 @@ __device__ __forceinline__ uint32_t hash_of(uint32_t w32, uint32_t b4) {
 }
 
 // LDS ring over descriptor offsets X = p + sh: holds [fill - kRing, fill).
+// Refills are LDS-DMA (buffer_load ... lds) issued after a batch's load wait, so they complete
+// under the next batch: `ready` is the fill level known to have landed (set at each wait).
 struct Ring {
     LDSA uint32_t* w;
     int sh;
     int fill;
-    __device__ __forceinline__ bool has(int p0, int p1) const { return p0 + sh >= fill - kRing && p1 + sh <= fill; }
+    int ready;
+    __device__ __forceinline__ bool has(int p0, int p1) const { return p0 + sh >= fill - kRing && p1 + sh <= ready; }
     __device__ __forceinline__ uint32_t dword(int a) const {
         return ((volatile const LDSA uint32_t*)w)[(a >> 2) & (kRing / 4 - 1)];
     }
@@ -97,6 +100,9 @@ struct OutRing {
     int flushed;          // output bytes [0, flushed) are in global memory
     __device__ __forceinline__ void put(int pos, uint32_t v) const {
         ((volatile LDSA uint8_t*)b)[(pos + sh) & (kOut - 1)] = (uint8_t)v;
+    }
+    __device__ __forceinline__ uint32_t get(int pos) const {
+        return ((volatile const LDSA uint8_t*)b)[(pos + sh) & (kOut - 1)];
     }
     __device__ __forceinline__ uint32_t dword(int X) const {
         return ((volatile const LDSA uint32_t*)b)[(X & (kOut - 1)) >> 2];
@@ -231,23 +237,40 @@ __device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const B
     const int first = __builtin_ctzll(mem), last = 63 - __builtin_clzll(mem);
     const int a0 = rdlanei((int)anc, first), a1 = rdlanei((int)anc, last) + rdlanei((int)lit, last);
     if (tot <= 4 * LZH_WAVE && R.has(a0, a1)) {
+        int carry = first;
         for (int pass = 0; pass * LZH_WAVE < tot; pass++) {
             const int ob = pass * LZH_WAVE + lane;
-            int k = first;
-            for (uint64_t mm = mem & (mem - 1); mm; mm &= mm - 1) {
-                const int m = __builtin_ctzll(mm);
-                k = ob >= rdlanei((int)st, m) ? m : k;
-            }
+            // owner of output byte ob: the last member starting at or before it.  Start marks go
+            // into this pass's own (not yet written) output bytes of the ring: cleared to 0xff,
+            // each member writes its lane at its start, every lane reads its byte back.
+            O.put(op + ob, 0xffu);
+            wave_lds_fence();
+            const int stl = (int)st;
+            if (((mem >> lane) & 1ull) && stl >= pass * LZH_WAVE && stl < (pass + 1) * LZH_WAVE)
+                O.put(op + stl, (uint32_t)lane);
+            wave_lds_fence();
+            const int mv = (int)O.get(op + ob);
+            const uint64_t smask = ballot(mv != 0xff);
+            const uint64_t le = smask & ((2ull << lane) - 1ull);
+            const int own = (int)lane_gather((uint32_t)mv, le ? 63 - __builtin_clzll(le) : lane);
+            const int k = le ? own : carry;
+            carry = rdlanei(k, 63);
             const int a = (int)lane_gather(anc, k), l = (int)lane_gather(lit, k);
             const int o = (int)lane_gather(off, k), m = (int)lane_gather(mlx, k);
             const int t = ob - (int)lane_gather(st, k);
             const SeqLayout S(l, true, m);
+#ifdef LZH_EXP_NOLB
+            const uint32_t lb = a;
+#else
             const uint32_t lb = R.byte(a + t - S.lit0);
+#endif
+#ifdef LZH_EXP_NOPUT
+            if (S.byte(t, lb, o) == 12345) O.put(op + ob, 1);
+#else
             if (ob < tot) O.put(op + ob, S.byte(t, lb, o));
+#endif
         }
-        op += tot;
-        if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
-        return op;
+        return op + tot;      // (flushed by the caller after its load wait: no store in that wait)
     }
     for (uint64_t mm = mem; mm; mm &= mm - 1) {
         const int k = __builtin_ctzll(mm);
@@ -467,11 +490,12 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
 #pragma unroll
         for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
     }
-    Ring R{ringw, in.sh, 0};
+    Ring R{ringw, in.sh, 0, 0};
     OutRing O{outb, out.sh, 0};
     const int endX = n + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
     wait_vm();
+    R.ready = R.fill;
     wave_lds_fence();
 
     int op = 0, anchor = 0;
@@ -500,7 +524,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             runb = unii(runb) != 0; retest = unii(retest) != 0;
             base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
             op = unii(op); anchor = unii(anchor); rc_tot = unii(rc_tot);
-            R.fill = unii(R.fill); O.flushed = unii(O.flushed);
+            R.fill = unii(R.fill); R.ready = unii(R.ready); O.flushed = unii(O.flushed);
             LZ_STAT(0, 1);
             LZ_CLK(9);                                                 // (loop overhead / uncharged)
 
@@ -554,14 +578,17 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             RECS_EMIT();
             rc_m = 0;
             rc_tot = 0;
+            LZ_CLK(2);                                                 // deferred emission
+            wait_vm();
+            R.ready = R.fill;
+            wave_lds_fence();
+            LZ_CLK(3);                                                 // exposed load wait
+            // ring refill and output flush after the wait: they complete under the next batch
             {
                 const int target = min(front + in.sh + kAhead, endX + 256);
                 for (int r = 0; r < 4 && R.fill < target; r++) { R.refill(in.r, lane); LZ_STAT(12, 1); }
             }
-            LZ_CLK(2);                                                 // deferred emission + refill
-            wait_vm();
-            wave_lds_fence();
-            LZ_CLK(3);                                                 // exposed load wait
+            if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
             int bkr, len;
             bool ok = eval_lane(ps, W, valid, bkr, len);
             if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
@@ -795,6 +822,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 if (prev >= 0) cand = ppos;
                 W.load(in, cand, valid);
                 wait_vm();
+                R.ready = R.fill;
                 ok = eval_lane(ps, W, valid, bkr, len);
                 if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
                 hits = ballot(ok);
@@ -853,7 +881,11 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             }
         }
     }
+    wait_vm();
+    R.ready = R.fill;
+    wave_lds_fence();
     RECS_EMIT();
+    if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
     op = emit_seq(in, R, out, O, op, anchor, n - anchor, false, 0, 0, lane);
     O.flush(out, op, lane);
     if (lane == 0) *out_size = (uint32_t)op;
