@@ -69,6 +69,19 @@ def cpu_baseline(sample: np.ndarray, codec: str, chunk: int, level: int, iters: 
     }, packed, cs
 
 
+def traffic_for(kernel):
+    """HBM-side bytes per dispatch of `kernel` from the committed PMC profile (profiles/traffic.json,
+    written by tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes on the
+    same workload), or None when no profile covers this kernel/workload."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            k = json.load(f)["kernels"].get(kernel)
+        return None if k is None else int(k["traffic_bytes_per_dispatch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def kernel_name(codec):
     """Compressor kernel the C-ABI launches for `codec` (api.cpp lzh_compress_kernel_only)."""
     if codec == "snappy":
@@ -175,6 +188,8 @@ def main():
 
     algo_bytes = n + comp_total                      # compress reads N, writes C
     achieved = algo_bytes / (k_ms * 1e-3) / 1e9
+    dec_achieved = algo_bytes / (d_ms * 1e-3) / 1e9   # decompress reads C, writes N
+    default_workload = args.codec == "lz4" and args.chunk_kib == 64 and args.corpus == "text" and args.size_mib == 1024
     total_bytes = world * n * args.steps
     value = total_bytes / elapsed / 1e6
     res = {
@@ -205,10 +220,21 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": None,
+            "traffic": traffic_for(kernel_name(args.codec)) if default_workload else None,
+            "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE + WRITE_SIZE, raw KiB x 1024, per launch)",
             "kernel": kernel_name(args.codec),
             "kernel_ms": round(k_ms, 3),
             "algorithmic_bytes_per_launch": int(algo_bytes),
+        },
+        "roofline_decompress": {
+            "bound": "hbm",
+            "achieved": round(dec_achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(dec_achieved / HBM_PEAK_GBS, 5),
+            "traffic": traffic_for("lzh_decompress_v2_kernel") if default_workload else None,
+            "kernel": "lzh_decompress_v2_kernel",
+            "kernel_ms": round(d_ms, 3),
         },
         "cpu_baseline": cpu,
         "ratio_pct": round(100 * ratio, 3),
