@@ -601,11 +601,29 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 uint64_t grp = 1ull << lane;
                 uint64_t coll = 0;
                 int prev = -1;
+                const uint64_t below = (1ull << lane) - 1ull;
                 bool okp = false;                                      // evaluation against lane prev
                 int bep = 0, lep = 0;
+#ifdef LZH_EXP_NOGROUPS
+                if (false) {
+#else
                 if (losers) {
+#endif
                     LZ_STAT(1, 1);
-                    slot_groups(h, valid, losers, grp, prev, lane);
+                    // slot groups without a loop: every lane of a slot read back the same claim
+                    // winner W (whichever lane the hardware let win), so equal W <=> same slot;
+                    // equality of the 6-bit W is bit-sliced over 6 ballots
+                    const uint32_t W = back - (uint32_t)base;
+                    uint64_t eq = vmask;
+#pragma unroll
+                    for (int b = 0; b < 6; b++) {
+                        const bool wb = (W >> b) & 1u;
+                        const uint64_t bm = ballot(valid && wb);
+                        eq &= wb ? bm : ~bm;
+                    }
+                    grp = valid ? eq : (1ull << lane);
+                    const uint64_t eb = grp & below;
+                    prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
                     coll = ballot(prev >= 0);
                     // a collider's candidate is usually its closest earlier slot member: evaluate
                     // that pair once per batch (the per-step test below then only selects)
@@ -628,7 +646,6 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     okp = valid && gw == ps.w;
                 }
                 LZ_CLK(4);                                             // eval + slot groups
-                const uint64_t below = (1ull << lane) - 1ull;
                 const int fv = __builtin_popcountll(vmask);           // first lane past mflimit
                 const uint64_t I0 = pins >= 0 ? (1ull << (pins - base)) : 0ull;
                 const int lo = q - base, hi0 = min(qlim - base, LZH_WAVE - 1);
@@ -695,6 +712,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         endp = endip || (eL < LZH_WAVE && LZH_WAVE - 1 >= fv);   // or the search ran past mflimit
                     }
                     I |= I0 | E;
+#ifdef LZH_EXP_NOVERIFY
+                    break;
+#endif
                     if (!(coll & E)) break;
                     const uint64_t mk = grp & below & I;
                     const int kt = mk ? 63 - __builtin_clzll(mk) : -1;
@@ -783,6 +803,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     }
                     // table: the last inserted lane of each slot, or the slot's old value
                     const bool inI = (I >> lane) & 1ull;
+#ifdef LZH_EXP_NORESTORE
+                    if (true) {} else
+#endif
                     if (!losers) {
                         if (valid && !inI) T.put(h, old);
                     } else {
