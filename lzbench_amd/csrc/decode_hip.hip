@@ -622,6 +622,68 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
+// Assemble a group's output [op, op + total): sequence k (member lane k, output start excl) is
+// litk literal bytes from stream position ip + lrel, then mlk match bytes copied from offset offk
+// (byte-by-byte semantics); a literal-only member has mlk = 0, a copy-only member litk = 0.
+// One output byte per lane per pass; the owner is the last start mark at or before the byte.
+__device__ __forceinline__ void emit_group(const Win& w, dec2::Sink& O, LDSA uint8_t* mark, int ip, int op,
+                                           int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
+                                           int off, int lane) {
+    const bool kmem = (keep >> lane) & 1ull;
+    int carry = 63 - __builtin_clzll(keep);                      // (pass 0 always has a start at 0)
+    for (int pass = 0; pass * LZH_WAVE < total; pass++) {
+        const int pb = pass * LZH_WAVE;
+        mark[lane] = 0xff;
+        wave_lds_fence();
+        if (kmem && excl >= pb && excl < pb + LZH_WAVE) mark[excl - pb] = (uint8_t)lane;
+        wave_lds_fence();
+        const int mv = (int)mark[lane];
+        const uint64_t S = ballot(mv != 0xff);
+        const uint64_t le = S & ((2ull << lane) - 1ull);
+        const int js = le ? 63 - __builtin_clzll(le) : lane;
+        const int own_here = (int)lane_gather((uint32_t)mv, js);
+        const int k = le ? own_here : carry;
+        carry = rdlanei(k, 63);
+        const uint32_t a = lane_gather(pA, k), b = lane_gather(lrel, k);
+        const int ek = (int)lane_gather((uint32_t)excl, k);
+        const int offk = (int)lane_gather((uint32_t)off, k);
+        const int litk = (int)(a & 0xffffu);
+        const int ob = pb + lane;
+        const bool act = ob < total;
+        const int u = ob - ek;
+        const bool is_lit = u < litk;
+        const uint32_t lb = w.lane_byte(ip + (int)b + (is_lit ? u : 0));
+        const int mu = u - litk;
+        const int mstart = op + ek + litk;
+        int src = mstart - offk + mu;
+        if (ballot(act && !is_lit && mu >= offk)) {                // overlapping copy: period offk
+            if (!is_lit && mu >= offk) src = mstart - offk + (int)((uint32_t)mu % (uint32_t)max(offk, 1));
+        }
+        const int pbase = op + pb;
+        const bool near = !is_lit && src >= O.ringlo && src >= pbase + LZH_WAVE - kW;
+        const bool inpass = !is_lit && src >= pbase;
+        uint32_t v = is_lit ? lb : (near && !inpass ? O.get(src) : 0u);
+        bool done = is_lit || (near && !inpass);
+        const bool far = act && !is_lit && !near;
+        if (ballot(far)) {   // far sources were flushed long ago: their stores must be done
+            wait_vm();
+            if (far) v = O.out.b_sc1(src);
+            done = done || far;
+        }
+        if (act && done) O.put(op + ob, v);
+        uint64_t dm = ballot(act && done) | ~ballot(act);
+        for (int r = 0; r < LZH_WAVE && ~dm; r++) {
+            const bool pend = !((dm >> lane) & 1ull);
+            const int sl = src - pbase;
+            const bool ready = pend && ((dm >> (sl & 63)) & 1ull);
+            const uint32_t vv = O.get(src);
+            if (ready) O.put(op + ob, vv);
+            dm |= ballot(ready);
+        }
+        O.maybe_flush(min(pbase + LZH_WAVE, op + total), lane);
+    }
+}
+
 __device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
     if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
     if (cs <= 0) return -1;
@@ -676,66 +738,136 @@ __device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_t* 
         const int lastk = 63 - __builtin_clzll(keep);
         const int total = rdlanei(incl, lastk);
         const int ip_next = ip + rdlanei(pe - ip, lastk);
-        // member data, packed for the per-byte gathers
-        const uint32_t pA = (uint32_t)lit | ((uint32_t)ml << 16);
-        const uint32_t pB = (uint32_t)(p1 - ip) | ((uint32_t)off << 16);
-        const bool kmem = (keep >> lane) & 1ull;
-        // ---- assemble the group's output, one byte per lane per pass
-        int carry = lastk;                                          // (pass 0 always has a start at 0)
-        for (int pass = 0; pass * LZH_WAVE < total; pass++) {
-            const int pb = pass * LZH_WAVE;
-            mark[lane] = 0xff;
-            wave_lds_fence();
-            if (kmem && excl >= pb && excl < pb + LZH_WAVE) mark[excl - pb] = (uint8_t)lane;
-            wave_lds_fence();
-            const int mv = (int)mark[lane];
-            const uint64_t S = ballot(mv != 0xff);
-            const uint64_t le = S & ((2ull << lane) - 1ull);
-            const int js = le ? 63 - __builtin_clzll(le) : lane;
-            const int own_here = (int)lane_gather((uint32_t)mv, js);
-            const int k = le ? own_here : carry;
-            carry = rdlanei(k, 63);
-            const uint32_t a = lane_gather(pA, k), b = lane_gather(pB, k);
-            const int ek = (int)lane_gather((uint32_t)excl, k);
-            const int litk = (int)(a & 0xffffu), offk = (int)(b >> 16);
-            const int ob = pb + lane;
-            const bool act = ob < total;
-            const int u = ob - ek;
-            const bool is_lit = u < litk;
-            const uint32_t lb = w.lane_byte(ip + (int)(b & 0xffffu) + (is_lit ? u : 0));
-            const int mu = u - litk;
-            const int mstart = op + ek + litk;
-            int src = mstart - offk + mu;
-            if (ballot(act && !is_lit && mu >= offk)) {              // overlapping copy: period offk
-                if (!is_lit && mu >= offk) src = mstart - offk + (int)((uint32_t)mu % (uint32_t)max(offk, 1));
-            }
-            const int pbase = op + pb;
-            const bool near = !is_lit && src >= O.ringlo && src >= pbase + LZH_WAVE - kW;
-            const bool inpass = !is_lit && src >= pbase;
-            uint32_t v = is_lit ? lb : (near && !inpass ? O.get(src) : 0u);
-            bool done = is_lit || (near && !inpass);
-            const bool far = act && !is_lit && !near;
-            if (ballot(far)) {   // far sources were flushed long ago: their stores must be done
-                wait_vm();
-                if (far) v = O.out.b_sc1(src);
-                done = done || far;
-            }
-            if (act && done) O.put(op + ob, v);
-            uint64_t dm = ballot(act && done) | ~ballot(act);
-            for (int r = 0; r < LZH_WAVE && ~dm; r++) {
-                const bool pend = !((dm >> lane) & 1ull);
-                const int sl = src - pbase;
-                const bool ready = pend && ((dm >> (sl & 63)) & 1ull);
-                const uint32_t vv = O.get(src);
-                if (ready) O.put(op + ob, vv);
-                dm |= ballot(ready);
-            }
-            O.maybe_flush(min(pbase + LZH_WAVE, op + total), lane);
-        }
+        emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)ml << 16), (uint32_t)(p1 - ip),
+                   off, lane);
         op += total;
         ip = ip_next;
     }
     return op;
+}
+
+
+// snappy tags a group at a time (same scheme): every lane parses a tag at ip + lane (literal with
+// at most one length byte, COPY_1/2/4), the walk follows the next-tag links, the acceptance rules
+// of snappy_decode below (snappy.cc:848-952) are checked per member against the prefix sum, and
+// the group is cut before the first failure (which, like 2..4-byte literal lengths, runs through
+// the checked per-tag path).
+__device__ int snappy_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
+    Win w;
+    w.bind(in);
+    w.load(0, lane);
+    int ip = 0;
+    uint32_t ulen = 0;
+    for (int shift = 0;; shift += 7) {
+        if (ip >= cs || shift >= 32) return -1;
+        const uint32_t c = w.byte(ip++);
+        const uint32_t val = c & 0x7fu;
+        if (shift == 28 && val > 15) return -1;
+        ulen |= val << shift;
+        if (c < 128) break;
+    }
+    if (ulen > (uint32_t)cap) return -1;
+    const int ul = (int)ulen;
+    int op = 0;
+    for (int guard = 0; guard <= cs && ip < cs; guard++) {
+        ip = unii(ip); op = unii(op);
+        O.flushed = unii(O.flushed); O.ringlo = unii(O.ringlo);
+        if (!w.covers(ip, ip + 2 * LZH_WAVE)) w.load(ip, lane);
+        const int x = ip + lane;
+        const uint32_t tw = w.lane_word(x);
+        const uint32_t c = tw & 0xffu, kind = c & 3u;
+        int len, lit, nx, off = 0, p1 = x + 1;
+        bool cplx = false, okr = true;
+        if (kind == 0) {
+            const int l6 = (int)(c >> 2) + 1;
+            const bool one = l6 == 61;                              // one length byte
+            cplx = l6 > 61;
+            len = one ? (int)((tw >> 8) & 0xffu) + 1 : l6;
+            p1 = x + 1 + (one ? 1 : 0);
+            lit = len;
+            nx = p1 + len;
+            okr = (!one || x + 2 <= cs) && p1 + len <= cs;
+        } else {
+            const int extra = kind == 1 ? 1 : (kind == 2 ? 2 : 4);
+            const uint32_t tw2 = w.lane_word(x + 1);
+            if (kind == 1) {
+                len = (int)((c >> 2) & 7u) + 4;
+                off = (int)(((c >> 5) << 8) | ((tw >> 8) & 0xffu));
+            } else {
+                len = (int)(c >> 2) + 1;
+                off = kind == 2 ? (int)((tw >> 8) & 0xffffu) : (int)tw2;
+            }
+            lit = 0;
+            nx = x + 1 + extra;
+            okr = nx <= cs && off > 0 && (uint32_t)off <= (uint32_t)cap;
+        }
+        const bool inwin = w.covers(x, nx + 4);
+        const int link = (cplx || !inwin) ? 255 : nx - ip;
+        uint64_t M = 0;
+        int j = 0;
+        for (int it = 0; it < LZH_WAVE; it++) {
+            const int nj = rdlanei(link, j);
+            if (nj == 255) break;
+            M |= 1ull << j;
+            if (nj >= LZH_WAVE || ip + nj >= cs) break;
+            j = nj;
+        }
+        const bool mem = (M >> lane) & 1ull;
+        const int L = mem ? len : 0;
+        const int incl = wave_incl_scan(L);
+        const int excl = incl - L;
+        const int opm = op + excl;
+        const bool bad = mem && (x >= cs || !okr || opm + len > ul || (kind != 0 && off > opm));
+        const uint64_t badm = ballot(bad);
+        const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
+        if (!keep) {
+            // one tag through the checked path (dec2 rules)
+            const uint32_t cc = w.byte(ip++);
+            const uint32_t kk = cc & 3u;
+            if (kk == 0) {
+                int ln = (int)(cc >> 2) + 1;
+                if (ln > 60) {
+                    const int nb = ln - 60;
+                    if (ip + nb > cs) return -1;
+                    uint32_t v = 0;
+                    for (int i = 0; i < nb; i++) v |= w.byte(ip + i) << (8 * i);
+                    ln = (int)v + 1;
+                    if (v >= 0x7fffffffu) return -1;
+                    ip += nb;
+                }
+                if ((int64_t)ip + ln > cs || (int64_t)op + ln > ul) return -1;
+                O.literals(w, in, ip, op, ln, lane);
+                ip += ln;
+                op += ln;
+            } else {
+                const int extra = kk == 1 ? 1 : (kk == 2 ? 2 : 4);
+                if (ip + extra > cs) return -1;
+                int ln;
+                uint32_t of;
+                if (kk == 1) {
+                    ln = (int)((cc >> 2) & 7u) + 4;
+                    of = ((cc >> 5) << 8) | w.byte(ip);
+                } else {
+                    ln = (int)(cc >> 2) + 1;
+                    of = 0;
+                    for (int i = 0; i < extra; i++) of |= w.byte(ip + i) << (8 * i);
+                }
+                ip += extra;
+                if (of == 0 || of > (uint32_t)op || op + ln > ul) return -1;
+                O.match(op, (int)of, ln, lane);
+                op += ln;
+            }
+            continue;
+        }
+        const int lastk = 63 - __builtin_clzll(keep);
+        const int total = rdlanei(incl, lastk);
+        const int ip_next = ip + rdlanei(nx - ip, lastk);
+        emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)(len - lit) << 16),
+                   (uint32_t)(p1 - ip), off, lane);
+        op += total;
+        ip = ip_next;
+    }
+    return op == ul ? op : -1;
 }
 
 }  // namespace dec4
@@ -766,7 +898,7 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
         r = codec == 0 ? dec3::lz4_decode(rin, cs, O, part, lane) : dec2::snappy_decode(rin, cs, O, part, lane);
 #else
         r = codec == 0 ? dec4::lz4_decode(rin, cs, O, (LDSA uint8_t*)win + dec2::kW, part, lane)
-                       : dec2::snappy_decode(rin, cs, O, part, lane);
+                       : dec4::snappy_decode(rin, cs, O, (LDSA uint8_t*)win + dec2::kW, part, lane);
 #endif
         if (r > 0) O.flush(r, lane);
     }
