@@ -681,23 +681,28 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         bool endip = false;                            // a match ended past mflimit
                         // link: next member lane, or 0x80 for the rare cases (long match, parse end)
                         const int link = (lng || p + kMinMatch + cn >= mfl1) ? 0x80 : f;
-                        for (int it = 0; it < LZH_WAVE; it++) {
-                            Mm |= 1ull << sl;
-                            int fs = rdlanei(link, sl);
-                            if (fs == 0x80) {
-                                int es;
-                                if (rdlane((uint32_t)lng, sl)) {       // match runs past the window
-                                    LZ_STAT(6, 1);
-                                    const int c = slow_count(in, base + sl, rdlanei((int)ce, sl), mlimit, lane);
-                                    es = sl + kMinMatch + c;
-                                    cn = lane == sl ? c : cn;
-                                    e = lane == sl ? es : e;
-                                    fs = ctz64v(es < LZH_WAVE ? (A & (~0ull << es)) : 0ull);
-                                } else {
-                                    es = rdlanei(e, sl);
-                                }
-                                if (base + es >= mfl1) { endip = true; break; }  // lz4.c:1142
+                        // (links strictly increase, so the walks end)
+                        for (;;) {
+                            int fs;
+                            for (;;) {                                 // common case: plain links
+                                Mm |= 1ull << sl;
+                                fs = rdlanei(link, sl);
+                                if (fs >= LZH_WAVE) break;
+                                sl = fs;
                             }
+                            if (fs != 0x80) break;                     // the chain leaves the batch
+                            int es;
+                            if (rdlane((uint32_t)lng, sl)) {           // match runs past the window
+                                LZ_STAT(6, 1);
+                                const int c = slow_count(in, base + sl, rdlanei((int)ce, sl), mlimit, lane);
+                                es = sl + kMinMatch + c;
+                                cn = lane == sl ? c : cn;
+                                e = lane == sl ? es : e;
+                                fs = ctz64v(es < LZH_WAVE ? (A & (~0ull << es)) : 0ull);
+                            } else {
+                                es = rdlanei(e, sl);
+                            }
+                            if (base + es >= mfl1) { endip = true; break; }  // lz4.c:1142
                             if (fs >= LZH_WAVE) break;
                             sl = fs;
                         }
