@@ -712,13 +712,14 @@ __device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_t* 
         // ---- the real chain from lane 0
         uint64_t M = 0;
         int j = 0;
-        for (int it = 0; it < LZH_WAVE; it++) {
-            const int nj = rdlanei(link, j);
-            if (nj == 255) break;
-            M |= 1ull << j;
+        int nj;
+        for (;;) {                                                  // (links strictly increase)
+            nj = rdlanei(link, j);
             if (nj >= LZH_WAVE) break;
+            M |= 1ull << j;
             j = nj;
         }
+        if (nj != 255) M |= 1ull << j;
         // ---- acceptance rules per member (as lz4_one); the chain ends before the first failure
         const bool mem = (M >> lane) & 1ull;
         const int L = mem ? lit + ml : 0;
@@ -802,16 +803,17 @@ __device__ int snappy_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_
             okr = nx <= cs && off > 0 && (uint32_t)off <= (uint32_t)cap;
         }
         const bool inwin = w.covers(x, nx + 4);
-        const int link = (cplx || !inwin) ? 255 : nx - ip;
+        // link: next tag lane; 255 = not parsed here; 254 = the stream ends after this tag
+        const int link = (cplx || !inwin || x >= cs) ? 255 : (nx >= cs ? 254 : nx - ip);
         uint64_t M = 0;
-        int j = 0;
-        for (int it = 0; it < LZH_WAVE; it++) {
-            const int nj = rdlanei(link, j);
-            if (nj == 255) break;
+        int j = 0, nj;
+        for (;;) {                                                  // (links strictly increase)
+            nj = rdlanei(link, j);
+            if (nj >= LZH_WAVE) break;
             M |= 1ull << j;
-            if (nj >= LZH_WAVE || ip + nj >= cs) break;
             j = nj;
         }
+        if (nj != 255) M |= 1ull << j;
         const bool mem = (M >> lane) & 1ull;
         const int L = mem ? len : 0;
         const int incl = wave_incl_scan(L);
