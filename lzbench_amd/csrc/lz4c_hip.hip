@@ -934,7 +934,10 @@ lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_read
                            uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t chunk0,
                            unsigned long long* stats) {
     // table 16 KiB | input ring 1 KiB | output ring 512 B  (17.5 KiB: 9 waves per CU)
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4];
+#ifndef LZH_LDS_PAD
+#define LZH_LDS_PAD 0
+#endif
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4 + LZH_LDS_PAD / 4];
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t off = chunk * chunk_size;
     if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
