@@ -716,7 +716,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         I = ballot(mle && lane == ej - 2);             // lz4.c:1146
                         endp = endip || (eL < LZH_WAVE && LZH_WAVE - 1 >= fv);   // or the search ran past mflimit
                     }
-                    I |= I0 | E;
+                    I = (Mm ? I : 0ull) | I0 | E;                          // (no stale bits from an earlier round)
 #ifdef LZH_EXP_NOVERIFY
                     break;
 #endif

@@ -1,6 +1,16 @@
-// lzbench_amd/csrc/snappyc_hip.hip -- snappy raw compressor (v2) for gfx950, bit-exact with
-// snappy 1.1.8.  Same parse as v1 (snappy_hip.hip; reference snappy/snappy.cc:510-681, framing
-// :1043-1111) with the structure of the LZ4 v4 kernel (lz4c_hip.hip):
+// lzbench_amd/csrc/snappyc_hip.hip -- snappy raw compressor for gfx950, bit-exact with snappy
+// 1.1.8 (reference snappy/snappy.cc:510-681, framing :1043-1111).
+//
+// Run batches (the common case, as in the LZ4 kernel lz4c_hip.hip): the probe offsets of a
+// snappy search are data independent -- 16 unrolled probes, then `skip >> 5` steps with skip
+// from 48 (snappy.cc:558-611) give offsets 0..32, 34, 36, .., 62, 64, 67, .. from the search
+// start (kPat0/kPat1) -- and after every copy snappy inserts ip-1, re-tests ip and searches from
+// ip+1 (:640-672).  So a batch evaluates 64 consecutive positions speculatively (hash, LDS table
+// claim/read-back, candidate window), resolves the chain of copies lane-parallel (per-lane match
+// end + next hit under the probe pattern, scalar walk over the links, colliders verified against
+// the resolved inserted set), and emits the batch's literals + copies lane-parallel under the
+// next batch's loads.  Searches that run past offset 63 (sparse probes) and the last ~64
+// positions of a fragment (exact termination) use the search batches below (v2):
 //   * 1 KiB LDS input ring per wave filled ahead by LDS-DMA: probe hashing, the ip-1 insert,
 //     ip-side match bytes and literal bytes read LDS;
 //   * speculative candidate window [cand, cand+24) per probe lane: the hit lane's window answers
@@ -19,6 +29,8 @@ namespace snv2 {
 constexpr int kRing = 1024;
 constexpr int kAhead = 704;
 constexpr int kRT = 16;
+constexpr uint64_t kPat0 = 0x55555555ffffffffull;   // probe offsets 0..63 of a search (0..32, 34, .., 62)
+constexpr uint64_t kPat1 = 0x2222222249249249ull;   // offsets 64..127 (64, 67, 70, ..)
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -32,7 +44,8 @@ struct Ring {
     LDSA uint32_t* w;
     int sh;
     int fill;
-    __device__ __forceinline__ bool has(int p0, int p1) const { return p0 + sh >= fill - kRing && p1 + sh <= fill; }
+    int ready;    // fill level known to have landed (refills are issued after a batch's load wait)
+    __device__ __forceinline__ bool has(int p0, int p1) const { return p0 + sh >= fill - kRing && p1 + sh <= ready; }
     __device__ __forceinline__ uint32_t dword(int a) const {
         return ((volatile const LDSA uint32_t*)w)[(a >> 2) & (kRing / 4 - 1)];
     }
@@ -153,9 +166,166 @@ __device__ __forceinline__ uint32_t spec_byte(int si, uint32_t e0, uint32_t e1, 
     return (v >> (8 * (si & 3))) & 0xffu;
 }
 
+// Layout of one (literal, copy) pair, byte t of it per lane: EmitLiteral (snappy.cc:342-383:
+// tag (len-1)<<2, or 60..63 followed by 1..4 length bytes) then EmitCopy (:385-443: 64-byte
+// COPY_2 pieces while len >= 68, a 60-byte piece if len > 64, then COPY_1 when the last piece is
+// < 12 long and the offset < 2048, else COPY_2).  lit may be 0 (no literal), mlen 0 (no copy).
+struct SnapSeq {
+    int hl, k, has60, rem, pre, cb, lit0, lit1, total;
+    uint32_t tag, nm1, lo, hi, offv;
+    bool c1;
+    __device__ __forceinline__ SnapSeq(int lit, uint32_t off, int mlen) {
+        hl = 0;
+        tag = 0;
+        nm1 = (uint32_t)(lit - 1);
+        if (lit > 0) {
+            if (nm1 < 60) { hl = 1; tag = nm1 << 2; }
+            else { const int cnt = (log2floor_u(nm1) >> 3) + 1; hl = 1 + cnt; tag = (uint32_t)(59 + cnt) << 2; }
+        }
+        k = 0;
+        has60 = 0;
+        rem = mlen;
+        if (mlen >= 12) {
+            k = mlen >= 68 ? (mlen - 68) / 64 + 1 : 0;
+            rem = mlen - 64 * k;
+            if (rem > 64) { has60 = 1; rem -= 60; }
+        }
+        offv = off;
+        c1 = rem < 12 && off < 2048u;
+        pre = 3 * (k + has60);
+        cb = mlen > 0 ? pre + (c1 ? 2 : 3) : 0;
+        lit0 = hl;
+        lit1 = hl + lit;
+        total = lit1 + cb;
+        lo = off & 0xffu;
+        hi = (off >> 8) & 0xffu;
+    }
+    __device__ __forceinline__ uint32_t byte(int t, uint32_t lb) const {
+        uint32_t v = tag;
+        v = (t >= 1 && t < hl) ? ((nm1 >> ((8 * (t - 1)) & 31)) & 0xffu) : v;
+        v = (t >= lit0 && t < lit1) ? lb : v;
+        const int ct = t - lit1;
+        if (ct >= 0) {
+            uint32_t cv;
+            if (ct < pre) {
+                const int piece = ct / 3, b = ct - 3 * piece;
+                cv = b == 0 ? ((piece < k) ? (2u | (63u << 2)) : (2u | (59u << 2))) : (b == 1 ? lo : hi);
+            } else {
+                const int b = ct - pre;
+                if (c1) cv = b == 0 ? (1u | ((uint32_t)(rem - 4) << 2) | ((offv >> 8) << 5)) : lo;
+                else cv = b == 0 ? (2u | ((uint32_t)(rem - 1) << 2)) : (b == 1 ? lo : hi);
+            }
+            v = cv;
+        }
+        return v;
+    }
+};
+
+// Sequences found by one batch, one per member lane (the lane of the copy's start): literal
+// start, literal length, offset, copy length, first output byte within the batch's output.
+// Emitted lane-parallel under the next batch's loads.  (Plain locals: a struct here would be
+// kept in scratch memory.)
+#define SREC_DECL uint32_t rc_anc = 0, rc_lit = 0, rc_off = 0, rc_ml = 0, rc_st = 0; uint64_t rc_m = 0; int rc_tot = 0
+#define SREC_EMIT() op = emit_recs(in, R, out, mark, op, rc_anc, rc_lit, rc_off, rc_ml, rc_st, rc_m, rc_tot, lane)
+
+__device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const Bytes& out, LDSA uint8_t* mark, int op,
+                                         uint32_t anc, uint32_t lit, uint32_t off, uint32_t ml, uint32_t st,
+                                         uint64_t mem, int tot, int lane) {
+    if (mem == 0) return op;
+    const int first = __builtin_ctzll(mem), last = 63 - __builtin_clzll(mem);
+    const int a0 = rdlanei((int)anc, first), a1 = rdlanei((int)anc, last) + rdlanei((int)lit, last);
+    if (tot <= 4 * LZH_WAVE && R.has(a0, a1)) {
+        int carry = first;
+        for (int pass = 0; pass * LZH_WAVE < tot; pass++) {
+            const int pb = pass * LZH_WAVE, ob = pb + lane;
+            // owner of output byte ob: the last member starting at or before it (start marks)
+            mark[lane] = 0xff;
+            wave_lds_fence();
+            const int stl = (int)st;
+            if (((mem >> lane) & 1ull) && stl >= pb && stl < pb + LZH_WAVE) mark[stl - pb] = (uint8_t)lane;
+            wave_lds_fence();
+            const int mv = (int)mark[lane];
+            const uint64_t smask = ballot(mv != 0xff);
+            const uint64_t le = smask & ((2ull << lane) - 1ull);
+            const int own = (int)lane_gather((uint32_t)mv, le ? 63 - __builtin_clzll(le) : lane);
+            const int k = le ? own : carry;
+            carry = rdlanei(k, 63);
+            const int a = (int)lane_gather(anc, k), l = (int)lane_gather(lit, k);
+            const uint32_t o = lane_gather(off, k);
+            const int m = (int)lane_gather(ml, k);
+            const int t = ob - (int)lane_gather(st, k);
+            const SnapSeq Q(l, o, m);
+            const uint32_t lb = R.byte(a + t - Q.lit0);
+            if (ob < tot) out.st8(op + ob, Q.byte(t, lb));
+        }
+        return op + tot;
+    }
+    for (uint64_t mm = mem; mm; mm &= mm - 1) {
+        const int k = __builtin_ctzll(mm);
+        op = emit_seq(in, R, out, op, rdlanei((int)anc, k), rdlanei((int)lit, k), rdlane(off, k), rdlanei((int)ml, k),
+                      lane);
+    }
+    return op;
+}
+
+__device__ __forceinline__ uint32_t byte_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x) >> 3; }
+__device__ __forceinline__ int ctz64v(uint64_t x) { return x ? __builtin_ctzll(x) : 64; }
+__device__ __forceinline__ uint64_t lane_bits(int lo, int hi) {   // bits lo..hi (0 <= lo <= hi <= 63)
+    return ((2ull << hi) - 1ull) & (~0ull << lo);
+}
+// lanes l (0..63) whose offset l - o from a search origin is a probe offset of the schedule
+__device__ __forceinline__ uint64_t pat_from(int o) {
+    if (o >= LZH_WAVE) return 0ull;
+    if (o >= 0) return kPat0 << o;
+    const int d = -o;
+    if (d < LZH_WAVE) return (kPat0 >> d) | (kPat1 << (LZH_WAVE - d));
+    if (d < 2 * LZH_WAVE) return kPat1 >> (d - LZH_WAVE);
+    return 0ull;
+}
+// probes after a copy ending at lane e: the re-test at e, then the search from e+1
+__device__ __forceinline__ uint64_t after_copy(int e) {
+    if (e >= LZH_WAVE) return 0ull;
+    return (1ull << e) | (e + 1 < LZH_WAVE ? kPat0 << (e + 1) : 0ull);
+}
+
+// P side: words at p, p+4, .., p+20 (ring); candidate side: 7 dwords from (c & ~3)
+struct PS { uint32_t w, q1, q2, q3, q4, q5; };
+__device__ __forceinline__ PS p_side(const Ring& R, const Bytes& in, bool ring, int p) {
+    const int X = (ring ? p + R.sh : p + in.sh), A = X & ~3;
+    const uint32_t s = (uint32_t)X & 3u;
+    uint32_t a0, a1, a2, a3, a4, a5, a6;
+    if (ring) {
+        a0 = R.dword(A); a1 = R.dword(A + 4); a2 = R.dword(A + 8); a3 = R.dword(A + 12);
+        a4 = R.dword(A + 16); a5 = R.dword(A + 20); a6 = R.dword(A + 24);
+    } else {
+        a0 = ld_b32(in.r, A); a1 = ld_b32(in.r, A + 4); a2 = ld_b32(in.r, A + 8); a3 = ld_b32(in.r, A + 12);
+        a4 = ld_b32(in.r, A + 16); a5 = ld_b32(in.r, A + 20); a6 = ld_b32(in.r, A + 24);
+    }
+    PS v;
+    v.w = __builtin_amdgcn_alignbyte(a1, a0, s);
+    v.q1 = __builtin_amdgcn_alignbyte(a2, a1, s);
+    v.q2 = __builtin_amdgcn_alignbyte(a3, a2, s);
+    v.q3 = __builtin_amdgcn_alignbyte(a4, a3, s);
+    v.q4 = __builtin_amdgcn_alignbyte(a5, a4, s);
+    v.q5 = __builtin_amdgcn_alignbyte(a6, a5, s);
+    return v;
+}
+// bytes matched after the first 4 (0..20) between two 24-byte windows
+__device__ __forceinline__ int match_after4(const PS& a, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t b4,
+                                            uint32_t b5) {
+    const uint32_t x1 = a.q1 ^ b1, x2 = a.q2 ^ b2, x3 = a.q3 ^ b3, x4 = a.q4 ^ b4, x5 = a.q5 ^ b5;
+    int l = 20;
+    l = x5 ? 16 + (int)byte_ctz(x5) : l;
+    l = x4 ? 12 + (int)byte_ctz(x4) : l;
+    l = x3 ? 8 + (int)byte_ctz(x3) : l;
+    l = x2 ? 4 + (int)byte_ctz(x2) : l;
+    l = x1 ? (int)byte_ctz(x1) : l;
+    return l;
+}
+
 // one fragment in[0, fn) appended at op
 __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int op, LDSA uint16_t* tab,
-                                 LDSA uint32_t* ringw, unsigned long long* stats) {
+                                 LDSA uint32_t* ringw, LDSA uint8_t* mark, unsigned long long* stats) {
     const int lane = threadIdx.x;
     Table T{tab};
     const uint32_t tsize = table_size_for((uint32_t)fn);
@@ -165,24 +335,271 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
         const int nvec = (int)(tsize * 2 / 16);
         for (int i = lane; i < nvec; i += LZH_WAVE) lds_zero16(t4 + 4 * i);
     }
-    Ring R{ringw, in.sh, 0};
+    Ring R{ringw, in.sh, 0, 0};
     const int endX = fn + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
     wait_vm();
+    R.ready = R.fill;
     wave_lds_fence();
 
     int next_emit = 0;
-    bool pend = false;
-    int p_src = 0, p_lit = 0, p_ml = 0;
-    uint32_t p_off = 0;
+    SREC_DECL;
     if (fn >= 15) {
         const int ip_limit = fn - 15;
+        // run-batch state: batch base, search origin, pending re-test (-1: none)
+        bool runm = true;
+        int base = 1, org = 1, rt = -1;
+        // search-batch state (see below)
         bool retest = false;
-        int rt = 0, q0 = 1, t0 = 0;
+        int q0 = 1, t0 = 0;
         bool U = ip_limit - q0 >= 16;
         int ci0 = 0, cq0 = U ? q0 + 16 : q0;
         uint32_t cu0 = U ? 48u : 32u;
         for (int guard = 0; guard < 4 * fn + 64; guard++) {
+            runm = unii(runm) != 0; retest = unii(retest) != 0; U = unii(U) != 0;
+            base = unii(base); org = unii(org); rt = unii(rt); q0 = unii(q0); t0 = unii(t0);
+            ci0 = unii(ci0); cq0 = unii(cq0); cu0 = uni(cu0); next_emit = unii(next_emit); op = unii(op);
+            rc_tot = unii(rc_tot); R.fill = unii(R.fill); R.ready = unii(R.ready);
+            SN_STAT(0, 1);
+            if (runm && (base + LZH_WAVE + 8 > ip_limit || (rt < 0 && base - org >= LZH_WAVE))) {
+                // leave run batches: sparse probes or close to ip_limit (exact termination below)
+                runm = false;
+                if (rt >= 0) {
+                    retest = true;
+                    q0 = rt + 1;
+                    t0 = 0;
+                } else {
+                    const int d = base - org;                 // schedule probes before base
+                    retest = false;
+                    q0 = org;
+                    t0 = d < LZH_WAVE ? __builtin_popcountll(kPat0 & ((1ull << d) - 1ull))
+                                      : 48 + __builtin_popcountll(kPat1 & ((1ull << (d - LZH_WAVE)) - 1ull));
+                }
+                U = ip_limit - q0 >= 16;
+                ci0 = 0;
+                cq0 = U ? q0 + 16 : q0;
+                cu0 = U ? 48u : 32u;
+            }
+            if (runm) {
+                // ================= run batch: positions base..base+63 (all probes valid)
+                const int p = base + lane;
+                const uint64_t P0 = (rt >= 0 ? 2ull : 0ull) | pat_from(org - base);
+                const uint64_t I0 = rt >= 0 ? 1ull : 0ull;              // lane 0 = rt-1 (inserted, snappy.cc:652)
+                const bool ring = R.has(base, base + LZH_WAVE + 28);
+                const PS ps = p_side(R, in, ring, p);
+                const uint32_t h = (ps.w * 0x1e35a7bdu) >> shift;
+                const uint32_t old = T.get(h);
+                T.put(h, (uint32_t)p);
+                wave_lds_fence();
+                const uint32_t back = T.get(h);
+                const uint64_t losers = ballot(back != (uint32_t)p);
+                const uint32_t cand = old;
+                uint32_t d0, d1, d2, d3, d4, d5, d6;
+                {
+                    const int cX = (int)cand + in.sh, cA = cX & ~3;
+                    d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
+                    d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
+                    d6 = ld_b32(in.r, cA + 24);
+                }
+                SREC_EMIT();
+                rc_m = 0;
+                rc_tot = 0;
+                wait_vm();
+                R.ready = R.fill;
+                wave_lds_fence();
+                {
+                    const int target = min(base + in.sh + kAhead, endX + 256);
+                    for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
+                }
+                const uint32_t cs = (uint32_t)(cand + in.sh) & 3u;
+                const bool ok = __builtin_amdgcn_alignbyte(d1, d0, cs) == ps.w;
+                const int len = match_after4(ps, __builtin_amdgcn_alignbyte(d2, d1, cs),
+                                             __builtin_amdgcn_alignbyte(d3, d2, cs),
+                                             __builtin_amdgcn_alignbyte(d4, d3, cs),
+                                             __builtin_amdgcn_alignbyte(d5, d4, cs),
+                                             __builtin_amdgcn_alignbyte(d6, d5, cs));
+                // slot groups: every lane of a slot read back the same claim winner
+                const uint64_t below = (1ull << lane) - 1ull;
+                uint64_t grp = 1ull << lane, coll = 0;
+                int prev = -1;
+                bool okp = false;
+                int lep = 0;
+                if (losers) {
+                    SN_STAT(1, 1);
+                    const uint32_t W = back - (uint32_t)base;
+                    uint64_t eq = ~0ull;
+#pragma unroll
+                    for (int b = 0; b < 6; b++) {
+                        const bool wb = (W >> b) & 1u;
+                        const uint64_t bm = ballot(wb);
+                        eq &= wb ? bm : ~bm;
+                    }
+                    grp = eq;
+                    const uint64_t eb = grp & below;
+                    prev = eb ? 63 - __builtin_clzll(eb) : -1;
+                    coll = ballot(prev >= 0);
+                    const int k = prev >= 0 ? prev : lane;
+                    const uint32_t gw = lane_gather(ps.w, k);
+                    lep = match_after4(ps, lane_gather(ps.q1, k), lane_gather(ps.q2, k), lane_gather(ps.q3, k),
+                                       lane_gather(ps.q4, k), lane_gather(ps.q5, k));
+                    okp = gw == ps.w;
+                }
+                // resolve (as the LZ4 kernel): assume each collider's candidate is its closest
+                // earlier slot member, walk, verify against the inserted set, repeat if needed
+                int ak = prev;
+                bool oke = prev >= 0 ? okp : ok;
+                uint32_t ce = prev >= 0 ? (uint32_t)(base + prev) : cand;
+                int le = prev >= 0 ? lep : len;
+                uint64_t Mm = 0, I = I0;
+                int cn = 0, e = 0, eL = 0;
+                bool endp = false;
+                for (int round = 0; round <= LZH_WAVE; round++) {
+                    const uint64_t A = ballot(oke);
+                    cn = min(le, fn - (p + 4));                          // FindMatchLength limit (ip_end)
+                    const bool lng = oke && le == 20 && p + 24 < fn;
+                    e = lane + 4 + cn;
+                    const int f = ctz64v(A & after_copy(e));
+                    const int link = (lng || p + 4 + cn >= ip_limit) ? 0x80 : f;
+                    Mm = 0;
+                    endp = false;
+                    uint64_t E;
+                    const uint64_t r0 = A & P0;
+                    if (!r0) {
+                        E = P0;
+                    } else {
+                        int sl = __builtin_ctzll(r0);
+                        for (;;) {                                       // (links strictly increase)
+                            int fs;
+                            for (;;) {
+                                Mm |= 1ull << sl;
+                                fs = rdlanei(link, sl);
+                                if (fs >= LZH_WAVE) break;
+                                sl = fs;
+                            }
+                            if (fs != 0x80) break;
+                            int es;
+                            if (rdlane((uint32_t)lng, sl)) {             // copy runs past the window
+                                SN_STAT(6, 1);
+                                const int a = base + sl + 4, M = rdlanei((int)ce, sl);
+                                int c = 20;
+                                for (int it = 0; it < (1 << 11) && a + c < fn; it++) {
+                                    const int o = c + 4 * lane;
+                                    const uint32_t x = in.w32(a + o) ^ in.w32(M + 4 + o);
+                                    const uint64_t ne = ballot(x != 0);
+                                    if (ne) {
+                                        const int l = ffs64(ne);
+                                        c += 4 * l + (int)byte_ctz(rdlane(x, l));
+                                        break;
+                                    }
+                                    c += 4 * LZH_WAVE;
+                                }
+                                c = min(c, fn - a);
+                                es = sl + 4 + c;
+                                cn = lane == sl ? c : cn;
+                                e = lane == sl ? es : e;
+                                fs = ctz64v(A & after_copy(es));
+                            } else {
+                                es = rdlanei(e, sl);
+                            }
+                            if (base + es >= ip_limit) { endp = true; break; }   // snappy.cc:646
+                            if (fs >= LZH_WAVE) break;
+                            sl = fs;
+                        }
+                        eL = rdlanei(e, sl);
+                        // probed lanes: the initial plan up to the first member, then after each
+                        // copy the re-test and the search pattern; ip-1 of each copy is inserted
+                        const uint64_t mle = Mm & (below | (1ull << lane));
+                        const int j = mle ? 63 - __builtin_clzll(mle) : lane;
+                        const int ej = (int)lane_gather((uint32_t)e, j);
+                        bool pr;
+                        if (!mle) pr = (P0 >> lane) & 1ull;
+                        else if (lane == j) pr = true;
+                        else pr = lane >= ej && ((after_copy(ej) >> lane) & 1ull);
+                        E = ballot(pr && (!endp || lane < eL));
+                        I = ballot(mle && lane != j && lane == ej - 1);
+                    }
+                    I = (Mm ? I : 0ull) | I0 | E;                          // (no stale bits from an earlier round)
+                    if (!(coll & E)) break;
+                    const uint64_t mk = grp & below & I;
+                    const int kt = mk ? 63 - __builtin_clzll(mk) : -1;
+                    const bool fix = ((E >> lane) & 1ull) && kt != ak;
+                    if (!ballot(fix)) break;
+                    SN_STAT(2, 1);
+                    const bool far = fix && kt >= 0 && kt != prev;
+                    if (fix) {
+                        ak = kt;
+                        oke = kt < 0 ? ok : okp;
+                        ce = kt < 0 ? cand : (uint32_t)(base + kt);
+                        le = kt < 0 ? len : lep;
+                    }
+                    if (ballot(far)) {                                   // an older member than prev
+                        const int k = far ? kt : lane;
+                        const uint32_t gw = lane_gather(ps.w, k);
+                        const int lf = match_after4(ps, lane_gather(ps.q1, k), lane_gather(ps.q2, k),
+                                                    lane_gather(ps.q3, k), lane_gather(ps.q4, k), lane_gather(ps.q5, k));
+                        if (far) { le = lf; oke = gw == ps.w; }
+                    }
+                }
+                // ---- records (literal from the previous copy's end, or next_emit)
+                if (Mm) {
+                    SN_STAT(3, __builtin_popcountll(Mm));
+                    const bool mem = (Mm >> lane) & 1ull;
+                    const uint64_t mb = Mm & below;
+                    const int jp = mb ? 63 - __builtin_clzll(mb) : lane;
+                    const int ep = (int)lane_gather((uint32_t)e, jp);
+                    const int anc = mb ? base + ep : next_emit;
+                    const int lit = p - anc, mlen = 4 + cn;
+                    const uint32_t offv = (uint32_t)(p - (int)ce);
+                    int L = 0;
+                    if (mem) { const SnapSeq Q(lit, offv, mlen); L = Q.total; }
+                    int incl = L;
+                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xf, 0xf, false);
+                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xf, 0xf, false);
+                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xf, 0xf, false);
+                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xf, 0xf, false);
+                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xa, 0xf, false);
+                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xc, 0xf, false);
+                    rc_anc = (uint32_t)anc;
+                    rc_lit = (uint32_t)lit;
+                    rc_off = offv;
+                    rc_ml = (uint32_t)mlen;
+                    rc_st = (uint32_t)(incl - L);
+                    rc_m = Mm;
+                    rc_tot = rdlanei(incl, 63);
+                    next_emit = base + eL;
+                }
+                if (endp) break;                                         // remainder from next_emit
+                // table: the last inserted lane of each slot, or the slot's old value
+                {
+                    const bool inI = (I >> lane) & 1ull;
+                    if (!losers) {
+                        if (!inI) T.put(h, old);
+                    } else {
+                        const uint64_t gi = grp & I;
+                        const bool wr = gi == 0 || (inI && (gi & ~((2ull << lane) - 1ull)) == 0);
+                        if (wr) T.put(h, inI ? (uint32_t)p : old);
+                    }
+                    wave_lds_fence();
+                }
+                if (Mm) {
+                    if (eL >= LZH_WAVE) {                                // re-test in a later batch
+                        rt = base + eL;
+                        org = rt + 1;
+                        base = rt - 1;
+                    } else {                                             // search continues past the batch
+                        rt = -1;
+                        org = base + eL + 1;
+                        base += LZH_WAVE;
+                    }
+                } else {
+                    rt = -1;
+                    base += LZH_WAVE;
+                }
+                continue;
+            }
+
+            // ================= search batch (sparse probes or near ip_limit): the probe plan
+            // along the exact schedule, first hit only (v2)
             // ---- probe plan
             int p = 0;
             bool valid = false, term = false;
@@ -232,15 +649,15 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
                 d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
             }
-            if (pend) {
-                op = emit_seq(in, R, out, op, p_src, p_lit, p_off, p_ml, lane);
-                pend = false;
-            }
+            SREC_EMIT();
+            rc_m = 0;
+            rc_tot = 0;
             {
                 const int target = min(front + in.sh + kAhead, endX + 256);
                 for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
             }
             wait_vm();
+            R.ready = R.fill;
             wave_lds_fence();
 
             bool ok = valid && __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)cX & 3u) == pw;
@@ -297,6 +714,8 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
                     d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
                 }
+                wait_vm();
+                R.ready = R.fill;
                 ok = valid && __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)cX & 3u) == pw;
                 hits = ballot(ok);
                 fh = ffs64(hits);
@@ -360,8 +779,16 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
             }
             len = min(len, fn - a);
             const int matched = 4 + len;
-            pend = true;
-            p_src = next_emit; p_lit = P - next_emit; p_off = (uint32_t)(P - M); p_ml = matched;
+            {
+                const SnapSeq Q(P - next_emit, (uint32_t)(P - M), matched);
+                rc_anc = (uint32_t)next_emit;
+                rc_lit = (uint32_t)(P - next_emit);
+                rc_off = (uint32_t)(P - M);
+                rc_ml = (uint32_t)matched;
+                rc_st = 0;
+                rc_m = 1;
+                rc_tot = Q.total;
+            }
             const int ip = P + matched;
             next_emit = ip;
             if (ip >= ip_limit) break;
@@ -373,9 +800,13 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
             ci0 = 0;
             cq0 = U ? q0 + 16 : q0;
             cu0 = U ? 48u : 32u;
+            // back to run batches: re-test batch at rt (lane 0 = rt-1 insert, lane 1 = rt)
+            runm = true;
+            base = rt - 1;
+            org = rt + 1;
         }
     }
-    if (pend) op = emit_seq(in, R, out, op, p_src, p_lit, p_off, p_ml, lane);
+    SREC_EMIT();
     if (next_emit < fn) op = emit_seq(in, R, out, op, next_emit, fn - next_emit, 0, 0, lane);
     wave_lds_fence();
     return op;
@@ -387,7 +818,7 @@ extern "C" __global__ void __launch_bounds__(64)
 lzh_snappy_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                               uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t chunk0,
                               unsigned long long* stats) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + 256];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + 256 + LZH_WAVE / 4];   // table | ring | marks
     const int lane = threadIdx.x;
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t off = chunk * chunk_size;
@@ -408,7 +839,8 @@ lzh_snappy_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
         const uint64_t readable = min<uint64_t>(in_readable - off - fpos, (uint64_t)fn + 64);
         Bytes rin;
         rin.init(in + off + fpos, readable);
-        op = snv2::compress_fragment(rin, fn, rout, op, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13), stats);
+        op = snv2::compress_fragment(rin, fn, rout, op, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13),
+                                     (LDSA uint8_t*)((LDSA uint32_t*)lds + (1 << 13) + 256), stats);
     }
     if (lane == 0) csizes[chunk] = (uint32_t)op;
 }
