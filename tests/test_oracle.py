@@ -87,3 +87,17 @@ def test_oracle_equals_reference_fresh_random():
             a = O.compress_chunks(data, codec, chunk)
             b = O.compress_chunks(data, codec, chunk, use_ref=True)
             assert (a[1] == b[1]).all() and (a[0] == b[0]).all(), (trial, n, kind, codec, chunk)
+
+
+@pytest.mark.skipif(not O.have_ref(), reason="reference build (oracle/_ref) not present")
+@pytest.mark.parametrize("gen", ["lowent", "periodic", "tinyvocab", "stripes"])
+@pytest.mark.parametrize("cfg", [("lz4", 65536, 1), ("lz4", 131072, 1), ("lz4fast", 65536, 2), ("snappy", 65536, 0),
+                                 ("snappy", 262144, 0)], ids=lambda c: f"{c[0]}-b{c[1] >> 10}-l{c[2]}")
+def test_oracle_matches_reference_on_stress_inputs(gen, cfg):
+    """the GPU stress inputs (tests/test_gpu_stress.py) through the restatement and the reference build"""
+    import test_gpu_stress as S
+    codec, chunk, level = cfg
+    data = S.GENS[gen](np.random.default_rng(1000 + len(gen)))
+    p, cs = O.compress_chunks(data, codec, chunk, level)
+    rp, rcs = O.compress_chunks(data, codec, chunk, level, use_ref=True)
+    assert (cs == rcs).all() and len(p) == len(rp) and (p == rp).all()
