@@ -182,22 +182,49 @@ struct DevBuf {
 
 struct Dev {
     int id = 0;
-    hipStream_t s = nullptr;
-    DevBuf in, packed, temp, csizes, offsets, status;
-    std::vector<uint32_t> h_cs;
-    std::vector<int32_t> h_status;
+    hipStream_t s = nullptr;      // kernels (even sub-batches)
+    hipStream_t s2 = nullptr;     // kernels (odd sub-batches: overlaps the tail of the previous grid)
+    hipStream_t sin = nullptr;    // host -> device copies
+    hipStream_t sout = nullptr;   // device -> host copies
+    DevBuf in, packed, temp, temp2, csizes, offsets, status;
+    uint32_t* h_cs = nullptr;     // pinned: chunk sizes / statuses read back per sub-batch
+    size_t h_cap = 0;
+    int ensure_host(size_t n) {
+        if (n <= h_cap) return 0;
+        if (h_cs) (void)hipHostFree(h_cs);
+        h_cs = nullptr;
+        h_cap = 0;
+        if (hipHostMalloc((void**)&h_cs, std::max<size_t>(n, 1024) * 4, hipHostMallocDefault) != hipSuccess) return -1;
+        h_cap = std::max<size_t>(n, 1024);
+        return 0;
+    }
 };
+
+struct HostReg { void* p; size_t n; };
 
 struct LzhCtx {
     uint32_t magic = 0x4c5a4858;  // "LZHX"
     int codec = 0;
     size_t chunk_size = 0;
     std::vector<Dev> devs;
+    std::vector<HostReg> regs;    // host ranges page-locked by this row (lzbench reuses its buffers)
 };
 
 LzhCtx* ctx_of(char* wm) {
     LzhCtx* c = (LzhCtx*)wm;
     return (c && c->magic == 0x4c5a4858) ? c : nullptr;
+}
+
+// page-lock [p, p+n) once per row so the copies run at PCIe rate and asynchronously (the
+// reference driver hands over pageable malloc'd buffers, lzbench.cpp:256-263); a range that
+// cannot be registered is simply copied from pageable memory
+void ensure_pinned(LzhCtx* c, const void* p, size_t n) {
+    if (!p || n < (1u << 20)) return;
+    const uintptr_t a0 = (uintptr_t)p & ~(uintptr_t)4095, a1 = ((uintptr_t)p + n + 4095) & ~(uintptr_t)4095;
+    for (const HostReg& r : c->regs)
+        if ((uintptr_t)r.p <= a0 && a1 <= (uintptr_t)r.p + r.n) return;
+    if (hipHostRegister((void*)a0, a1 - a0, hipHostRegisterPortable) == hipSuccess) c->regs.push_back({(void*)a0, a1 - a0});
+    else (void)hipGetLastError();
 }
 
 char* ctx_new(int codec, size_t chunk_size, size_t ngpus) {
@@ -213,8 +240,12 @@ char* ctx_new(int codec, size_t chunk_size, size_t ngpus) {
     c->chunk_size = chunk_size;
     c->devs.resize(ngpus);
     for (size_t g = 0; g < ngpus; g++) {
-        c->devs[g].id = (int)g;
-        if (hipSetDevice((int)g) != hipSuccess || hipStreamCreateWithFlags(&c->devs[g].s, hipStreamNonBlocking) != hipSuccess) {
+        Dev& d = c->devs[g];
+        d.id = (int)g;
+        if (hipSetDevice((int)g) != hipSuccess || hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&d.s2, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&d.sin, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&d.sout, hipStreamNonBlocking) != hipSuccess) {
             fprintf(stderr, "lzbench_hip: cannot open device %zu\n", g);
             delete c;
             return nullptr;
@@ -223,83 +254,155 @@ char* ctx_new(int codec, size_t chunk_size, size_t ngpus) {
     return (char*)c;
 }
 
+// chunks per pipelined sub-batch: ~128 MiB of input and at least 1 024 chunks (a full grid round
+// of the widest-LDS kernel); consecutive sub-batches alternate between two kernel streams so a
+// grid's tail overlaps the next grid
+size_t sub_batch_chunks(size_t chunk) {
+    return std::max<size_t>(1024, ((size_t)128 << 20) / std::max<size_t>(chunk, 1));
+}
+
+struct Events {
+    std::vector<hipEvent_t> ev;
+    hipEvent_t get(size_t i) {
+        while (ev.size() <= i) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+            ev.push_back(e);
+        }
+        return ev[i];
+    }
+    ~Events() { for (hipEvent_t e : ev) (void)hipEventDestroy(e); }
+};
+
 // process one run: chunks [0, k) of uniform size `chunk` (last ragged) covering n bytes of
 // host input; results appended at out (capacity outcap). Returns packed bytes or < 0.
+// Each GPU takes a contiguous chunk range; within it, sub-batches are pipelined over three
+// streams (host->device copy | compress + scan + pack | device->host copy), and the packed
+// sub-batches are gathered to `out` in chunk order as their sizes come back.
 int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t chunk, uint8_t* out, size_t outcap,
                      size_t* compr_sizes) {
     const size_t k = lzh_num_chunks(n, chunk);
     const size_t G = std::min(c->devs.size(), k);
-    std::vector<size_t> c0(G + 1), totals(G, 0);
+    const size_t sbk = sub_batch_chunks(chunk);
+    std::vector<size_t> c0(G + 1);
     for (size_t g = 0; g <= G; g++) c0[g] = k * g / G;
+    ensure_pinned(c, in, n);
+    ensure_pinned(c, out, outcap);
+    std::vector<Events> evin(G), evk(G);
+    const size_t sb_packed = align_up(lzh_max_packed_bytes(c->codec, sbk * chunk, chunk) + 64, 256);
     for (size_t g = 0; g < G; g++) {
         Dev& d = c->devs[g];
         if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
         const size_t off = c0[g] * chunk, nn = std::min(n, c0[g + 1] * chunk) - off, kk = c0[g + 1] - c0[g];
-        if (d.in.ensure(nn + 64) || d.packed.ensure(lzh_max_packed_bytes(c->codec, nn, chunk) + 64) ||
-            d.temp.ensure(lzh_compress_temp_bytes(c->codec, nn, chunk)) || d.csizes.ensure(kk * 4 + 64) ||
-            d.offsets.ensure((kk + 1) * 8 + 64))
+        const size_t nsub = (kk + sbk - 1) / sbk;
+        if (d.in.ensure(nn + 64) || d.packed.ensure(nsub * sb_packed) ||
+            d.temp.ensure(lzh_compress_temp_bytes(c->codec, std::min(nn, sbk * chunk), chunk)) ||
+            (nsub > 1 && d.temp2.ensure(lzh_compress_temp_bytes(c->codec, std::min(nn, sbk * chunk), chunk))) ||
+            d.csizes.ensure(kk * 4 + 64) || d.offsets.ensure((kk + nsub) * 8 + 64) || d.ensure_host(kk))
             return LZH_ESPACE;
-        if (hipMemcpyAsync(d.in.p, in + off, nn, hipMemcpyHostToDevice, d.s) != hipSuccess) return LZH_EHIP;
-        int rc = lzh_compress_async(c->codec, level, d.in.p, nn, d.in.cap, chunk, d.packed.p, d.packed.cap,
-                                    (uint32_t*)d.csizes.p, (uint64_t*)d.offsets.p, d.temp.p, d.temp.cap, d.s);
-        if (rc) return rc;
-        d.h_cs.resize(kk);
-        if (hipMemcpyAsync(d.h_cs.data(), d.csizes.p, kk * 4, hipMemcpyDeviceToHost, d.s) != hipSuccess) return LZH_EHIP;
+        for (size_t i = 0; i < nsub; i++) {
+            const size_t ci = i * sbk, ck = std::min(sbk, kk - ci);
+            const size_t ro = ci * chunk, rn = std::min(nn, (ci + ck) * chunk) - ro;
+            hipEvent_t e_in = evin[g].get(i), e_k = evk[g].get(i);
+            if (!e_in || !e_k) return LZH_EHIP;
+            LZH_CHECK(hipMemcpyAsync((uint8_t*)d.in.p + ro, in + off + ro, rn, hipMemcpyHostToDevice, d.sin));
+            LZH_CHECK(hipEventRecord(e_in, d.sin));
+            hipStream_t ks = (i & 1) ? d.s2 : d.s;
+            DevBuf& tb = (i & 1) ? d.temp2 : d.temp;
+            LZH_CHECK(hipStreamWaitEvent(ks, e_in, 0));
+            int rc = lzh_compress_async(c->codec, level, (uint8_t*)d.in.p + ro, rn, rn + 64, chunk,
+                                        (uint8_t*)d.packed.p + i * sb_packed, sb_packed, (uint32_t*)d.csizes.p + ci,
+                                        (uint64_t*)d.offsets.p + ci + i, tb.p, tb.cap, ks);
+            if (rc) return rc;
+            LZH_CHECK(hipMemcpyAsync(d.h_cs + ci, (uint32_t*)d.csizes.p + ci, ck * 4, hipMemcpyDeviceToHost, ks));
+            LZH_CHECK(hipEventRecord(e_k, ks));
+        }
     }
     size_t base = 0;
+    bool fits = true;
     for (size_t g = 0; g < G; g++) {   // host-side gather in chunk order
         Dev& d = c->devs[g];
-        if (hipSetDevice(d.id) != hipSuccess || hipStreamSynchronize(d.s) != hipSuccess) return LZH_EHIP;
-        size_t tot = 0;
-        for (size_t i = 0; i < d.h_cs.size(); i++) { compr_sizes[c0[g] + i] = d.h_cs[i]; tot += d.h_cs[i]; }
-        if (base + tot > outcap) return 0;   // lzbench: cannot store
-        if (hipMemcpyAsync(out + base, d.packed.p, tot, hipMemcpyDeviceToHost, d.s) != hipSuccess) return LZH_EHIP;
-        totals[g] = tot;
-        base += tot;
+        if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
+        const size_t kk = c0[g + 1] - c0[g], nsub = (kk + sbk - 1) / sbk;
+        for (size_t i = 0; i < nsub; i++) {
+            const size_t ci = i * sbk, ck = std::min(sbk, kk - ci);
+            LZH_CHECK(hipEventSynchronize(evk[g].get(i)));
+            size_t tot = 0;
+            for (size_t j = 0; j < ck; j++) { compr_sizes[c0[g] + ci + j] = d.h_cs[ci + j]; tot += d.h_cs[ci + j]; }
+            if (!fits || base + tot > outcap) { fits = false; continue; }   // lzbench: cannot store
+            LZH_CHECK(hipStreamWaitEvent(d.sout, evk[g].get(i), 0));
+            LZH_CHECK(hipMemcpyAsync(out + base, (uint8_t*)d.packed.p + i * sb_packed, tot, hipMemcpyDeviceToHost, d.sout));
+            base += tot;
+        }
     }
     for (size_t g = 0; g < G; g++) {
-        if (hipSetDevice(c->devs[g].id) != hipSuccess || hipStreamSynchronize(c->devs[g].s) != hipSuccess) return LZH_EHIP;
+        if (hipSetDevice(c->devs[g].id) != hipSuccess || hipStreamSynchronize(c->devs[g].sout) != hipSuccess ||
+            hipStreamSynchronize(c->devs[g].s) != hipSuccess || hipStreamSynchronize(c->devs[g].s2) != hipSuccess)
+            return LZH_EHIP;
     }
-    return (int64_t)base;
+    return fits ? (int64_t)base : 0;
 }
 
 int64_t run_decompress(LzhCtx* c, const uint8_t* in, const size_t* compr_sizes, size_t n, size_t chunk, uint8_t* out) {
     const size_t k = lzh_num_chunks(n, chunk);
     const size_t G = std::min(c->devs.size(), k);
+    const size_t sbk = sub_batch_chunks(chunk);
     std::vector<size_t> c0(G + 1);
     for (size_t g = 0; g <= G; g++) c0[g] = k * g / G;
     std::vector<size_t> coff(k + 1, 0);
     for (size_t i = 0; i < k; i++) coff[i + 1] = coff[i] + compr_sizes[i];
+    ensure_pinned(c, in, coff[k]);
+    ensure_pinned(c, out, n);
+    std::vector<Events> evin(G), evk(G);
     for (size_t g = 0; g < G; g++) {
         Dev& d = c->devs[g];
         if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
-        const size_t kk = c0[g + 1] - c0[g];
+        const size_t kk = c0[g + 1] - c0[g], nsub = (kk + sbk - 1) / sbk;
         const size_t off = c0[g] * chunk, nn = std::min(n, c0[g + 1] * chunk) - off;
         const size_t pin = coff[c0[g + 1]] - coff[c0[g]];
         if (d.in.ensure(pin + 64) || d.packed.ensure(nn + 64) || d.csizes.ensure(kk * 4 + 64) ||
-            d.status.ensure(kk * 4 + 64) || d.temp.ensure(lzh_decompress_temp_bytes(c->codec, nn, chunk)))
+            d.status.ensure(kk * 4 + 64) ||
+            d.temp.ensure(lzh_decompress_temp_bytes(c->codec, std::min(nn, sbk * chunk), chunk)) ||
+            d.temp2.ensure(lzh_decompress_temp_bytes(c->codec, std::min(nn, sbk * chunk), chunk)) ||
+            d.ensure_host(2 * kk))
             return LZH_ESPACE;
-        d.h_cs.resize(kk);
-        for (size_t i = 0; i < kk; i++) d.h_cs[i] = (uint32_t)compr_sizes[c0[g] + i];
-        if (hipMemcpyAsync(d.in.p, in + coff[c0[g]], pin, hipMemcpyHostToDevice, d.s) != hipSuccess ||
-            hipMemcpyAsync(d.csizes.p, d.h_cs.data(), kk * 4, hipMemcpyHostToDevice, d.s) != hipSuccess)
-            return LZH_EHIP;
-        int rc = lzh_decompress_async(c->codec, d.in.p, d.in.cap, (const uint32_t*)d.csizes.p, nullptr, nn, chunk,
-                                      d.packed.p, (int32_t*)d.status.p, d.temp.p, d.temp.cap, d.s);
-        if (rc) return rc;
-        d.h_status.resize(kk);
-        if (hipMemcpyAsync(d.h_status.data(), d.status.p, kk * 4, hipMemcpyDeviceToHost, d.s) != hipSuccess ||
-            hipMemcpyAsync(out + off, d.packed.p, nn, hipMemcpyDeviceToHost, d.s) != hipSuccess)
-            return LZH_EHIP;
+        uint32_t* h_in = d.h_cs;          // sizes in
+        int32_t* h_st = (int32_t*)d.h_cs + kk;   // statuses out
+        for (size_t i = 0; i < kk; i++) h_in[i] = (uint32_t)compr_sizes[c0[g] + i];
+        for (size_t i = 0; i < nsub; i++) {
+            const size_t ci = i * sbk, ck = std::min(sbk, kk - ci);
+            const size_t ro = ci * chunk, rn = std::min(nn, (ci + ck) * chunk) - ro;
+            const size_t po = coff[c0[g] + ci] - coff[c0[g]], pn = coff[c0[g] + ci + ck] - coff[c0[g] + ci];
+            hipEvent_t e_in = evin[g].get(i), e_k = evk[g].get(i);
+            if (!e_in || !e_k) return LZH_EHIP;
+            LZH_CHECK(hipMemcpyAsync((uint8_t*)d.in.p + po, in + coff[c0[g]] + po, pn, hipMemcpyHostToDevice, d.sin));
+            LZH_CHECK(hipMemcpyAsync((uint32_t*)d.csizes.p + ci, h_in + ci, ck * 4, hipMemcpyHostToDevice, d.sin));
+            LZH_CHECK(hipEventRecord(e_in, d.sin));
+            hipStream_t ks = (i & 1) ? d.s2 : d.s;
+            DevBuf& tb = (i & 1) ? d.temp2 : d.temp;
+            LZH_CHECK(hipStreamWaitEvent(ks, e_in, 0));
+            int rc = lzh_decompress_async(c->codec, (uint8_t*)d.in.p + po, pn + 64, (const uint32_t*)d.csizes.p + ci,
+                                          nullptr, rn, chunk, (uint8_t*)d.packed.p + ro, (int32_t*)d.status.p + ci,
+                                          tb.p, tb.cap, ks);
+            if (rc) return rc;
+            LZH_CHECK(hipEventRecord(e_k, ks));
+            LZH_CHECK(hipStreamWaitEvent(d.sout, e_k, 0));
+            LZH_CHECK(hipMemcpyAsync(h_st + ci, (int32_t*)d.status.p + ci, ck * 4, hipMemcpyDeviceToHost, d.sout));
+            LZH_CHECK(hipMemcpyAsync(out + off + ro, (uint8_t*)d.packed.p + ro, rn, hipMemcpyDeviceToHost, d.sout));
+        }
     }
     int64_t sum = 0;
     bool bad = false;
     for (size_t g = 0; g < G; g++) {
         Dev& d = c->devs[g];
-        if (hipSetDevice(d.id) != hipSuccess || hipStreamSynchronize(d.s) != hipSuccess) return LZH_EHIP;
-        for (size_t i = 0; i < d.h_status.size(); i++) {
-            if (d.h_status[i] < 0) bad = true;
-            sum += d.h_status[i];
+        if (hipSetDevice(d.id) != hipSuccess || hipStreamSynchronize(d.sout) != hipSuccess ||
+            hipStreamSynchronize(d.s) != hipSuccess || hipStreamSynchronize(d.s2) != hipSuccess)
+            return LZH_EHIP;
+        const size_t kk = c0[g + 1] - c0[g];
+        const int32_t* h_st = (const int32_t*)d.h_cs + kk;
+        for (size_t i = 0; i < kk; i++) {
+            if (h_st[i] < 0) bad = true;
+            sum += h_st[i];
         }
     }
     return bad ? LZH_ECORRUPT : sum;
@@ -336,9 +439,15 @@ void lzbench_hip_deinit(char* wm) {
     if (!c) return;
     for (Dev& d : c->devs) {
         (void)hipSetDevice(d.id);
-        d.in.release(); d.packed.release(); d.temp.release(); d.csizes.release(); d.offsets.release(); d.status.release();
+        d.in.release(); d.packed.release(); d.temp.release(); d.temp2.release(); d.csizes.release(); d.offsets.release();
+        d.status.release();
+        if (d.h_cs) (void)hipHostFree(d.h_cs);
         if (d.s) (void)hipStreamDestroy(d.s);
+        if (d.s2) (void)hipStreamDestroy(d.s2);
+        if (d.sin) (void)hipStreamDestroy(d.sin);
+        if (d.sout) (void)hipStreamDestroy(d.sout);
     }
+    for (const HostReg& r : c->regs) (void)hipHostUnregister(r.p);
     c->magic = 0;
     delete c;
 }
@@ -363,6 +472,8 @@ int64_t lzbench_hip_memcpy(char* in, size_t insize, char* out, size_t outsize, s
     if (!c || outsize < insize) return 0;
     Dev& d = c->devs[0];
     if (hipSetDevice(d.id) != hipSuccess || d.in.ensure(insize + 64)) return 0;
+    ensure_pinned(c, in, insize);
+    ensure_pinned(c, out, outsize);
     if (hipMemcpyAsync(d.in.p, in, insize, hipMemcpyHostToDevice, d.s) != hipSuccess ||
         hipMemcpyAsync(out, d.in.p, insize, hipMemcpyDeviceToHost, d.s) != hipSuccess ||
         hipStreamSynchronize(d.s) != hipSuccess)
