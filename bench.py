@@ -84,9 +84,7 @@ def traffic_for(kernel):
 
 def kernel_name(codec):
     """Compressor kernel the C-ABI launches for `codec` (api.cpp lzh_compress_kernel_only)."""
-    if codec == "snappy":
-        return "lzh_snappy_compress_kernel" if os.environ.get("LZH_SNAPPY_V1", "0") != "0" else "lzh_snappy_compress_v2_kernel"
-    return "lzh_lz4_compress_kernel" if os.environ.get("LZH_LZ4_V1", "0") != "0" else "lzh_lz4_compress_v2_kernel"
+    return "lzh_snappy_compress_v2_kernel" if codec == "snappy" else "lzh_lz4_compress_v2_kernel"
 
 
 def main():

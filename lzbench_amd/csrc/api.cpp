@@ -75,21 +75,11 @@ int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, s
     if (k > 0xffffffffu || chunk_size > 0x7fff0000u) return LZH_EARG;
     const size_t stride = lzh_stage_stride(codec, chunk_size);
     if (codec == LZH_CODEC_LZ4) {
-        static const bool use_v1 = getenv("LZH_LZ4_V1") && atoi(getenv("LZH_LZ4_V1")) != 0;
-        if (use_v1)
-            LZH_CHECK(lzh_launch_lz4_compress((const uint8_t*)d_in, n, in_readable, chunk_size, level < 1 ? 1 : level,
-                                              (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
-        else
-            LZH_CHECK(lzh_launch_lz4_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, level < 1 ? 1 : level,
-                                                 (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
+        LZH_CHECK(lzh_launch_lz4_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, level < 1 ? 1 : level,
+                                             (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
     } else if (codec == LZH_CODEC_SNAPPY) {
-        static const bool use_v1 = getenv("LZH_SNAPPY_V1") && atoi(getenv("LZH_SNAPPY_V1")) != 0;
-        if (use_v1)
-            LZH_CHECK(lzh_launch_snappy_compress((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
-                                                 stride, d_csizes, (uint32_t)k, s));
-        else
-            LZH_CHECK(lzh_launch_snappy_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size,
-                                                    (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
+        LZH_CHECK(lzh_launch_snappy_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
+                                                stride, d_csizes, (uint32_t)k, s));
     } else {
         return LZH_EARG;
     }

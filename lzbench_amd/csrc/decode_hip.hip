@@ -1,11 +1,11 @@
 // lzbench_amd/csrc/decode_hip.hip -- LZ4 and snappy block decoders for gfx950.
 //
-// One 64-lane wavefront per chunk.  The sequence/tag parse is wave-uniform: the compressed
-// stream is held in a 512-byte register window (two VGPRs across the wave) and read with
-// v_readlane, so token, length and offset bytes cost no memory round trip.  Literal and
-// match bytes are moved 64 lanes at a time.  Match sources are read back from the output
-// with L1-bypassing (sc1) loads after the wave's own earlier stores have drained, only
-// when the source overlaps bytes written since the last drain.
+// One 64-lane wavefront per chunk.  The compressed stream is read from a 512-byte register
+// window (two VGPRs across the wave: v_readlane / ds_bpermute, no memory round trip); the
+// last 4 KiB of decoded output stay in an LDS window (match sources there are LDS-to-LDS
+// copies) and leave for HBM as aligned dword stores; far match sources are read back from the
+// already-flushed output with L1-bypassing loads.  Sequences / tags are decoded a group at a
+// time (groups::), with a checked one-at-a-time path for everything a group does not take.
 //
 // Acceptance rules follow the reference decoders so malformed input is rejected:
 //   LZ4_decompress_safe   /root/reference/lz4/lz4.c:1707-1729, :1929-2151, :2170-2176
@@ -65,166 +65,18 @@ struct Win {
     }
 };
 
-__device__ __forceinline__ void copy_in_out(const Bytes& in, int src, const Bytes& out, int dst, int len, int lane) {
-    copy_span(in, src, out, dst, len, lane, LZH_WAVE);
-}
-
-// literal run in[src, src+len) -> out[dst..]: straight from the register window when it holds
-// the run (no memory round trip), else through memory
-__device__ __forceinline__ void copy_lit(const Win& w, const Bytes& in, int src, const Bytes& out, int dst, int len,
-                                         int lane) {
-    if (len <= 2 * LZH_WAVE && w.covers(src, src + len)) {
-        for (int base = 0; base < len; base += LZH_WAVE) {
-            const uint32_t v = w.lane_byte(src + base + lane);
-            if (base + lane < len) out.st8(dst + base + lane, v);
-        }
-        return;
-    }
-    copy_in_out(in, src, out, dst, len, lane);
-}
-
-// out[op + t] = out[op - off + (t mod off)] for t < len; all sources precede op
-__device__ __forceinline__ void copy_match(const Bytes& out, int op, int off, int len, int& flushed, int lane) {
-    const int src0 = op - off;
-    if (src0 + min(off, len) > flushed) { wait_vm(); flushed = op; }
-    for (int base = 0; base < len; base += LZH_WAVE) {
-        const int t = base + lane;
-        if (t < len) {
-            const int s = src0 + (off >= len ? t : (int)((uint32_t)t % (uint32_t)off));
-            const uint32_t v = out.b_sc1(s);
-            out.st8(op + t, v);
-        }
-    }
-}
-
 __device__ __forceinline__ void copy_raw(const Bytes& in, const Bytes& out, int len, int lane) {
     copy_span(in, 0, out, 0, len, lane, LZH_WAVE);
-}
-
-// returns decoded size or a negative error
-__device__ int lz4_decode(const Bytes& in, int cs, const Bytes& out, int cap, int lane) {
-    if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
-    if (cs <= 0) return -1;
-    Win w;
-    w.bind(in);
-    w.load(0, lane);
-    int ip = 0, op = 0, flushed = 0;
-    for (int guard = 0; guard <= cs; guard++) {
-        if (ip >= cs) return -ip - 1;
-        w.ensure(ip, lane);
-        const uint32_t tok = w.byte(ip++);
-        int lit = (int)(tok >> 4);
-        if (lit == 15) {
-            if (ip >= cs - 15) return -ip - 1;
-            for (int it = 0; it <= cs; it++) {
-                w.ensure(ip, lane);
-                const uint32_t s = w.byte(ip++);
-                lit += (int)s;
-                if (ip >= cs - 15 || s != 255) break;
-            }
-        }
-        if (op + lit > cap - 12 || ip + lit > cs - 8) {
-            if (ip + lit != cs || op + lit > cap) return -ip - 1;
-            copy_lit(w, in, ip, out, op, lit, lane);
-            op += lit;
-            break;
-        }
-        copy_lit(w, in, ip, out, op, lit, lane);
-        ip += lit;
-        op += lit;
-        w.ensure(ip, lane);
-        const int off = (int)(w.byte(ip) | (w.byte(ip + 1) << 8));
-        ip += 2;
-        int ml = (int)(tok & 15u);
-        if (ml == 15) {
-            for (int it = 0; it <= cs; it++) {
-                w.ensure(ip, lane);
-                const uint32_t s = w.byte(ip++);
-                ml += (int)s;
-                if (ip >= cs - 4) return -ip - 1;
-                if (s != 255) break;
-            }
-        }
-        ml += 4;
-        if (off > op) return -ip - 1;
-        if (op + ml > cap - 5) return -ip - 1;
-        if (off == 0) {   // reference leaves zeros here; never produced by a compressor
-            for (int base = 0; base < ml; base += LZH_WAVE) if (base + lane < ml) out.st8(op + base + lane, 0);
-        } else {
-            copy_match(out, op, off, ml, flushed, lane);
-        }
-        op += ml;
-    }
-    return op;
-}
-
-__device__ int snappy_decode(const Bytes& in, int cs, const Bytes& out, int cap, int lane) {
-    Win w;
-    w.bind(in);
-    w.load(0, lane);
-    int ip = 0;
-    uint32_t ulen = 0;
-    for (int shift = 0;; shift += 7) {
-        if (ip >= cs || shift >= 32) return -1;
-        const uint32_t c = w.byte(ip++);
-        const uint32_t val = c & 0x7fu;
-        if (shift == 28 && val > 15) return -1;
-        ulen |= val << shift;
-        if (c < 128) break;
-    }
-    if (ulen > (uint32_t)cap) return -1;
-    const int ul = (int)ulen;
-    int op = 0, flushed = 0;
-    for (int guard = 0; guard <= cs && ip < cs; guard++) {
-        w.ensure(ip, lane);
-        const uint32_t c = w.byte(ip++);
-        const uint32_t kind = c & 3u;
-        if (kind == 0) {
-            int len = (int)(c >> 2) + 1;
-            if (len > 60) {
-                const int nb = len - 60;
-                if (ip + nb > cs) return -1;
-                uint32_t v = 0;
-                for (int i = 0; i < nb; i++) v |= w.byte(ip + i) << (8 * i);
-                len = (int)v + 1;
-                if (v >= 0x7fffffffu) return -1;
-                ip += nb;
-            }
-            if ((int64_t)ip + len > cs || (int64_t)op + len > ul) return -1;
-            copy_lit(w, in, ip, out, op, len, lane);
-            ip += len;
-            op += len;
-        } else {
-            const int extra = kind == 1 ? 1 : (kind == 2 ? 2 : 4);
-            if (ip + extra > cs) return -1;
-            int len;
-            uint32_t off;
-            if (kind == 1) {
-                len = (int)((c >> 2) & 7u) + 4;
-                off = ((c >> 5) << 8) | w.byte(ip);
-            } else {
-                len = (int)(c >> 2) + 1;
-                off = 0;
-                for (int i = 0; i < extra; i++) off |= w.byte(ip + i) << (8 * i);
-            }
-            ip += extra;
-            if (off == 0 || off > (uint32_t)op || op + len > ul) return -1;
-            copy_match(out, op, (int)off, len, flushed, lane);
-            op += len;
-        }
-    }
-    return op == ul ? op : -1;
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
-// v2: output through an LDS window.  The last kW decoded bytes of the chunk stay in LDS, so a
-// match whose source lies in them (most of them: median offsets are a few KiB) is an
-// LDS-to-LDS copy with no memory round trip; decoded bytes leave for global memory as aligned
-// dword stores once 256 are pending.  Far matches read the (already flushed) output with
-// L1-bypassing loads.
-namespace dec2 {
+// Output through an LDS window.  The last kW decoded bytes of the chunk stay in LDS, so a
+// match whose source lies in them is an LDS-to-LDS copy with no memory round trip; decoded
+// bytes leave for global memory as aligned dword stores once 256 are pending.  Far matches read
+// the (already flushed) output with L1-bypassing loads.
+namespace owin {
 
 #ifndef LZH_DEC_KW
 #define LZH_DEC_KW 4096
@@ -312,144 +164,17 @@ struct Sink {
     }
 };
 
-// returns decoded size or a negative error (same acceptance rules as lz4_decode above)
-__device__ int lz4_decode(const Bytes& in, int cs, Sink& O, int cap, int lane) {
-    if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
-    if (cs <= 0) return -1;
-    Win w;
-    w.bind(in);
-    w.load(0, lane);
-    int ip = 0, op = 0;
-    for (int guard = 0; guard <= cs; guard++) {
-        ip = unii(ip); op = unii(op);
-        if (ip >= cs) return -ip - 1;
-        w.ensure(ip, lane);
-        const uint32_t tok = w.byte(ip++);
-        int lit = (int)(tok >> 4);
-        if (lit == 15) {
-            if (ip >= cs - 15) return -ip - 1;
-            for (int it = 0; it <= cs; it++) {
-                w.ensure(ip, lane);
-                const uint32_t s = w.byte(ip++);
-                lit += (int)s;
-                if (ip >= cs - 15 || s != 255) break;
-            }
-        }
-        if (op + lit > cap - 12 || ip + lit > cs - 8) {
-            if (ip + lit != cs || op + lit > cap) return -ip - 1;
-            O.literals(w, in, ip, op, lit, lane);
-            op += lit;
-            break;
-        }
-        O.literals(w, in, ip, op, lit, lane);
-        ip += lit;
-        op += lit;
-        w.ensure(ip, lane);
-        const int off = (int)(w.byte(ip) | (w.byte(ip + 1) << 8));
-        ip += 2;
-        int ml = (int)(tok & 15u);
-        if (ml == 15) {
-            for (int it = 0; it <= cs; it++) {
-                w.ensure(ip, lane);
-                const uint32_t s = w.byte(ip++);
-                ml += (int)s;
-                if (ip >= cs - 4) return -ip - 1;
-                if (s != 255) break;
-            }
-        }
-        ml += 4;
-        if (off > op) return -ip - 1;
-        if (op + ml > cap - 5) return -ip - 1;
-        if (off == 0) {   // reference leaves zeros here; never produced by a compressor
-            for (int base = 0; base < ml; base += LZH_WAVE) {
-                if (base + lane < ml) O.put(op + base + lane, 0);
-                O.maybe_flush(op + min(base + LZH_WAVE, ml), lane);
-            }
-        } else {
-            O.match(op, off, ml, lane);
-        }
-        op += ml;
-    }
-    return op;
-}
-
-__device__ int snappy_decode(const Bytes& in, int cs, Sink& O, int cap, int lane) {
-    Win w;
-    w.bind(in);
-    w.load(0, lane);
-    int ip = 0;
-    uint32_t ulen = 0;
-    for (int shift = 0;; shift += 7) {
-        if (ip >= cs || shift >= 32) return -1;
-        const uint32_t c = w.byte(ip++);
-        const uint32_t val = c & 0x7fu;
-        if (shift == 28 && val > 15) return -1;
-        ulen |= val << shift;
-        if (c < 128) break;
-    }
-    if (ulen > (uint32_t)cap) return -1;
-    const int ul = (int)ulen;
-    int op = 0;
-    for (int guard = 0; guard <= cs && ip < cs; guard++) {
-        ip = unii(ip); op = unii(op);
-        w.ensure(ip, lane);
-        const uint32_t c = w.byte(ip++);
-        const uint32_t kind = c & 3u;
-        if (kind == 0) {
-            int len = (int)(c >> 2) + 1;
-            if (len > 60) {
-                const int nb = len - 60;
-                if (ip + nb > cs) return -1;
-                uint32_t v = 0;
-                for (int i = 0; i < nb; i++) v |= w.byte(ip + i) << (8 * i);
-                len = (int)v + 1;
-                if (v >= 0x7fffffffu) return -1;
-                ip += nb;
-            }
-            if ((int64_t)ip + len > cs || (int64_t)op + len > ul) return -1;
-            O.literals(w, in, ip, op, len, lane);
-            ip += len;
-            op += len;
-        } else {
-            const int extra = kind == 1 ? 1 : (kind == 2 ? 2 : 4);
-            if (ip + extra > cs) return -1;
-            int len;
-            uint32_t off;
-            if (kind == 1) {
-                len = (int)((c >> 2) & 7u) + 4;
-                off = ((c >> 5) << 8) | w.byte(ip);
-            } else {
-                len = (int)(c >> 2) + 1;
-                off = 0;
-                for (int i = 0; i < extra; i++) off |= w.byte(ip + i) << (8 * i);
-            }
-            ip += extra;
-            if (off == 0 || off > (uint32_t)op || op + len > ul) return -1;
-            O.match(op, (int)off, len, lane);
-            op += len;
-        }
-    }
-    return op == ul ? op : -1;
-}
-
-}  // namespace dec2
+}  // namespace owin
 
 // ---------------------------------------------------------------------------------------
-// v3: LZ4 sequences decoded a group at a time.  Every lane parses "a token at ip + lane" from
-// the register window; a short scalar walk picks the real chain of short sequences (no
-// length bytes) and records them lane-indexed; then each lane assembles one output byte per
-// pass (its sequence found by a popcount over the sequence-start mask): literal bytes come
-// from the register window, match bytes from the LDS output window (byte-by-byte overlap
-// semantics through the source rule src = match_start - off + (k mod off)), in dependency
-// rounds when a source lies in the same pass.  Sequences the group path cannot take (length
-// bytes, the last sequence, any rule violation) run through the v2 per-sequence path, which
-// applies the reference acceptance rules.
-namespace dec3 {
+// One LZ4 sequence at a time with every acceptance rule of LZ4_decompress_safe (lz4.c:1707-1729,
+// :1929-2151): the path for what a group does not take (255-run lengths, the last-literals
+// sequence, malformed input).  Returns 0 = continue, 1 = done (last literals), < 0 = error.
+namespace checked {
 
-using dec2::kW;
+using owin::kW;
 
-// decodes one sequence the v2 way; returns 0 = continue, 1 = done (last literals), <0 error
-__device__ __forceinline__ int lz4_one(const Bytes& in, int cs, dec2::Sink& O, Win& w, int cap, int& ip, int& op,
+__device__ __forceinline__ int lz4_one(const Bytes& in, int cs, owin::Sink& O, Win& w, int cap, int& ip, int& op,
                                        int lane) {
     if (ip >= cs) return -ip - 1;
     w.ensure(ip, lane);
@@ -501,116 +226,21 @@ __device__ __forceinline__ int lz4_one(const Bytes& in, int cs, dec2::Sink& O, W
     return 0;
 }
 
-constexpr int kGroupOut = 4 * LZH_WAVE;      // output bytes per group (4 passes)
-
-__device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, int cap, int lane) {
-    if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
-    if (cs <= 0) return -1;
-    Win w;
-    w.bind(in);
-    w.load(0, lane);
-    int ip = 0, op = 0;
-    for (int guard = 0; guard <= cs; guard++) {
-        ip = unii(ip); op = unii(op);
-        O.flushed = unii(O.flushed); O.ringlo = unii(O.ringlo);
-        // ---- every lane parses a token at ip + lane
-        if (!w.covers(ip, ip + 2 * LZH_WAVE)) w.load(ip, lane);
-        const uint32_t tw = w.lane_word(ip + lane);
-        const uint32_t lit_l = (tw >> 4) & 15u, mlc_l = tw & 15u;
-        const uint32_t ow = w.lane_word(ip + lane + 1 + (int)lit_l);
-        const uint32_t info = (ow & 0xffffu) | (lit_l << 16) | (mlc_l << 20) |
-                              ((lit_l == 15u || mlc_l == 15u) ? (1u << 24) : 0u);
-        // ---- scalar walk over the chain of short sequences
-        uint32_t A = 0, B = 0;                  // lane k: sequence k (A: j | lit<<8 | mlc<<12, B: out start | off<<16)
-        uint64_t S0 = 0, S1 = 0, S2 = 0, S3 = 0;  // sequence starts in the group's output
-        int k = 0, o = 0, x = ip;
-        for (; k < LZH_WAVE; k++) {
-            const int j = x - ip;
-            if (j >= LZH_WAVE) break;
-            const uint32_t inf = rdlane(info, j);
-            const int lit = (int)((inf >> 16) & 15u), mlc = (int)((inf >> 20) & 15u), off = (int)(inf & 0xffffu);
-            if (inf >> 24) break;                                          // length bytes
-            const int opm = op + o + lit;
-            if (opm > cap - 12 || x + 1 + lit > cs - 8) break;             // last literals / malformed
-            if (off == 0 || off > opm || opm + mlc + 4 > cap - 5) break;   // left to the checked path
-            if (o + lit + mlc + 4 > kGroupOut) break;
-            A = (lane == k) ? ((uint32_t)j | ((uint32_t)lit << 8) | ((uint32_t)mlc << 12)) : A;
-            B = (lane == k) ? ((uint32_t)o | ((uint32_t)off << 16)) : B;
-            const uint64_t bit = 1ull << (o & 63);
-            if (o < 64) S0 |= bit; else if (o < 128) S1 |= bit; else if (o < 192) S2 |= bit; else S3 |= bit;
-            o += lit + mlc + 4;
-            x += 3 + lit;
-        }
-        if (k == 0) {
-            const int r = lz4_one(in, cs, O, w, cap, ip, op, lane);
-            if (r < 0) return r;
-            if (r == 1) break;
-            continue;
-        }
-        // ---- assemble the group's output, one byte per lane per pass
-        const int total = o;
-        int before = 0;                                 // sequence starts in earlier passes
-        for (int pass = 0; pass * LZH_WAVE < total; pass++) {
-            const uint64_t Sp = pass == 0 ? S0 : (pass == 1 ? S1 : (pass == 2 ? S2 : S3));
-            const int ob = pass * LZH_WAVE + lane;
-            const bool act = ob < total;
-            const int kk = before + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(Sp >> 32),
-                                        __builtin_amdgcn_mbcnt_lo((uint32_t)Sp, 0u)) +
-                           (int)((Sp >> lane) & 1ull) - 1;
-            const uint32_t a = lane_gather(A, kk), b = lane_gather(B, kk);
-            const int jk = (int)(a & 255u), litk = (int)((a >> 8) & 15u);
-            const int ostart = (int)(b & 0xffffu), offk = (int)(b >> 16);
-            const int u = ob - ostart;
-            const bool is_lit = u < litk;
-            const uint32_t lb = w.lane_byte(ip + jk + 1 + (is_lit ? u : 0));
-            const int mu = u - litk;
-            const int mstart = op + ostart + litk;
-            const int src = mstart - offk + (mu < offk ? mu : (int)((uint32_t)mu % (uint32_t)max(offk, 1)));
-            const int pbase = op + pass * LZH_WAVE;
-            const bool near = !is_lit && src >= O.ringlo && src >= pbase + LZH_WAVE - kW;
-            const bool inpass = !is_lit && src >= pbase;
-            uint32_t v = is_lit ? lb : (near && !inpass ? O.get(src) : 0u);
-            bool done = is_lit || (near && !inpass);
-            const bool far = act && !is_lit && !near;
-            if (ballot(far)) {   // far sources were flushed long ago: their stores must be done
-                wait_vm();
-                if (far) v = O.out.b_sc1(src);
-                done = done || far;
-            }
-            if (act && done) O.put(op + ob, v);
-            uint64_t dm = ballot(act && done) | ~ballot(act);
-            for (int r = 0; r < LZH_WAVE && ~dm; r++) {
-                const bool pend = !((dm >> lane) & 1ull);
-                const int sl = src - pbase;
-                const bool ready = pend && ((dm >> (sl & 63)) & 1ull);
-                const uint32_t vv = O.get(src);
-                if (ready) O.put(op + ob, vv);
-                dm |= ballot(ready);
-            }
-            before += __builtin_popcountll(Sp);
-            O.maybe_flush(min(pbase + LZH_WAVE, op + total), lane);
-        }
-        op += total;
-        ip = x;
-    }
-    return op;
-}
-
-}  // namespace dec3
+}  // namespace checked
 
 // ---------------------------------------------------------------------------------------
-// v4: LZ4 groups resolved lane-parallel.  Every lane parses "a sequence at ip + lane" in full
-// (token, one literal-length byte, offset, one match-length byte) from the register window; a
-// scalar walk over the per-lane next-token links picks the real chain (a few instructions per
-// sequence); the reference acceptance rules are checked per member lane against a DPP prefix
-// sum of the output lengths, and the chain is cut before the first member that fails them (it,
-// the last sequence and sequences with 255-run lengths go through the checked v2 path).  Output
-// bytes are assembled one per lane per pass: the owning sequence is found from per-pass start
-// marks in LDS, literal bytes come from the register window, match bytes from the LDS output
-// window (or global memory for far sources) in dependency rounds.
-namespace dec4 {
+// Groups resolved lane-parallel.  Every lane parses "a sequence at ip + lane" in full (token, one
+// literal-length byte, offset, one match-length byte) from the register window; a scalar walk
+// over the per-lane next-token links picks the real chain (a few instructions per sequence);
+// the reference acceptance rules are checked per member lane against a DPP prefix sum of the
+// output lengths, and the chain is cut before the first member that fails them (it, the last
+// sequence and sequences with 255-run lengths go through the checked path).  Output bytes are
+// assembled one per lane per pass: the owning sequence is found from per-pass start marks in
+// LDS, literal bytes come from the register window, match bytes from the LDS output window (or
+// global memory for far sources) in dependency rounds.
+namespace groups {
 
-using dec2::kW;
+using owin::kW;
 
 __device__ __forceinline__ int wave_incl_scan(int x) {
     x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
@@ -626,7 +256,7 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 // litk literal bytes from stream position ip + lrel, then mlk match bytes copied from offset offk
 // (byte-by-byte semantics); a literal-only member has mlk = 0, a copy-only member litk = 0.
 // One output byte per lane per pass; the owner is the last start mark at or before the byte.
-__device__ __forceinline__ void emit_group(const Win& w, dec2::Sink& O, LDSA uint8_t* mark, int ip, int op,
+__device__ __forceinline__ void emit_group(const Win& w, owin::Sink& O, LDSA uint8_t* mark, int ip, int op,
                                            int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
                                            int off, int lane) {
     const bool kmem = (keep >> lane) & 1ull;
@@ -684,7 +314,7 @@ __device__ __forceinline__ void emit_group(const Win& w, dec2::Sink& O, LDSA uin
     }
 }
 
-__device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
+__device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
     if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
     if (cs <= 0) return -1;
     Win w;
@@ -731,7 +361,7 @@ __device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_t* 
         const uint64_t badm = ballot(bad);
         const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
         if (!keep) {
-            const int r = dec3::lz4_one(in, cs, O, w, cap, ip, op, lane);
+            const int r = checked::lz4_one(in, cs, O, w, cap, ip, op, lane);
             if (r < 0) return r;
             if (r == 1) break;
             continue;
@@ -753,7 +383,7 @@ __device__ int lz4_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_t* 
 // of snappy_decode below (snappy.cc:848-952) are checked per member against the prefix sum, and
 // the group is cut before the first failure (which, like 2..4-byte literal lengths, runs through
 // the checked per-tag path).
-__device__ int snappy_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
+__device__ int snappy_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
     Win w;
     w.bind(in);
     w.load(0, lane);
@@ -823,7 +453,7 @@ __device__ int snappy_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_
         const uint64_t badm = ballot(bad);
         const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
         if (!keep) {
-            // one tag through the checked path (dec2 rules)
+            // one tag through the checked path (snappy.cc:848-952 rules)
             const uint32_t cc = w.byte(ip++);
             const uint32_t kk = cc & 3u;
             if (kk == 0) {
@@ -872,13 +502,13 @@ __device__ int snappy_decode(const Bytes& in, int cs, dec2::Sink& O, LDSA uint8_
     return op == ul ? op : -1;
 }
 
-}  // namespace dec4
+}  // namespace groups
 
 extern "C" __global__ void __launch_bounds__(64)
 lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                          const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                          int32_t* status, uint32_t chunk0) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[dec2::kW + LZH_WAVE];   // output window | start marks
+    __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + LZH_WAVE];   // output window | start marks
     const int lane = threadIdx.x;
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t ooff = chunk * chunk_size;
@@ -895,59 +525,20 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
         copy_raw(rin, rout, part, lane);
         r = part;
     } else {
-        dec2::Sink O{(LDSA uint8_t*)win, rout, 0, 0};
-#ifdef LZH_DEC_V3
-        r = codec == 0 ? dec3::lz4_decode(rin, cs, O, part, lane) : dec2::snappy_decode(rin, cs, O, part, lane);
-#else
-        r = codec == 0 ? dec4::lz4_decode(rin, cs, O, (LDSA uint8_t*)win + dec2::kW, part, lane)
-                       : dec4::snappy_decode(rin, cs, O, (LDSA uint8_t*)win + dec2::kW, part, lane);
-#endif
+        owin::Sink O{(LDSA uint8_t*)win, rout, 0, 0};
+        r = codec == 0 ? groups::lz4_decode(rin, cs, O, (LDSA uint8_t*)win + owin::kW, part, lane)
+                       : groups::snappy_decode(rin, cs, O, (LDSA uint8_t*)win + owin::kW, part, lane);
         if (r > 0) O.flush(r, lane);
     }
     if (lane == 0) status[chunk] = r;
 }
 
-// codec: 0 = lz4, 1 = snappy, 2 = raw copy only.  offsets[i] = byte offset of chunk i in
-// `packed`; a chunk whose csize equals its size was stored raw (lzbench.cpp:311-315).
-extern "C" __global__ void __launch_bounds__(64)
-lzh_decompress_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
-                      const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
-                      int32_t* status, uint32_t chunk0) {
-    const int lane = threadIdx.x;
-    const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
-    const uint64_t ooff = chunk * chunk_size;
-    if (ooff >= n_total) return;
-    const int part = (int)min(chunk_size, n_total - ooff);
-    const uint64_t ioff = offsets[chunk];
-    const int cs = (int)csizes[chunk];
-    const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
-    Bytes rin, rout;
-    rin.init(packed + ioff, readable);
-    rout.init(out + ooff, (uint64_t)part);
-    int r;
-    if (cs == part || codec == 2) {
-        copy_raw(rin, rout, part, lane);
-        r = part;
-    } else if (codec == 0) {
-        r = lz4_decode(rin, cs, rout, part, lane);
-    } else {
-        r = snappy_decode(rin, cs, rout, part, lane);
-    }
-    if (lane == 0) status[chunk] = r;
-}
-
 #include "launch.h"
-#include <stdlib.h>
 hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                  const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                  int32_t* status, uint32_t nchunks, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
-    static const bool use_v1 = getenv("LZH_DEC_V1") && atoi(getenv("LZH_DEC_V1")) != 0;
-    if (use_v1)
-        hipLaunchKernelGGL(lzh_decompress_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
-                           offsets, csizes, n_total, chunk_size, out, status, 0u);
-    else
-        hipLaunchKernelGGL(lzh_decompress_v2_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
-                           offsets, csizes, n_total, chunk_size, out, status, 0u);
+    hipLaunchKernelGGL(lzh_decompress_v2_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
+                       offsets, csizes, n_total, chunk_size, out, status, 0u);
     return hipGetLastError();
 }

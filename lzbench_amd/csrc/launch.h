@@ -4,14 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-hipError_t lzh_launch_lz4_compress(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
-                                   int acc, uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
-                                   hipStream_t s);
 hipError_t lzh_launch_lz4_compress_v2(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                                       int acc, uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
-                                      hipStream_t s);
-hipError_t lzh_launch_snappy_compress(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
-                                      uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
                                       hipStream_t s);
 hipError_t lzh_launch_snappy_compress_v2(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                                          uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,

@@ -156,9 +156,6 @@ struct SeqLayout {
 // Common case (<= 256 bytes, literals in the input ring): assembled in the output ring.
 __device__ __forceinline__ int emit_seq(const Bytes& in, const Ring& R, const Bytes& out, OutRing& O, int op,
                                         int anchor, int lit, bool has_match, int off, int ml, int lane) {
-#ifdef LZH_EXP_NOEMIT
-    if (has_match) return op + 3 + lit;
-#endif
     // (ml counts match bytes beyond the 4-byte minimum, as the token does)
     if (has_match && lit < 15 && ml < 15 && R.has(anchor, anchor + 16)) {
         // short sequence (no length bytes): token, lit literals, 2-byte offset
@@ -259,16 +256,8 @@ __device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const B
             const int o = (int)lane_gather(off, k), m = (int)lane_gather(mlx, k);
             const int t = ob - (int)lane_gather(st, k);
             const SeqLayout S(l, true, m);
-#ifdef LZH_EXP_NOLB
-            const uint32_t lb = a;
-#else
             const uint32_t lb = R.byte(a + t - S.lit0);
-#endif
-#ifdef LZH_EXP_NOPUT
-            if (S.byte(t, lb, o) == 12345) O.put(op + ob, 1);
-#else
             if (ob < tot) O.put(op + ob, S.byte(t, lb, o));
-#endif
         }
         return op + tot;      // (flushed by the caller after its load wait: no store in that wait)
     }
@@ -604,11 +593,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 const uint64_t below = (1ull << lane) - 1ull;
                 bool okp = false;                                      // evaluation against lane prev
                 int bep = 0, lep = 0;
-#ifdef LZH_EXP_NOGROUPS
-                if (false) {
-#else
                 if (losers) {
-#endif
                     LZ_STAT(1, 1);
                     // slot groups without a loop: every lane of a slot read back the same claim
                     // winner W (whichever lane the hardware let win), so equal W <=> same slot;
@@ -717,9 +702,6 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         endp = endip || (eL < LZH_WAVE && LZH_WAVE - 1 >= fv);   // or the search ran past mflimit
                     }
                     I = (Mm ? I : 0ull) | I0 | E;                          // (no stale bits from an earlier round)
-#ifdef LZH_EXP_NOVERIFY
-                    break;
-#endif
                     if (!(coll & E)) break;
                     const uint64_t mk = grp & below & I;
                     const int kt = mk ? 63 - __builtin_clzll(mk) : -1;
@@ -808,9 +790,6 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     }
                     // table: the last inserted lane of each slot, or the slot's old value
                     const bool inI = (I >> lane) & 1ull;
-#ifdef LZH_EXP_NORESTORE
-                    if (true) {} else
-#endif
                     if (!losers) {
                         if (valid && !inI) T.put(h, old);
                     } else {
