@@ -231,7 +231,7 @@ __device__ __forceinline__ int lz4_one(const Bytes& in, int cs, owin::Sink& O, W
 // ---------------------------------------------------------------------------------------
 // Groups resolved lane-parallel.  Every lane parses "a sequence at ip + lane" in full (token, one
 // literal-length byte, offset, one match-length byte) from the register window; a scalar walk
-// over the per-lane next-token links picks the real chain (a few instructions per sequence);
+// over the per-lane next-token links (binary lifting, chain_members) picks the real chain;
 // the reference acceptance rules are checked per member lane against a DPP prefix sum of the
 // output lengths, and the chain is cut before the first member that fails them (it, the last
 // sequence and sequences with 255-run lengths go through the checked path).  Output bytes are
@@ -314,6 +314,27 @@ __device__ __forceinline__ void emit_group(const Win& w, owin::Sink& O, LDSA uin
     }
 }
 
+// Lanes on the chain that starts at lane 0 and follows `link` (next lane, strictly increasing;
+// >= 64 = leaves the group, 255 = the lane itself is not taken), by binary lifting: jump tables
+// J_k = link^(2^k) through ds_bpermute, then every lane lifts from lane 0 to the furthest chain
+// lane <= itself.  No scalar walk (the decoder is scalar-issue bound).
+__device__ __forceinline__ uint64_t chain_members(int link, int lane) {
+    const int J0 = min(link, LZH_WAVE);
+    const int J1 = J0 < LZH_WAVE ? (int)lane_gather((uint32_t)J0, J0) : LZH_WAVE;
+    const int J2 = J1 < LZH_WAVE ? (int)lane_gather((uint32_t)J1, J1) : LZH_WAVE;
+    const int J3 = J2 < LZH_WAVE ? (int)lane_gather((uint32_t)J2, J2) : LZH_WAVE;
+    const int J4 = J3 < LZH_WAVE ? (int)lane_gather((uint32_t)J3, J3) : LZH_WAVE;
+    const int J5 = J4 < LZH_WAVE ? (int)lane_gather((uint32_t)J4, J4) : LZH_WAVE;
+    int x = 0, y;
+    y = (int)lane_gather((uint32_t)J5, x); x = y <= lane ? y : x;
+    y = (int)lane_gather((uint32_t)J4, x); x = y <= lane ? y : x;
+    y = (int)lane_gather((uint32_t)J3, x); x = y <= lane ? y : x;
+    y = (int)lane_gather((uint32_t)J2, x); x = y <= lane ? y : x;
+    y = (int)lane_gather((uint32_t)J1, x); x = y <= lane ? y : x;
+    y = (int)lane_gather((uint32_t)J0, x); x = y <= lane ? y : x;
+    return ballot(x == lane && link != 255);
+}
+
 __device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
     if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
     if (cs <= 0) return -1;
@@ -340,16 +361,7 @@ __device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* 
         const bool cplx = !inwin || (ln == 15 && b1 == 255) || (mc == 15 && b2 == 255);
         const int link = cplx ? 255 : pe - ip;
         // ---- the real chain from lane 0
-        uint64_t M = 0;
-        int j = 0;
-        int nj;
-        for (;;) {                                                  // (links strictly increase)
-            nj = rdlanei(link, j);
-            if (nj >= LZH_WAVE) break;
-            M |= 1ull << j;
-            j = nj;
-        }
-        if (nj != 255) M |= 1ull << j;
+        const uint64_t M = chain_members(link, lane);
         // ---- acceptance rules per member (as lz4_one); the chain ends before the first failure
         const bool mem = (M >> lane) & 1ull;
         const int L = mem ? lit + ml : 0;
@@ -435,15 +447,7 @@ __device__ int snappy_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_
         const bool inwin = w.covers(x, nx + 4);
         // link: next tag lane; 255 = not parsed here; 254 = the stream ends after this tag
         const int link = (cplx || !inwin || x >= cs) ? 255 : (nx >= cs ? 254 : nx - ip);
-        uint64_t M = 0;
-        int j = 0, nj;
-        for (;;) {                                                  // (links strictly increase)
-            nj = rdlanei(link, j);
-            if (nj >= LZH_WAVE) break;
-            M |= 1ull << j;
-            j = nj;
-        }
-        if (nj != 255) M |= 1ull << j;
+        const uint64_t M = chain_members(link, lane);
         const bool mem = (M >> lane) & 1ull;
         const int L = mem ? len : 0;
         const int incl = wave_incl_scan(L);
