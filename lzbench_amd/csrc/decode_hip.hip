@@ -230,8 +230,8 @@ __device__ __forceinline__ int lz4_one(const Bytes& in, int cs, owin::Sink& O, W
 
 // ---------------------------------------------------------------------------------------
 // Groups resolved lane-parallel.  Every lane parses "a sequence at ip + lane" in full (token, one
-// literal-length byte, offset, one match-length byte) from the register window; a scalar walk
-// over the per-lane next-token links (binary lifting, chain_members) picks the real chain;
+// literal-length byte, offset, one match-length byte) from the register window; binary lifting
+// over the per-lane next-token links (chain_members) picks the real chain;
 // the reference acceptance rules are checked per member lane against a DPP prefix sum of the
 // output lengths, and the chain is cut before the first member that fails them (it, the last
 // sequence and sequences with 255-run lengths go through the checked path).  Output bytes are
