@@ -15,6 +15,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int unii(int v) { return (int)__builtin_amdgcn_readfirstlane((uint32_t)v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
     uint64_t a = (uint64_t)p;

@@ -460,6 +460,43 @@ __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t los
     }
 }
 
+// Records of a run batch (anchor, literals, offset, match length, output start per member
+// lane), built from the batch's pending resolve state: catch-up bounded by the previous match end
+// (lz4.c:1017-1020), lengths, DPP prefix sum of the output sizes.
+#define RUN_RECORDS()                                                                              \
+    do {                                                                                           \
+        if (pr_m) {                                                                                \
+            LZ_STAT(3, __builtin_popcountll(pr_m));                                                \
+            const uint64_t below_ = (1ull << lane) - 1ull;                                         \
+            const int p_ = pr_base + lane;                                                         \
+            const bool mem_ = (pr_m >> lane) & 1ull;                                               \
+            const uint64_t mb_ = pr_m & below_;                                                    \
+            const int jp_ = mb_ ? 63 - __builtin_clzll(mb_) : lane;                                \
+            const int ep_ = (int)lane_gather((uint32_t)pr_e, jp_);                                 \
+            const int anc_ = mb_ ? pr_base + ep_ : pr_anchor;                                      \
+            const int maxb_ = min(p_ - anc_, (int)pr_ce);                                          \
+            int bk_ = min(pr_be, maxb_);                                                           \
+            const bool scu_ = mem_ && pr_be == 4 && maxb_ > 4;                                     \
+            for (uint64_t sm_ = ballot(scu_); sm_; sm_ &= sm_ - 1) {                               \
+                LZ_STAT(5, 1);                                                                     \
+                const int k_ = __builtin_ctzll(sm_);                                               \
+                const int b_ = slow_catchup(in, pr_base + k_, rdlanei((int)pr_ce, k_), rdlanei(anc_, k_), lane); \
+                bk_ = lane == k_ ? b_ : bk_;                                                       \
+            }                                                                                      \
+            const int lit_ = p_ - bk_ - anc_, mlx_ = bk_ + pr_cn;                                  \
+            const int L_ = mem_ ? 3 + lit_ + ext_len_bytes(lit_) + ext_len_bytes(mlx_) : 0;        \
+            const int incl_ = wave_incl_scan(L_);                                                  \
+            rc_anc = (uint32_t)anc_;                                                               \
+            rc_lit = (uint32_t)lit_;                                                               \
+            rc_off = (uint32_t)(p_ - (int)pr_ce);                                                  \
+            rc_mlx = (uint32_t)mlx_;                                                               \
+            rc_st = (uint32_t)(incl_ - L_);                                                        \
+            rc_m = pr_m;                                                                           \
+            rc_tot = rdlanei(incl_, 63);                                                           \
+            pr_m = 0;                                                                              \
+        }                                                                                          \
+    } while (0)
+
 template <bool kSmall, bool kStats>
 __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab,
                                LDSA uint32_t* ringw, LDSA uint8_t* outb, uint32_t* out_size,
@@ -489,6 +526,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
 
     int op = 0, anchor = 0;
     RECS_DECL;                               // sequences waiting to be emitted
+    uint64_t pr_m = 0;                       // a run batch whose records are not built yet
+    int pr_base = 0, pr_anchor = 0, pr_e = 0, pr_cn = 0, pr_be = 0;
+    uint32_t pr_ce = 0;
 
     if (n >= kMinLength) {
         const int mfl1 = n - kMfLimit + 1;
@@ -563,7 +603,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             MWin W;
             W.load(in, cand, valid);
             LZ_CLK(1);                                                 // table read/claim/read back, loads issued
-            // ---- deferred emission (LDS work under the loads above)
+            // ---- deferred records + emission of the previous batch (under the loads above)
+            pr_m = uni64(pr_m); pr_base = unii(pr_base); pr_anchor = unii(pr_anchor);
+            RUN_RECORDS();
             RECS_EMIT();
             rc_m = 0;
             rc_tot = 0;
@@ -740,33 +782,8 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 }
                 LZ_CLK(5);                                             // chain resolve
                 // ---- records of the members (emitted under the next batch's loads)
-                if (Mm) {
-                    LZ_STAT(3, __builtin_popcountll(Mm));
-                    const bool mem = (Mm >> lane) & 1ull;
-                    const uint64_t mb = Mm & below;
-                    const int jp = mb ? 63 - __builtin_clzll(mb) : lane;
-                    const int ep = (int)lane_gather((uint32_t)e, jp);
-                    const int anc = mb ? base + ep : anchor;           // previous match end (or anchor)
-                    const int maxb = min(p - anc, (int)ce);
-                    int bk = min(be, maxb);
-                    const bool scu = mem && be == 4 && maxb > 4;       // catch-up past the window
-                    for (uint64_t sm = ballot(scu); sm; sm &= sm - 1) {
-                        LZ_STAT(5, 1);
-                        const int k = __builtin_ctzll(sm);
-                        const int b = slow_catchup(in, base + k, rdlanei((int)ce, k), rdlanei(anc, k), lane);
-                        bk = lane == k ? b : bk;
-                    }
-                    const int lit = p - bk - anc, mlx = bk + cn;
-                    const int L = mem ? 3 + lit + ext_len_bytes(lit) + ext_len_bytes(mlx) : 0;
-                    const int incl = wave_incl_scan(L);
-                    rc_anc = (uint32_t)anc;
-                    rc_lit = (uint32_t)lit;
-                    rc_off = (uint32_t)(p - (int)ce);
-                    rc_mlx = (uint32_t)mlx;
-                    rc_st = (uint32_t)(incl - L);
-                    rc_m = Mm;
-                    rc_tot = rdlanei(incl, 63);
-                }
+                // the sequences' records are built under the next batch's loads (RUN_RECORDS)
+                pr_m = Mm; pr_base = base; pr_anchor = anchor; pr_e = e; pr_cn = cn; pr_be = be; pr_ce = ce;
                 LZ_CLK(6);                                             // records
                 if (endp) {
                     go = false;
@@ -895,6 +912,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
     wait_vm();
     R.ready = R.fill;
     wave_lds_fence();
+    RUN_RECORDS();
     RECS_EMIT();
     if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
     op = emit_seq(in, R, out, O, op, anchor, n - anchor, false, 0, 0, lane);
