@@ -261,11 +261,15 @@ __device__ __forceinline__ void emit_group(const Win& w, owin::Sink& O, LDSA uin
                                            int off, int lane) {
     const bool kmem = (keep >> lane) & 1ull;
     int carry = 63 - __builtin_clzll(keep);                      // (pass 0 always has a start at 0)
+    // Branch-free pass body: lanes that have nothing to store write to harmless places (the mark
+    // scratch's second half, or output bytes past `total` / of this pass that a later round or
+    // group overwrites before any flush), so no exec-mask juggling per conditional access.
     for (int pass = 0; pass * LZH_WAVE < total; pass++) {
         const int pb = pass * LZH_WAVE;
         mark[lane] = 0xff;
         wave_lds_fence();
-        if (kmem && excl >= pb && excl < pb + LZH_WAVE) mark[excl - pb] = (uint8_t)lane;
+        const bool mine = kmem && excl >= pb && excl < pb + LZH_WAVE;
+        mark[mine ? excl - pb : LZH_WAVE + lane] = (uint8_t)lane;
         wave_lds_fence();
         const int mv = (int)mark[lane];
         const uint64_t S = ballot(mv != 0xff);
@@ -287,27 +291,30 @@ __device__ __forceinline__ void emit_group(const Win& w, owin::Sink& O, LDSA uin
         const int mstart = op + ek + litk;
         int src = mstart - offk + mu;
         if (ballot(act && !is_lit && mu >= offk)) {                // overlapping copy: period offk
-            if (!is_lit && mu >= offk) src = mstart - offk + (int)((uint32_t)mu % (uint32_t)max(offk, 1));
+            const int md = (int)((uint32_t)mu % (uint32_t)max(offk, 1));
+            src = (!is_lit && mu >= offk) ? mstart - offk + md : src;
         }
         const int pbase = op + pb;
         const bool near = !is_lit && src >= O.ringlo && src >= pbase + LZH_WAVE - kW;
         const bool inpass = !is_lit && src >= pbase;
-        uint32_t v = is_lit ? lb : (near && !inpass ? O.get(src) : 0u);
+        const uint32_t g = O.get(src);
+        uint32_t v = is_lit ? lb : g;
         bool done = is_lit || (near && !inpass);
         const bool far = act && !is_lit && !near;
         if (ballot(far)) {   // far sources were flushed long ago: their stores must be done
             wait_vm();
-            if (far) v = O.out.b_sc1(src);
+            const uint32_t gv = O.out.b_sc1(far ? src : 0);
+            v = far ? gv : v;
             done = done || far;
         }
-        if (act && done) O.put(op + ob, v);
+        O.put(op + ob, v);
         uint64_t dm = ballot(act && done) | ~ballot(act);
         for (int r = 0; r < LZH_WAVE && ~dm; r++) {
-            const bool pend = !((dm >> lane) & 1ull);
             const int sl = src - pbase;
-            const bool ready = pend && ((dm >> (sl & 63)) & 1ull);
+            const bool ready = !((dm >> lane) & 1ull) && ((dm >> (sl & 63)) & 1ull);
             const uint32_t vv = O.get(src);
-            if (ready) O.put(op + ob, vv);
+            v = ready ? vv : v;
+            O.put(op + ob, v);
             dm |= ballot(ready);
         }
         O.maybe_flush(min(pbase + LZH_WAVE, op + total), lane);
@@ -512,7 +519,7 @@ extern "C" __global__ void __launch_bounds__(64)
 lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                          const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                          int32_t* status, uint32_t chunk0) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + LZH_WAVE];   // output window | start marks
+    __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + 2 * LZH_WAVE];   // output window | start marks
     const int lane = threadIdx.x;
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t ooff = chunk * chunk_size;
