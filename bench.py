@@ -109,7 +109,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))   # (ranks > GPUs only in rehearsal runs)
     dist = None
     if world > 1:
         import torch.distributed as dist
