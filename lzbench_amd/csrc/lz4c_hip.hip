@@ -35,6 +35,9 @@ constexpr int kMinLength = 13;
 constexpr int kRing = 1024;           // bytes of LDS input ring per wave
 constexpr int kAhead = 704;           // keep the ring filled this far past the batch front
 constexpr int kOut = 512;             // bytes of LDS output ring per wave
+#ifndef LZH_BRFREE
+#define LZH_BRFREE 1
+#endif
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -279,6 +282,8 @@ struct PSide {
     uint32_t m4, w, q0, q1, q2, q3, q4;       // words at p-4, p, p+4, .., p+20
 };
 
+// (a single-base read with ds_read2_b32 pairs for batches whose dwords do not wrap was
+// measured 1% slower: fewer VALU instructions are not what bounds this kernel)
 __device__ __forceinline__ PSide p_side_ring(const Ring& R, int p) {
     const int X = p - 4 + R.sh, A = X & ~3;
     const uint32_t s = (uint32_t)X & 3u;
@@ -321,8 +326,12 @@ struct MWin {
         const int X = (valid ? (int)c : 0) + in.sh;
         const int A = (X & ~3) - 4;
         sm = X & 3;
+#if LZH_BRFREE
+        {   // (idle lanes load the chunk's first bytes: in range, and their evaluation is masked)
+#else
         d0 = d1 = d2 = d3 = d4 = d5 = d6 = d7 = 0;
         if (valid) {
+#endif
             // d0 (bytes before the candidate) matters only when A >= 0: clamped, separate load
             // (a merged wide load starting at offset -4 would fail its range check as a whole)
             d0 = ld_b32(in.r, max(A, 0)); d1 = ld_b32(in.r, A + 4); d2 = ld_b32(in.r, A + 8); d3 = ld_b32(in.r, A + 12);
@@ -595,7 +604,8 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             const uint32_t h = hash_of<kSmall>(ps.w, b4);
             LZ_CLK(0);                                                 // lanes -> positions, P side, hash
             const uint32_t old = T.get(h);
-            if (valid) T.put(h, (uint32_t)p);
+            if (LZH_BRFREE && vmask == ~0ull) T.put(h, (uint32_t)p);   // (no exec-mask juggling)
+            else if (valid) T.put(h, (uint32_t)p);
             wave_lds_fence();
             const uint32_t back = T.get(h);
             const uint64_t losers = ballot(valid && back != (uint32_t)p);
@@ -807,7 +817,12 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     }
                     // table: the last inserted lane of each slot, or the slot's old value
                     const bool inI = (I >> lane) & 1ull;
-                    if (!losers) {
+                    if (LZH_BRFREE && vmask == ~0ull) {
+                        // every lane stores its slot's final value (all lanes of a slot agree):
+                        // the slot's last inserted lane, else its old value
+                        const uint64_t gi = grp & I;
+                        T.put(h, gi ? (uint32_t)(base + 63 - __builtin_clzll(gi)) : old);
+                    } else if (!losers) {
                         if (valid && !inI) T.put(h, old);
                     } else {
                         const uint64_t gi = grp & I;

@@ -12,6 +12,7 @@
 //   * lzbench_compress / lzbench_decompress chunk loops with the raw-store rule
 //     (lzbench.cpp:266-329), or ONE call per chunk list through a row's batched hook.
 // Added: -g# = number of GPUs a HIP row shards the chunk list over (its additional_param).
+#include <dirent.h>
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -19,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -113,6 +115,8 @@ struct row_t {
 };
 struct params_t {
     int show_speed = 1, compress_only = 0, verbose = 2, ngpus = 1;
+    int random_read = 0;        // -R: one random chunk-aligned block per file (lzbench.cpp:671-681)
+    uint64_t mem_limit = 0;     // -m: read files in parts of this many bytes (lzbench.cpp:652-656, :699-713)
     timetype_e timetype = FASTEST;
     textformat_e textformat = TEXT;
     size_t chunk_size = (1ull << 31) - (1ull << 31) / 6;
@@ -381,8 +385,11 @@ static void usage(params_t* P) {
     fprintf(stderr, " -iX,Y set min. number of compression and decompression iterations (default = %u, %u)\n", P->c_iters, P->d_iters);
     fprintf(stderr, " -j    join files in memory but compress them independently (for many small files)\n");
     fprintf(stderr, " -l    list of available compressors and aliases\n");
+    fprintf(stderr, " -R    read block/chunk size from random blocks (to estimate for large files)\n");
+    fprintf(stderr, " -m#   set memory limit to # MB (default = no limit)\n");
     fprintf(stderr, " -o#   output text format 1=Markdown, 2=text, 3=text+origSize, 4=CSV (default = %d)\n", P->textformat);
     fprintf(stderr, " -p#   print time for all iterations: 1=fastest 2=average 3=median (default = %d)\n", P->timetype);
+    fprintf(stderr, " -r    operate recursively on directories\n");
     fprintf(stderr, " -s#   use only compressors with compression speed over # MB (default = %u MB)\n", P->cspeed);
     fprintf(stderr, " -tX,Y set min. time in seconds for compression and decompression (default = %.0f, %.0f)\n",
             P->cmintime / 1000.0, P->dmintime / 1000.0);
@@ -399,6 +406,22 @@ static int read_file(const char* fn, std::vector<uint8_t>& out) {
     const size_t r = n ? fread(out.data(), 1, (size_t)n, f) : 0;
     fclose(f);
     return r == (size_t)n ? 0 : -1;
+}
+
+// inputs: files as given; directories expanded (sorted) when -r is set, else skipped
+static void expand_inputs(const char* path, bool recursive, std::vector<std::string>& out) {
+    struct stat st;
+    if (stat(path, &st) != 0) { out.push_back(path); return; }      // (reported when opened)
+    if (!S_ISDIR(st.st_mode)) { out.push_back(path); return; }
+    if (!recursive) { fprintf(stderr, "%s is a directory (use -r)\n", path); return; }
+    DIR* d = opendir(path);
+    if (!d) return;
+    std::vector<std::string> names;
+    while (struct dirent* e = readdir(d))
+        if (strcmp(e->d_name, ".") && strcmp(e->d_name, "..")) names.push_back(e->d_name);
+    closedir(d);
+    std::sort(names.begin(), names.end());
+    for (const std::string& n : names) expand_inputs((std::string(path) + "/" + n).c_str(), true, out);
 }
 
 static void bench_buffer(params_t* P, std::vector<size_t>& fs, const std::vector<uint8_t>& data, const char* list) {
@@ -426,7 +449,7 @@ int main(int argc, char** argv) {
     params_t* P = &params;
     const char* list = "hip";
     int sort_col = 0;
-    bool join = false;
+    bool join = false, recursive = false;
     int ngpu = 0;
     g_gpu = hipGetDeviceCount(&ngpu) == hipSuccess && ngpu > 0;
     load_sys_lz4();
@@ -450,6 +473,9 @@ int main(int argc, char** argv) {
             case 'g': P->ngpus = num ? (int)num : 1; break;
             case 'i': P->c_iters = num; { unsigned v = P->d_iters; if (second(v)) P->d_iters = v; } break;
             case 'j': join = true; break;
+            case 'm': P->mem_limit = (uint64_t)num << 18; if (P->textformat == TEXT) P->textformat = TEXT_FULL; break;
+            case 'r': recursive = true; break;
+            case 'R': P->random_read = 1; srand((unsigned)time(NULL)); break;
             case 'o': P->textformat = (textformat_e)num; if (P->textformat == CSV) P->verbose = 0; break;
             case 'p': P->timetype = (timetype_e)num; break;
             case 's': P->cspeed = num; break;
@@ -487,25 +513,58 @@ int main(int argc, char** argv) {
     LZB_PRINT(2, PROGNAME " 1.8-hip (lzbench chunk loop, MI355X codec rows; %d GPU%s visible)\n\n", ngpu, ngpu == 1 ? "" : "s");
     print_header(P);
 
+    std::vector<std::string> inputs;
+    for (int i = 1; i < argc; i++) expand_inputs(argv[i], recursive, inputs);
     if (join) {
         std::vector<uint8_t> all;
         std::vector<size_t> fs;
-        for (int i = 1; i < argc; i++) {
+        for (const std::string& fn : inputs) {
             std::vector<uint8_t> d;
-            if (read_file(argv[i], d)) { fprintf(stderr, "cannot read %s\n", argv[i]); continue; }
+            if (read_file(fn.c_str(), d)) { fprintf(stderr, "cannot read %s\n", fn.c_str()); continue; }
             fs.push_back(d.size());
             all.insert(all.end(), d.begin(), d.end());
         }
-        P->in_filename = fs.size() == 1 ? argv[1] : "(joined files)";
+        P->in_filename = fs.size() == 1 ? inputs[0].c_str() : "(joined files)";
         bench_buffer(P, fs, all, list);
     } else {
-        for (int i = 1; i < argc; i++) {
-            std::vector<uint8_t> d;
-            if (read_file(argv[i], d)) { fprintf(stderr, "cannot read %s\n", argv[i]); continue; }
-            std::vector<size_t> fs(1, d.size());
-            const char* base = strrchr(argv[i], '/');
-            P->in_filename = base ? base + 1 : argv[i];
-            bench_buffer(P, fs, d, list);
+        for (const std::string& fn : inputs) {
+            FILE* f = fopen(fn.c_str(), "rb");
+            if (!f) { perror(fn.c_str()); continue; }
+            const char* base = strrchr(fn.c_str(), '/');
+            const std::string name = base ? base + 1 : fn.c_str();
+            fseeko(f, 0, SEEK_END);
+            const uint64_t real = (uint64_t)ftello(f);
+            rewind(f);
+            uint64_t insize = (P->mem_limit && real > P->mem_limit) ? P->mem_limit : real;
+            if (P->random_read) {                 // lzbench.cpp:671-681
+                uint64_t pos = 0;
+                if (P->chunk_size < real) {
+                    pos = (uint64_t)(rand() % (int)(real / P->chunk_size)) * P->chunk_size;
+                    insize = P->chunk_size;
+                    fseeko(f, (off_t)pos, SEEK_SET);
+                } else {
+                    insize = real;
+                }
+                printf("Seeking to: %llu %llu %llu\n", (unsigned long long)pos, (unsigned long long)P->chunk_size,
+                       (unsigned long long)insize);
+            }
+            std::vector<uint8_t> d((size_t)insize);
+            d.resize(insize ? fread(d.data(), 1, (size_t)insize, f) : 0);
+            if (P->mem_limit && real > P->mem_limit) {     // parts (lzbench.cpp:699-713)
+                for (int part = 1; !d.empty(); part++) {
+                    const std::string pn = name + " part " + std::to_string(part);
+                    P->in_filename = pn.c_str();
+                    std::vector<size_t> fs(1, d.size());
+                    bench_buffer(P, fs, d, list);
+                    d.resize((size_t)insize);
+                    d.resize(fread(d.data(), 1, (size_t)insize, f));
+                }
+            } else {
+                std::vector<size_t> fs(1, d.size());
+                P->in_filename = name.c_str();
+                bench_buffer(P, fs, d, list);
+            }
+            fclose(f);
         }
     }
     if (sort_col > 0 && sort_col <= 5) {

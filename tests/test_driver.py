@@ -92,3 +92,53 @@ def test_gpu_rows_joined_multi_file(tmp_path):
     key = [k for k in r if k.startswith("hip_lz4")][0]
     exp = len(O.compress_chunks(a, "lz4", 65536)[0]) + len(O.compress_chunks(b, "lz4", 65536)[0])
     assert int(r[key][4]) == exp and "ERROR" not in out
+
+
+def _full_rows(out):
+    """(name, orig size, compr size, filename) of each row in the text+origSize format."""
+    res = []
+    for line in out.splitlines():
+        if "MB/s" in line:
+            p = line[23:].split()
+            res.append((line[:23].strip(), int(p[4]), int(p[5]), " ".join(p[7:])))
+    return res
+
+
+def test_mem_limit_reads_parts(tmp_path):
+    """-m#: the file is benchmarked in parts of # << 18 bytes, named "<file> part i", in the
+    text+origSize format (lzbench.cpp:652-656, :699-713, :856-858)."""
+    d = L.datagen("text", 600_000, seed=5)
+    p = tmp_path / "big.txt"
+    p.write_bytes(d.tobytes())
+    got = [r for r in _full_rows(run(["-elz4", "-b64", "-m1", "-t0,0", "-i1,1", str(p)])) if r[0].startswith("lz4 ")]
+    lim = 1 << 18
+    assert [r[3] for r in got] == ["big.txt part 1", "big.txt part 2", "big.txt part 3"]
+    for i, r in enumerate(got):
+        part = d[i * lim:(i + 1) * lim]
+        assert r[1] == len(part) and r[2] == len(O.compress_chunks(part, "lz4", 65536)[0])
+
+
+def test_random_read_one_block(tmp_path):
+    """-R: one random chunk-aligned block of the chunk size (lzbench.cpp:671-681)."""
+    d = L.datagen("json", 5 * 65536 + 99, seed=6)
+    p = tmp_path / "r.json"
+    p.write_bytes(d.tobytes())
+    out = run(["-elz4", "-b64", "-R", "-t0,0", "-i1,1", str(p)])
+    seek = [l for l in out.splitlines() if l.startswith("Seeking to:")]
+    pos, cs, n = map(int, seek[0].split()[2:5])
+    assert cs == 65536 and n == 65536 and pos % 65536 == 0 and pos + n <= len(d)
+    r = rows(out)
+    key = [k for k in r if k.startswith("lz4 ")][0]
+    assert int(r[key][4]) == len(O.compress_chunks(d[pos:pos + n], "lz4", 65536)[0])
+
+
+def test_recursive_directories(tmp_path):
+    """-r walks directories (sorted); without it a directory is skipped with a message."""
+    (tmp_path / "sub").mkdir()
+    (tmp_path / "a.txt").write_bytes(L.datagen("text", 70_000, seed=7).tobytes())
+    (tmp_path / "sub" / "b.json").write_bytes(L.datagen("json", 50_000, seed=8).tobytes())
+    out = run(["-elz4", "-b64", "-r", "-t0,0", "-i1,1", str(tmp_path)])
+    names = [l.split()[-1] for l in out.splitlines() if l.startswith("lz4 ")]
+    assert names == ["a.txt", "b.json"]
+    r = subprocess.run([EXE, "-elz4", "-t0,0", str(tmp_path)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "is a directory" in r.stderr
