@@ -41,7 +41,9 @@
 extern "C" {
 #endif
 
-enum { LZH_CODEC_LZ4 = 0, LZH_CODEC_SNAPPY = 1, LZH_CODEC_MEMCPY = 2 };
+/* LZH_CODEC_ZSTD: decode only (zstd 1.5.2 frames as lzbench's zstd rows write them, one frame
+ * per chunk: content size present, no dictionary, no checksum), lzh_decompress_async only */
+enum { LZH_CODEC_LZ4 = 0, LZH_CODEC_SNAPPY = 1, LZH_CODEC_MEMCPY = 2, LZH_CODEC_ZSTD = 3 };
 enum { LZH_OK = 0, LZH_EARG = -1, LZH_EHIP = -2, LZH_ESPACE = -3, LZH_ECORRUPT = -4 };
 
 /* ---- 1. lzbench rows (per-chunk ABI) ------------------------------------------------ */
@@ -83,7 +85,9 @@ int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t 
                        void* d_packed, size_t packed_cap, uint32_t* d_csizes, uint64_t* d_offsets,
                        void* d_temp, size_t temp_bytes, void* hip_stream);
 /* d_offsets may be NULL (then derived from d_csizes into d_temp).  d_status: nchunks i32,
- * decoded size per chunk or negative on malformed input. */
+ * decoded size per chunk or negative on malformed input (zstd: -1 corrupt, -2 unsupported
+ * frame feature).  A chunk whose compressed size equals its size is stored raw (all codecs).
+ * Replaces (zstd): lzbench_zstd_decompress, compressors.cpp:1767-1773 (ZSTD_decompressDCtx). */
 int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable, const uint32_t* d_csizes,
                          const uint64_t* d_offsets, size_t n, size_t chunk_size, void* d_out, int32_t* d_status,
                          void* d_temp, size_t temp_bytes, void* hip_stream);

@@ -23,7 +23,7 @@ import numpy as np
 __all__ = [
     "ExtensionMissing", "lib", "CODECS", "COMP_DESC", "CompressorDesc", "find_compressor",
     "compress_chunks", "decompress_chunks", "chunk_sizes_for", "datagen", "DeviceCodec",
-    "LZH_CODEC_LZ4", "LZH_CODEC_SNAPPY", "LZH_CODEC_MEMCPY", "PAD_SIZE", "get_compress_bound",
+    "LZH_CODEC_LZ4", "LZH_CODEC_SNAPPY", "LZH_CODEC_MEMCPY", "LZH_CODEC_ZSTD", "PAD_SIZE", "get_compress_bound",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -31,8 +31,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LZH_LIB") or os.path.join(_HERE, "liblzbench_hip.so")
 DATAGEN_PATH = os.path.join(_HERE, "libdatagen.so")
 
-LZH_CODEC_LZ4, LZH_CODEC_SNAPPY, LZH_CODEC_MEMCPY = 0, 1, 2
-CODECS = {"lz4": LZH_CODEC_LZ4, "lz4fast": LZH_CODEC_LZ4, "snappy": LZH_CODEC_SNAPPY, "memcpy": LZH_CODEC_MEMCPY}
+LZH_CODEC_LZ4, LZH_CODEC_SNAPPY, LZH_CODEC_MEMCPY, LZH_CODEC_ZSTD = 0, 1, 2, 3
+CODECS = {"lz4": LZH_CODEC_LZ4, "lz4fast": LZH_CODEC_LZ4, "snappy": LZH_CODEC_SNAPPY, "memcpy": LZH_CODEC_MEMCPY,
+          "zstd": LZH_CODEC_ZSTD}   # zstd: decode only (DeviceCodec.decompress)
 PAD_SIZE = 16 * 1024          # lzbench.h:14
 
 

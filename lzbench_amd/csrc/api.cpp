@@ -46,6 +46,8 @@ size_t lzh_num_chunks(size_t n, size_t chunk_size) {
 static size_t codec_bound(int codec, size_t part) {
     if (codec == LZH_CODEC_LZ4) return part + part / 255 + 16;     // LZ4_compressBound, lz4.h:171
     if (codec == LZH_CODEC_SNAPPY) return 32 + part + part / 6;    // MaxCompressedLength, snappy.cc:99-121
+    if (codec == LZH_CODEC_ZSTD)                                    // ZSTD_COMPRESSBOUND, zstd.h:~210
+        return part + (part >> 8) + (part < (128u << 10) ? ((128u << 10) - part) >> 11 : 0);
     return part;
 }
 
@@ -97,6 +99,7 @@ int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t 
     hipStream_t s = (hipStream_t)hip_stream;
     if (!chunk_size || !d_packed || !d_csizes || !d_offsets || (n && !d_in)) return LZH_EARG;
     if (in_readable < n) return LZH_EARG;
+    if (codec == LZH_CODEC_ZSTD) return LZH_EARG;                     // (decode only this round)
     const size_t k = lzh_num_chunks(n, chunk_size);
     if (codec == LZH_CODEC_MEMCPY) {
         if (packed_cap < n) return LZH_ESPACE;
@@ -134,7 +137,8 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
                          void* d_temp, size_t temp_bytes, void* hip_stream) {
     hipStream_t s = (hipStream_t)hip_stream;
     if (!chunk_size || !d_csizes || !d_status || (n && (!d_out || !d_packed))) return LZH_EARG;
-    if (codec < 0 || codec > 2) return LZH_EARG;
+    if (codec < 0 || codec > LZH_CODEC_ZSTD) return LZH_EARG;
+    if (codec == LZH_CODEC_ZSTD && chunk_size > (1u << 30)) return LZH_EARG;
     const size_t k = lzh_num_chunks(n, chunk_size);
     if (n == 0) return LZH_OK;
     const uint64_t* offs = d_offsets;
@@ -143,8 +147,12 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
         LZH_CHECK(lzh_launch_scan(d_csizes, k, (uint64_t*)d_temp, nullptr, s));
         offs = (const uint64_t*)d_temp;
     }
-    LZH_CHECK(lzh_launch_decompress(codec, (const uint8_t*)d_packed, packed_readable, offs, d_csizes, n, chunk_size,
-                                    (uint8_t*)d_out, d_status, (uint32_t)k, s));
+    if (codec == LZH_CODEC_ZSTD)
+        LZH_CHECK(lzh_launch_zstd_decompress((const uint8_t*)d_packed, packed_readable, offs, d_csizes, n, chunk_size,
+                                             (uint8_t*)d_out, d_status, (uint32_t)k, s));
+    else
+        LZH_CHECK(lzh_launch_decompress(codec, (const uint8_t*)d_packed, packed_readable, offs, d_csizes, n,
+                                        chunk_size, (uint8_t*)d_out, d_status, (uint32_t)k, s));
     return LZH_OK;
 }
 

@@ -544,6 +544,732 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
     if (lane == 0) status[chunk] = r;
 }
 
+// ---------------------------------------------------------------------------------------
+// zstd frames (RFC 8878), the decode side of lzbench's zstd rows (compressors.cpp:1767-1773:
+// ZSTD_decompressDCtx of one frame per chunk).  Reference decoder: zstd 1.5.2
+//   frame / blocks       zstd/lib/decompress/zstd_decompress.c (ZSTD_decompressFrame)
+//   literals, sequences  zstd/lib/decompress/zstd_decompress_block.c (ZSTD_decodeLiteralsBlock,
+//                        ZSTD_decodeSeqHeaders, ZSTD_buildFSETable, ZSTD_decodeSequence,
+//                        ZSTD_decompressSequences_body)
+//   Huffman              zstd/lib/decompress/huf_decompress.c (HUF_readDTableX1, 1X1 / 4X1 streams)
+//   FSE headers          zstd/lib/common/entropy_common.c (FSE_readNCount, HUF_readStats),
+//                        zstd/lib/common/fse_decompress.c (weights: two interleaved states)
+// One wave per frame.  Entropy decoding is inherently sequential, so it runs as wave-uniform
+// scalar code (every lane holds the same state; tables in LDS read at uniform addresses); the
+// backward bitstreams are read through 512-byte register windows (v_readlane, no memory round
+// trip per refill).  Literals are decoded into the tail of the chunk's own output region (the
+// frame content size is known), and the sequences are executed with the LZ4 decoder's group
+// emitter: up to 64 sequences per group, one output byte per lane per pass, through the LDS
+// output window.
+// Scope: frames as lzbench writes them (content size present, no dictionary, no checksum);
+// others return kErrUnsupported.  Valid frames decode to the reference's bytes; corrupt frames
+// are rejected without faulting (verdicts on corrupt input are not pinned to the reference's).
+namespace zstdd {
+
+using owin::kW;
+constexpr int kErrCorrupt = -1, kErrUnsupported = -2;
+#ifndef LZH_ZSTD_DEBUG
+#define LZH_ZSTD_DEBUG 0
+#endif
+// corrupt: -1, or (debug builds) -(10000 + source line) to locate the failing check
+#define ZC (LZH_ZSTD_DEBUG ? -(10000 + __LINE__) : kErrCorrupt)
+constexpr int kBlockMax = 128 * 1024;
+constexpr int kHufLogMax = 11;          // the reference encoder's maximum (HUF_TABLELOG_DEFAULT)
+
+// literal-length / match-length codes: baseline and extra bits (RFC 8878 3.1.1.3.2.1.1;
+// common/zstd_internal.h LL_bits / ML_bits) and the predefined distributions (3.1.1.3.2.2;
+// LL/ML/OF_defaultNorm)
+__constant__ uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10,   11,   12,   13,    14,    15,    16,   18,
+                                     20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+__constant__ uint8_t kLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  1,  1,
+                                    1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ uint32_t kMLBase[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14,  15,  16,  17,  18,   19,   20,
+                                     21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32,  33,  34,  35,  37,   39,   41,
+                                     43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+__constant__ uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                    0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ int8_t kLLNorm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                   2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+__constant__ int8_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1,  1,  1,  1,  1,  1,  1,  1,  1,  1,  1,
+                                   1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__constant__ int8_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+// per-wave LDS
+struct Lds {
+    uint8_t win[kW + 2 * LZH_WAVE];     // output window | start marks (groups::emit_group)
+    uint16_t huf[1 << kHufLogMax];      // Huffman decoding table: symbol | nbBits << 8
+    uint32_t ll[512], ml[512], of[256]; // sequence FSE tables: symbol | nbBits << 8 | base << 16
+    uint32_t wt[64];                    // FSE table of the Huffman weights (accuracy <= 6)
+    uint8_t weights[256];
+    int16_t norm[256];
+    uint16_t next[256];
+};
+
+__device__ __forceinline__ uint32_t lds_u32(const LDSA uint32_t* p) { return uni(*(volatile const LDSA uint32_t*)p); }
+__device__ __forceinline__ uint32_t lds_u16(const LDSA uint16_t* p) { return uni(*(volatile const LDSA uint16_t*)p); }
+__device__ __forceinline__ uint32_t lds_u8(const LDSA uint8_t* p) { return uni(*(volatile const LDSA uint8_t*)p); }
+__device__ __forceinline__ int hb32(uint32_t v) { return 31 - __builtin_clz(v); }   // v > 0
+
+// uniform little-endian reads from a forward register window (Win) over the frame
+__device__ __forceinline__ uint32_t fbyte(Win& w, int pos, int lane) { w.ensure(pos, lane); return uni(w.byte(pos)); }
+__device__ __forceinline__ uint32_t fword(Win& w, int pos, int lane) {   // bytes pos..pos+3
+    w.ensure(pos, lane);
+    const int x = pos + w.sh, d = (x - w.wb) >> 2;
+    const uint32_t a = d < 64 ? rdlane(w.w0, d) : rdlane(w.w1, d - 64);
+    const uint32_t b = d + 1 < 64 ? rdlane(w.w0, d + 1) : rdlane(w.w1, d + 1 - 64);
+    return uni(__builtin_amdgcn_alignbyte(b, a, (uint32_t)x & 3u));
+}
+
+// Backward bitstream (RFC 8878 4.1 / bitstream.h BIT_DStream): bits [0, B) of the stream are
+// unread, the next field is bits [B - n, B) (most significant first).  c holds stream bits
+// [ce - 64, ce) (ce a multiple of 8; zeros below bit 0); source bytes come through a 512-byte
+// register window that slides down the stream.
+struct BackBits {
+    rsrc_t r;
+    int sh;
+    int wb;              // descriptor offset of the window start (multiple of 4)
+    uint32_t w0, w1;     // window dwords [wb, wb + 256), [wb + 256, wb + 512)
+    int s0;              // descriptor offset of stream byte 0
+    int B, ce;
+    uint64_t c;
+    bool bad;
+
+    __device__ __forceinline__ uint32_t dw(int D) const {
+        const int d = (D - wb) >> 2;
+        return uni(d < 64 ? rdlane(w0, d) : rdlane(w1, d - 64));
+    }
+    __device__ __forceinline__ void cover(int D0, int D1, int lane) {   // dwords [D0, D1) (<= 16 B)
+        if (D0 >= wb && D1 <= wb + 512) return;
+        if (D0 >= wb - 256 && D1 <= wb + 256) {
+            w1 = w0;
+            wb -= 256;
+            w0 = ld_b32(r, wb + 4 * lane);
+            return;
+        }
+        wb = D1 - 512;
+        w0 = ld_b32(r, wb + 4 * lane);
+        w1 = ld_b32(r, wb + 256 + 4 * lane);
+    }
+    // the 8 stream bytes ending at byte e (e >= 8), little-endian
+    __device__ __forceinline__ uint64_t le64(int X, int lane) {
+        const int D = X & ~3;
+        cover(D, D + 12, lane);
+        const uint64_t lo = ((uint64_t)dw(D + 4) << 32) | dw(D);
+        const uint32_t hi = dw(D + 8);
+        const int s = 8 * (X & 3);
+        return s ? (lo >> s) | ((uint64_t)hi << (64 - s)) : lo;
+    }
+    __device__ __forceinline__ void refill(int lane) {
+        if (B < 0) { bad = true; B = 0; }
+        const int e = (B + 7) >> 3;
+        if (e >= 8) c = le64(s0 + e - 8, lane);
+        else c = e ? le64(s0, lane) << (8 * (8 - e)) : 0ull;
+        ce = 8 * e;
+    }
+    // stream = descriptor bytes [start, start + size) of (r, sh); false if the end mark is missing
+    __device__ __forceinline__ bool init(const Bytes& src, int start, int size, int lane) {
+        r = src.r; sh = src.sh; s0 = start + sh; bad = false;
+        wb = ((s0 + size + 3) & ~3) - 512;
+        w0 = ld_b32(r, wb + 4 * lane);
+        w1 = ld_b32(r, wb + 256 + 4 * lane);
+        if (size <= 0) return false;
+        const int X = s0 + size - 1;
+        const uint32_t last = (dw(X & ~3) >> (8 * (X & 3))) & 0xffu;
+        if (last == 0) return false;
+        B = 8 * (size - 1) + hb32(last);
+        refill(lane);
+        return true;
+    }
+    // make sure n more bits can be peeked (n <= 32)
+    __device__ __forceinline__ void need(int n, int lane) { if (ce - B + n > 64) refill(lane); }
+    __device__ __forceinline__ uint32_t peek(int n) const {   // 1 <= n <= 32, after need(n)
+        return (uint32_t)((c << (ce - B)) >> (64 - n));
+    }
+    __device__ __forceinline__ uint32_t read(int n, int lane) {
+        if (n == 0) return 0;
+        need(n, lane);
+        const uint32_t v = peek(n);
+        B -= n;
+        return v;
+    }
+};
+
+// FSE_readNCount (entropy_common.c:70-215) over the frame from byte pos: normalized counts
+// into L.norm[0..maxSym], returns the header size in bytes (<= 0: corrupt); *al = accuracy log
+__device__ int read_ncount(Win& fw, int pos, int end, int maxSym, int maxLog, LDSA Lds& L, int& al, int& nsym,
+                           int lane) {
+    for (int i = lane; i < 256; i += LZH_WAVE) L.norm[i] = 0;
+    int bit = 0;                                      // bits consumed from pos
+    auto peek32 = [&](void) -> uint32_t {
+        const int p = pos + (bit >> 3);
+        const uint64_t v = ((uint64_t)fword(fw, p + 4, lane) << 32) | fword(fw, p, lane);
+        return (uint32_t)(v >> (bit & 7));
+    };
+    uint32_t bs = peek32();
+    int nb = (int)(bs & 15u) + 5;
+    if (nb > maxLog) return ZC;
+    al = nb;
+    bit = 4;
+    int remaining = (1 << nb) + 1, threshold = 1 << nb;
+    nb++;
+    int sym = 0;
+    bool prev0 = false;
+    for (int guard = 0; guard < 512; guard++) {
+        if (prev0) {                                  // 2-bit repeat flags: 3 = three more zeros, go on
+            for (int g2 = 0; g2 < 256; g2++) {
+                const uint32_t r2 = peek32() & 3u;
+                bit += 2;
+                sym += (int)r2;
+                if (r2 != 3) break;
+            }
+            if (sym > maxSym) return ZC;
+        }
+        bs = peek32();
+        const int mx = (2 * threshold - 1) - remaining;
+        int count;
+        if ((int)(bs & (uint32_t)(threshold - 1)) < mx) {
+            count = (int)(bs & (uint32_t)(threshold - 1));
+            bit += nb - 1;
+        } else {
+            count = (int)(bs & (uint32_t)(2 * threshold - 1));
+            if (count >= threshold) count -= mx;
+            bit += nb;
+        }
+        count--;
+        remaining -= count < 0 ? -count : count;
+        if (sym > maxSym) return ZC;
+        if (lane == 0) L.norm[sym] = (int16_t)count;
+        sym++;
+        prev0 = count == 0;
+        if (remaining < threshold) {
+            if (remaining <= 1) break;
+            nb = hb32((uint32_t)remaining) + 1;
+            threshold = 1 << (nb - 1);
+        }
+        if (sym > maxSym) break;
+    }
+    wave_lds_fence();
+    if (remaining != 1 || bit > 8 * (end - pos)) return ZC;
+    nsym = sym;
+    return (bit + 7) >> 3;
+}
+
+// FSE_buildDTable (fse_decompress.c:72-160; ZSTD_buildFSETable for the sequence tables):
+// symbols spread over the table, then each cell's next-state base and bit count
+__device__ void build_fse(LDSA uint32_t* T, int al, int nsym, LDSA Lds& L, int lane) {
+    const int size = 1 << al, mask = size - 1;
+    int high = size - 1;
+    for (int s = 0; s < nsym; s++) {                  // low-probability symbols at the top
+        const int n = (int16_t)lds_u16((const LDSA uint16_t*)&L.norm[s]);
+        if (n == -1) {
+            if (lane == 0) T[high] = (uint32_t)s;
+            high--;
+        }
+        if (lane == 0) L.next[s] = (uint16_t)(n == -1 ? 1 : n);
+    }
+    wave_lds_fence();
+    const int step = (size >> 1) + (size >> 3) + 3;
+    int p = 0;
+    for (int s = 0; s < nsym; s++) {
+        const int n = (int16_t)lds_u16((const LDSA uint16_t*)&L.norm[s]);
+        for (int i = 0; i < n; i++) {
+            if (lane == 0) T[p] = (uint32_t)s;
+            p = (p + step) & mask;
+            while (p > high) p = (p + step) & mask;
+        }
+    }
+    wave_lds_fence();
+    for (int u = 0; u < size; u++) {
+        const uint32_t s = lds_u32(&T[u]) & 0xffu;
+        const uint32_t nx = lds_u16(&L.next[s]);
+        if (lane == 0) L.next[s] = (uint16_t)(nx + 1);
+        const int nb = al - hb32(nx);
+        const uint32_t base = (nx << nb) - (uint32_t)size;
+        if (lane == 0) T[u] = s | ((uint32_t)nb << 8) | (base << 16);
+        wave_lds_fence();
+    }
+}
+
+// sequence table for one of LL / OF / ML (ZSTD_buildSeqTable, zstd_decompress_block.c:~560):
+// mode 0 predefined, 1 RLE, 2 FSE-compressed, 3 repeat.  Returns bytes consumed, < 0 corrupt.
+__device__ int seq_table(Win& fw, int pos, int end, int mode, int which, LDSA uint32_t* T, int& al, bool& valid,
+                         LDSA Lds& L, int lane) {
+    const int maxSym = which == 0 ? 35 : (which == 1 ? 31 : 52);
+    const int maxLog = which == 1 ? 8 : 9;
+    if (mode == 0) {
+        const int n = which == 0 ? 36 : (which == 1 ? 29 : 53);
+        for (int s = lane; s < n; s += LZH_WAVE)
+            L.norm[s] = which == 0 ? kLLNorm[s] : (which == 1 ? kOFNorm[s] : kMLNorm[s]);
+        wave_lds_fence();
+        al = which == 1 ? 5 : 6;
+        build_fse(T, al, n, L, lane);
+        valid = true;
+        return 0;
+    }
+    if (mode == 1) {
+        if (pos >= end) return ZC;
+        const int s = (int)fbyte(fw, pos, lane);
+        if (s > maxSym) return ZC;
+        if (lane == 0) T[0] = (uint32_t)s;
+        wave_lds_fence();
+        al = 0;
+        valid = true;
+        return 1;
+    }
+    if (mode == 2) {
+        int nsym = 0;
+        const int h = read_ncount(fw, pos, end, maxSym, maxLog, L, al, nsym, lane);
+        if (h <= 0) return h < 0 ? h : ZC;
+        if (pos + h > end) return ZC;
+        build_fse(T, al, nsym, L, lane);
+        valid = true;
+        return h;
+    }
+    return valid ? 0 : -1;                             // repeat: the previous block's table
+}
+
+// Huffman tree description (HUF_readStats, entropy_common.c:271-334; HUF_readDTableX1,
+// huf_decompress.c:342-470) at pos.  Returns bytes consumed (< 0 corrupt), *tl = table log.
+__device__ int read_huf(Win& fw, const Bytes& src, int pos, int end, LDSA Lds& L, int& tl, int lane) {
+    if (pos >= end) return ZC;
+    const int hb = (int)fbyte(fw, pos, lane);
+    int n, used;
+    if (hb >= 128) {                                   // direct 4-bit weights
+        n = hb - 127;
+        used = 1 + (n + 1) / 2;
+        if (pos + used > end) return ZC;
+        for (int i = 0; i < n; i++) {
+            const uint32_t b = fbyte(fw, pos + 1 + i / 2, lane);
+            if (lane == 0) L.weights[i] = (uint8_t)((i & 1) ? (b & 15u) : (b >> 4));
+        }
+    } else {                                           // FSE-compressed weights, accuracy <= 6
+        used = 1 + hb;
+        if (pos + used > end || hb == 0) return ZC;
+        int al = 0, nsym = 0;
+        const int h = read_ncount(fw, pos + 1, pos + 1 + hb, 255, 6, L, al, nsym, lane);
+        if (h < 0) return h;
+        if (h == 0 || h >= hb) return ZC;
+        build_fse(L.wt, al, nsym, L, lane);
+        BackBits bb;
+        if (!bb.init(src, pos + 1 + h, hb - h, lane)) return ZC;
+        // two interleaved states (fse_decompress.c:199-250): after each symbol's state
+        // update, an exhausted stream ends with one more symbol from the other state
+        uint32_t st[2];
+        st[0] = bb.read(al, lane);
+        st[1] = bb.read(al, lane);
+        n = 0;
+        for (int k = 0;; k ^= 1) {
+            if (n > 253) return ZC;
+            const uint32_t e = lds_u32(&L.wt[st[k]]);
+            if (lane == 0) L.weights[n] = (uint8_t)(e & 0xffu);
+            n++;
+            const int nb = (int)((e >> 8) & 0xffu);
+            bb.need(nb, lane);
+            st[k] = (e >> 16) + (nb ? bb.peek(nb) : 0u);
+            bb.B -= nb;
+            if (bb.B < 0) {
+                const uint32_t e2 = lds_u32(&L.wt[st[k ^ 1]]);
+                if (lane == 0) L.weights[n] = (uint8_t)(e2 & 0xffu);
+                n++;
+                break;
+            }
+        }
+    }
+    wave_lds_fence();
+    // weights -> table log, the implied last weight (HUF_readStats: a clean power of 2 completes
+    // the total), at least two and an even number of weight-1 symbols
+    uint32_t total = 0;
+    int c1 = 0;
+    for (int i = 0; i < n; i++) {
+        const int w = (int)lds_u8(&L.weights[i]);
+        if (w > 12) return ZC;
+        c1 += w == 1;
+        total += (1u << w) >> 1;
+    }
+    if (total == 0) return ZC;
+    tl = hb32(total) + 1;
+    if (tl > 12) return ZC;
+    if (tl > kHufLogMax) return kErrUnsupported;
+    const uint32_t rest = (1u << tl) - total;
+    if (rest & (rest - 1)) return ZC;
+    const int lw = hb32(rest) + 1;
+    if (lane == 0) L.weights[n] = (uint8_t)lw;
+    c1 += lw == 1;
+    n++;
+    if (c1 < 2 || (c1 & 1)) return ZC;
+    wave_lds_fence();
+    // table (HUF_readDTableX1): weight 1 first, symbols in order within a weight, 2^(w-1) cells
+    // each; symbols of a weight found by ballot over the 4 x 64 weights held in registers
+    uint32_t wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) wv[j] = lane + 64 * j < n ? (uint32_t)L.weights[lane + 64 * j] : 0u;
+    int start = 0;
+    for (int w = 1; w <= tl; w++) {
+        const int len = 1 << (w - 1);
+        const uint32_t cell = (uint32_t)(tl + 1 - w) << 8;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            for (uint64_t m = ballot(wv[j] == (uint32_t)w); m; m &= m - 1) {
+                const uint32_t s = (uint32_t)(__builtin_ctzll(m) + 64 * j);
+                for (int i = lane; i < len; i += LZH_WAVE) L.huf[start + i] = (uint16_t)(cell | s);
+                start += len;
+            }
+        }
+    }
+    wave_lds_fence();
+    return used;
+}
+
+// literals of one Huffman stream set into out[dst .. dst + rs): 1 or 4 streams (1X1 / 4X1)
+__device__ int huf_streams(const Bytes& src, int pos, int csize, int nstreams, const Bytes& out, int dst, int rs,
+                            int tl, LDSA Lds& L, int lane) {
+    if (nstreams == 1) {
+        BackBits b;
+        if (!b.init(src, pos, csize, lane)) return ZC;
+        for (int i = 0; i < rs; i++) {
+            b.need(tl, lane);
+            const uint32_t e = lds_u16(&L.huf[b.peek(tl)]);
+            b.B -= (int)(e >> 8);
+            if (lane == 0) out.st8(dst + i, e & 0xffu);
+        }
+        return (b.B == 0 && !b.bad) ? 0 : ZC;
+    }
+    if (csize < 10) return ZC;
+    Win fw;
+    fw.bind(src);
+    fw.load(pos, lane);
+    const int z1 = (int)(fword(fw, pos, lane) & 0xffffu), z2 = (int)(fword(fw, pos + 2, lane) & 0xffffu),
+              z3 = (int)(fword(fw, pos + 4, lane) & 0xffffu);
+    const int z4 = csize - 6 - z1 - z2 - z3;
+    if (z4 < 1) return ZC;
+    const int seg = (rs + 3) / 4, last = rs - 3 * seg;
+    if (last < 0) return ZC;
+    BackBits b0, b1, b2, b3;
+    const int p1 = pos + 6;
+    if (!b0.init(src, p1, z1, lane) || !b1.init(src, p1 + z1, z2, lane) || !b2.init(src, p1 + z1 + z2, z3, lane) ||
+        !b3.init(src, p1 + z1 + z2 + z3, z4, lane))
+        return ZC;
+    for (int i = 0; i < seg; i++) {
+        b0.need(tl, lane); b1.need(tl, lane); b2.need(tl, lane);
+        const uint32_t e0 = lds_u16(&L.huf[b0.peek(tl)]);
+        const uint32_t e1 = lds_u16(&L.huf[b1.peek(tl)]);
+        const uint32_t e2 = lds_u16(&L.huf[b2.peek(tl)]);
+        b0.B -= (int)(e0 >> 8); b1.B -= (int)(e1 >> 8); b2.B -= (int)(e2 >> 8);
+        uint32_t e3 = 0;
+        if (i < last) {
+            b3.need(tl, lane);
+            e3 = lds_u16(&L.huf[b3.peek(tl)]);
+            b3.B -= (int)(e3 >> 8);
+        }
+        const uint32_t v = lane == 0 ? e0 : (lane == 1 ? e1 : (lane == 2 ? e2 : e3));
+        if (lane < 3 || (lane == 3 && i < last)) out.st8(dst + lane * seg + i, v & 0xffu);
+    }
+    return (b0.B == 0 && b1.B == 0 && b2.B == 0 && b3.B == 0 && !(b0.bad || b1.bad || b2.bad || b3.bad)) ? 0 : ZC;
+}
+
+struct FrameState {
+    int rep0, rep1, rep2;
+    int llA, ofA, mlA;                  // accuracy logs of the current tables
+    bool llV, ofV, mlV, hufV;           // tables valid for "repeat" / treeless modes
+    int hufTl;
+};
+
+// one compressed block [bs, be) of the frame; output continues at op (returns new op, < 0 error)
+__device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& lw, owin::Sink& O, LDSA Lds& L,
+                            FrameState& F, int bs, int be, int op, int fcs, int lane) {
+    // ---- literals section (ZSTD_decodeLiteralsBlock)
+    const uint32_t b0 = fbyte(fw, bs, lane);
+    const int ltype = (int)(b0 & 3u), sf = (int)((b0 >> 2) & 3u);
+    int rs, lpos, seqpos;
+    Bytes lsrc;                                       // where the literals are read from
+    if (ltype <= 1) {
+        int hsz;
+        if ((sf & 1) == 0) { hsz = 1; rs = (int)(b0 >> 3); }
+        else if (sf == 1) { hsz = 2; rs = (int)((b0 >> 4) + (fbyte(fw, bs + 1, lane) << 4)); }
+        else { hsz = 3; rs = (int)((b0 >> 4) + (fbyte(fw, bs + 1, lane) << 4) + (fbyte(fw, bs + 2, lane) << 12)); }
+        if (rs > kBlockMax) return ZC;
+        if (ltype == 0) {
+            if (bs + hsz + rs > be) return ZC;
+            lsrc = rin;
+            lpos = bs + hsz;
+            seqpos = bs + hsz + rs;
+        } else {
+            if (bs + hsz + 1 > be || rs > fcs - op) return ZC;
+            const uint32_t v = fbyte(fw, bs + hsz, lane);
+            lsrc = lout;
+            lpos = fcs - rs;
+            for (int i = lane; i < rs; i += LZH_WAVE) O.out.st8(lpos + i, v);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            seqpos = bs + hsz + 1;
+        }
+    } else {
+        const int hsz = sf <= 1 ? 3 : (sf == 2 ? 4 : 5);
+        const int bits = sf <= 1 ? 10 : (sf == 2 ? 14 : 18);
+        if (bs + hsz > be) return ZC;
+        uint64_t h = 0;
+        for (int i = 0; i < hsz; i++) h |= (uint64_t)fbyte(fw, bs + i, lane) << (8 * i);
+        rs = (int)((h >> 4) & ((1u << bits) - 1));
+        const int cs = (int)((h >> (4 + bits)) & ((1u << bits) - 1));
+        if (rs > kBlockMax || bs + hsz + cs > be || rs > fcs - op) return ZC;
+        int p = bs + hsz;
+        if (ltype == 2) {
+            int tl = 0;
+            const int u = read_huf(fw, rin, p, bs + hsz + cs, L, tl, lane);
+            if (u < 0) return u;
+            F.hufV = true;
+            F.hufTl = tl;
+            p += u;
+        } else if (!F.hufV) {
+            return ZC;
+        }
+        lsrc = lout;
+        lpos = fcs - rs;
+        const int hr = huf_streams(rin, p, bs + hsz + cs - p, sf == 0 ? 1 : 4, O.out, lpos, rs, F.hufTl, L, lane);
+        if (hr < 0) return hr;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // literal stores visible to the window loads
+        seqpos = bs + hsz + cs;
+    }
+    lw.bind(lsrc);
+    lw.load(lpos, lane);
+
+    // ---- sequences section header (ZSTD_decodeSeqHeaders)
+    if (seqpos >= be) return ZC;
+    int p = seqpos;
+    int nseq = (int)fbyte(fw, p++, lane);
+    if (nseq >= 128) {
+        if (nseq == 255) {
+            if (p + 2 > be) return ZC;
+            nseq = (int)(fbyte(fw, p, lane) + (fbyte(fw, p + 1, lane) << 8)) + 0x7F00;
+            p += 2;
+        } else {
+            if (p + 1 > be) return ZC;
+            nseq = ((nseq - 128) << 8) + (int)fbyte(fw, p++, lane);
+        }
+    }
+    int lp = 0;                                       // literals consumed
+    if (nseq > 0) {
+        if (p >= be) return ZC;
+        const uint32_t modes = fbyte(fw, p++, lane);
+        if (modes & 3u) return ZC;
+        int u = seq_table(fw, p, be, (int)(modes >> 6), 0, L.ll, F.llA, F.llV, L, lane);
+        if (u < 0) return ZC;
+        p += u;
+        u = seq_table(fw, p, be, (int)((modes >> 4) & 3u), 1, L.of, F.ofA, F.ofV, L, lane);
+        if (u < 0) return ZC;
+        p += u;
+        u = seq_table(fw, p, be, (int)((modes >> 2) & 3u), 2, L.ml, F.mlA, F.mlV, L, lane);
+        if (u < 0) return ZC;
+        p += u;
+        // ---- sequences (ZSTD_decodeSequence), executed a group at a time
+        BackBits sb;
+        if (!sb.init(rin, p, be - p, lane)) return ZC;
+        uint32_t sLL = sb.read(F.llA, lane), sOF = sb.read(F.ofA, lane), sML = sb.read(F.mlA, lane);
+        int k = 0, glit = 0, gout = 0;                // group: members, literal bytes, output bytes
+        uint32_t g_lit = 0, g_ml = 0, g_off = 0, g_ex = 0, g_lrel = 0;
+        bool pend_big = false;
+        int big_ll = 0, big_ml = 0, big_off = 0;
+        for (int i = 0; i < nseq; i++) {
+            const uint32_t eLL = lds_u32(&L.ll[sLL]), eOF = lds_u32(&L.of[sOF]), eML = lds_u32(&L.ml[sML]);
+            const int ofc = (int)(eOF & 0xffu), mlc = (int)(eML & 0xffu), llc = (int)(eLL & 0xffu);
+            int off;
+            const int ll0 = llc == 0;
+            if (ofc > 1) {
+                off = (int)((1u << ofc) - 3u + sb.read(ofc, lane));
+                F.rep2 = F.rep1; F.rep1 = F.rep0; F.rep0 = off;
+            } else {
+                const int idx = ofc + ll0 + (int)(ofc ? sb.read(1, lane) : 0u);   // 0..3
+                if (ofc == 0) {
+                    off = ll0 ? F.rep1 : F.rep0;
+                    if (ll0) { F.rep1 = F.rep0; F.rep0 = off; }
+                } else {
+                    int t = idx == 3 ? F.rep0 - 1 : (idx == 1 ? F.rep1 : F.rep2);
+                    t += t == 0;                      // (as the reference: offset 0 becomes 1)
+                    if (idx != 1) F.rep2 = F.rep1;
+                    F.rep1 = F.rep0;
+                    F.rep0 = off = t;
+                }
+            }
+            const int ml = (int)kMLBase[mlc] + (int)sb.read(kMLBits[mlc], lane);
+            const int ll = (int)kLLBase[llc] + (int)sb.read(kLLBits[llc], lane);
+            if (i + 1 < nseq) {                       // state updates: LL, ML, OF
+                sLL = (eLL >> 16) + sb.read((int)((eLL >> 8) & 0xffu), lane);
+                sML = (eML >> 16) + sb.read((int)((eML >> 8) & 0xffu), lane);
+                sOF = (eOF >> 16) + sb.read((int)((eOF >> 8) & 0xffu), lane);
+            } else {
+                // the reference also updates the states after the last sequence and then accepts
+                // an exhausted or overrun stream (ZSTD_decompressSequences_body: reload >= completed)
+                const int extra = (int)((eLL >> 8) & 0xffu) + (int)((eML >> 8) & 0xffu) + (int)((eOF >> 8) & 0xffu);
+                if (sb.B > extra) return ZC;
+                sb.B = 0;
+            }
+            if (sb.B < 0 || sb.bad) return ZC;
+            // validity (ZSTD_execSequence): literals available, offset within the output, room
+            const int o0 = op + gout;                 // output position of this sequence
+            if (ll > rs - lp - glit || off > o0 + ll || (int64_t)o0 + ll + ml > (int64_t)(fcs - (rs - lp - glit - ll)))
+                return ZC;
+            const bool big = ll > 255 || ml > 4095;
+            if (big || k == LZH_WAVE || glit + ll > 384) {
+                // emit the pending group
+                if (k > 0) {
+                    const int ip = lpos + lp;
+                    if (!lw.covers(ip, ip + glit + 16)) lw.load(ip, lane);
+                    const uint64_t keep = k == LZH_WAVE ? ~0ull : ((1ull << k) - 1ull);
+                    groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kW, ip, op, gout, keep, (int)g_ex,
+                                       g_lit | (g_ml << 16), g_lrel, (int)g_off, lane);
+                    op += gout;
+                    lp += glit;
+                    k = 0; glit = 0; gout = 0;
+                }
+                pend_big = big;
+                big_ll = ll; big_ml = ml; big_off = off;
+            }
+            if (pend_big) {                           // a long sequence on its own
+                O.literals(lw, lsrc, lpos + lp, op, big_ll, lane);
+                op += big_ll;
+                lp += big_ll;
+                O.match(op, big_off, big_ml, lane);
+                op += big_ml;
+                pend_big = false;
+                continue;
+            }
+            g_lit = lane == k ? (uint32_t)ll : g_lit;
+            g_ml = lane == k ? (uint32_t)ml : g_ml;
+            g_off = lane == k ? (uint32_t)off : g_off;
+            g_ex = lane == k ? (uint32_t)gout : g_ex;
+            g_lrel = lane == k ? (uint32_t)glit : g_lrel;
+            k++;
+            glit += ll;
+            gout += ll + ml;
+        }
+        if (k > 0) {
+            const int ip = lpos + lp;
+            if (!lw.covers(ip, ip + glit + 16)) lw.load(ip, lane);
+            const uint64_t keep = k == LZH_WAVE ? ~0ull : ((1ull << k) - 1ull);
+            groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kW, ip, op, gout, keep, (int)g_ex, g_lit | (g_ml << 16),
+                               g_lrel, (int)g_off, lane);
+            op += gout;
+            lp += glit;
+        }
+    } else if (p != be) {
+        return ZC;
+    }
+    // last literals
+    const int rem = rs - lp;
+    if (rem > 0) {
+        if (rem > fcs - op) return ZC;
+        O.literals(lw, lsrc, lpos + lp, op, rem, lane);
+        op += rem;
+    }
+    return op;
+}
+
+// one frame in rin[0, cs) -> out[0, cap): returns the decoded size or an error code
+// lout: the output region for reading decoded literals back (whole dwords: its range ends at
+// the dword holding the last byte, so no load that straddles the end reads back as zero)
+__device__ int decode_frame(const Bytes& rin, const Bytes& lout, int cs, owin::Sink& O, LDSA Lds& L, int cap,
+                            int lane) {
+    Win fw;
+    fw.bind(rin);
+    fw.load(0, lane);
+    if (cs < 9) return ZC;
+    const uint32_t magic = fword(fw, 0, lane);
+    if (magic != 0xFD2FB528u) return (magic & 0xFFFFFFF0u) == 0x184D2A50u ? kErrUnsupported : kErrCorrupt;
+    const uint32_t fhd = fbyte(fw, 4, lane);
+    const int fcsf = (int)(fhd >> 6), single = (int)((fhd >> 5) & 1u);
+    if (fhd & 8u) return ZC;                  // reserved bit
+    if (fhd & 4u) return kErrUnsupported;              // content checksum
+    int p = 5;
+    if (!single) {
+        const uint32_t wd = fbyte(fw, p++, lane);
+        if ((wd >> 3) + 10 > 27) return kErrUnsupported;   // window beyond the reference's default limit
+    }
+    const int dsz = (int)(fhd & 3u) == 3 ? 4 : (int)(fhd & 3u);
+    uint32_t dict = 0;
+    for (int i = 0; i < dsz; i++) dict |= fbyte(fw, p + i, lane) << (8 * i);
+    p += dsz;
+    if (dict) return kErrUnsupported;
+    const int fsz = fcsf == 0 ? (single ? 1 : 0) : (fcsf == 1 ? 2 : (fcsf == 2 ? 4 : 8));
+    if (fsz == 0) return kErrUnsupported;              // content size absent
+    uint64_t fcs = 0;
+    for (int i = 0; i < fsz; i++) fcs |= (uint64_t)fbyte(fw, p + i, lane) << (8 * i);
+    if (fsz == 2) fcs += 256;
+    p += fsz;
+    if (fcs > (uint64_t)cap) return ZC;
+    const int n = (int)fcs;
+    FrameState F{1, 4, 8, 0, 0, 0, false, false, false, false, 0};
+    Win lw;
+    lw.bind(rin);
+    lw.load(0, lane);
+    int op = 0;
+    for (int guard = 0; guard <= cs; guard++) {
+        if (p + 3 > cs) return ZC;
+        const uint32_t bh = fbyte(fw, p, lane) | (fbyte(fw, p + 1, lane) << 8) | (fbyte(fw, p + 2, lane) << 16);
+        p += 3;
+        const int last = (int)(bh & 1u), type = (int)((bh >> 1) & 3u), bsz = (int)(bh >> 3);
+        if (bsz > kBlockMax) return ZC;
+        if (type == 0) {
+            if (p + bsz > cs || bsz > n - op) return ZC;
+            O.literals(fw, rin, p, op, bsz, lane);
+            op += bsz;
+            p += bsz;
+        } else if (type == 1) {
+            if (p + 1 > cs || bsz > n - op) return ZC;
+            const uint32_t v = fbyte(fw, p, lane);
+            for (int base = 0; base < bsz; base += LZH_WAVE) {
+                if (base + lane < bsz) O.put(op + base + lane, v);
+                O.maybe_flush(op + min(base + LZH_WAVE, bsz), lane);
+            }
+            op += bsz;
+            p += 1;
+        } else if (type == 2) {
+            if (p + bsz > cs) return ZC;
+            const int r = decode_block(rin, lout, fw, lw, O, L, F, p, p + bsz, op, n, lane);
+            if (r < 0) return r;
+            op = r;
+            p += bsz;
+        } else {
+            return ZC;
+        }
+        if (last) break;
+    }
+    if (op != n || p != cs) return ZC;
+    return op;
+}
+
+}  // namespace zstdd
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                           const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
+                           int32_t* status, uint32_t chunk0) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_raw[(sizeof(zstdd::Lds) + 3) / 4];
+    LDSA zstdd::Lds& L = *(LDSA zstdd::Lds*)lds_raw;
+    const int lane = threadIdx.x;
+    const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
+    const uint64_t ooff = chunk * chunk_size;
+    if (ooff >= n_total) return;
+    const int part = (int)min(chunk_size, n_total - ooff);
+    const uint64_t ioff = offsets[chunk];
+    const int cs = (int)csizes[chunk];
+    // (+16: whole-dword reads of the frame's last bytes; bytes past the frame are never used)
+    const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+    Bytes rin, rout;
+    rin.init(packed + ioff, readable);
+    rout.init(out + ooff, (uint64_t)part);
+    int r;
+    if (cs == part) {                                  // stored raw by the chunk loop (lzbench.cpp:284-288)
+        copy_raw(rin, rout, part, lane);
+        r = part;
+    } else {
+        owin::Sink O{(LDSA uint8_t*)L.win, rout, 0, 0};
+        Bytes lout;
+        lout.init(out + ooff, (uint64_t)part + 3);
+        r = zstdd::decode_frame(rin, lout, cs, O, L, part, lane);
+        if (r > 0) O.flush(r, lane);
+    }
+    if (lane == 0) status[chunk] = r;
+}
+
 #include "launch.h"
 hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                  const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
@@ -551,5 +1277,14 @@ hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t pack
     if (nchunks == 0) return hipSuccess;
     hipLaunchKernelGGL(lzh_decompress_v2_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
                        offsets, csizes, n_total, chunk_size, out, status, 0u);
+    return hipGetLastError();
+}
+
+hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                                      const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
+                                      int32_t* status, uint32_t nchunks, hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(lzh_zstd_decompress_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets,
+                       csizes, n_total, chunk_size, out, status, 0u);
     return hipGetLastError();
 }

@@ -11,6 +11,8 @@
  *   lz4 row adapters   /root/reference/_lzbench/compressors.cpp:343-362
  *     (LZ4_compress_default / LZ4_compress_fast(level), LZ4_decompress_fast)
  *   snappy adapters    /root/reference/_lzbench/compressors.cpp:1282-1292
+ *   zstd adapters      /root/reference/_lzbench/compressors.cpp:1745-1778 (codec 2: ZSTD_getParams(level,
+ *                      part, 0), contentSizeFlag = 1, ZSTD_compress_advanced; ZSTD_decompressDCtx)
  */
 #include <cstdint>
 #include <cstring>
@@ -19,6 +21,8 @@
 #include <vector>
 #include "lz4.h"
 #include "snappy.h"
+#define ZSTD_STATIC_LINKING_ONLY   /* ZSTD_compress_advanced, as lzbench uses it */
+#include "zstd.h"
 
 #define REF_COMPRESS_BOUND(n) ((n) + (n) / 6 + 16 * 1024)   /* GET_COMPRESS_BOUND, lzbench.h:17 */
 
@@ -33,7 +37,32 @@ size_t ref_snappy_compress(const char* s, size_t n, char* d) { size_t out = 0; s
 int ref_snappy_uncompress(const char* s, size_t csize, char* d) { return snappy::RawUncompress(s, csize, d) ? 1 : 0; }
 size_t ref_snappy_max_compressed_length(size_t n) { return snappy::MaxCompressedLength(n); }
 
+// one compression / decompression context per thread, created once (lzbench_zstd_init)
+struct ZstdCtx {
+    ZSTD_CCtx* c = ZSTD_createCCtx();
+    ZSTD_DCtx* d = ZSTD_createDCtx();
+    ~ZstdCtx() { ZSTD_freeCCtx(c); ZSTD_freeDCtx(d); }
+};
+static ZstdCtx& zctx() { static thread_local ZstdCtx z; return z; }
+
+int64_t ref_zstd_compress(const char* in, size_t n, char* out, size_t cap, int level) {
+    ZSTD_parameters p = ZSTD_getParams(level, n, 0);
+    ZSTD_CCtx_setParameter(zctx().c, ZSTD_c_compressionLevel, level);
+    p.fParams.contentSizeFlag = 1;
+    const size_t r = ZSTD_compress_advanced(zctx().c, out, cap, in, n, NULL, 0, p);
+    return ZSTD_isError(r) ? -1 : (int64_t)r;
+}
+int64_t ref_zstd_decompress(const char* in, size_t csize, char* out, size_t cap) {
+    const size_t r = ZSTD_decompressDCtx(zctx().d, out, cap, in, csize);
+    return ZSTD_isError(r) ? -1 : (int64_t)r;
+}
+int ref_zstd_version(void) { return (int)ZSTD_versionNumber(); }
+
 static int64_t one_compress(int codec, int level, const char* in, size_t part, char* out, size_t outpart) {
+    if (codec == 2) {
+        const int64_t r = ref_zstd_compress(in, part, out, outpart, level < 1 ? 1 : level);
+        return r < 0 ? 0 : r;
+    }
     if (codec == 0) {
         if (level <= 1) return LZ4_compress_default(in, out, (int)part, (int)outpart);
         return LZ4_compress_fast(in, out, (int)part, (int)outpart, level);
@@ -44,6 +73,7 @@ static int64_t one_compress(int codec, int level, const char* in, size_t part, c
 }
 
 static int64_t one_decompress(int codec, const char* in, size_t csize, char* out, size_t osize) {
+    if (codec == 2) return ref_zstd_decompress(in, csize, out, osize);
     if (codec == 0) { LZ4_decompress_fast(in, out, (int)osize); return (int64_t)osize; }
     snappy::RawUncompress(in, csize, out);
     return (int64_t)osize;

@@ -73,11 +73,16 @@ def ref():
         L.ref_compress_chunks_mt.argtypes = [C.c_int, C.c_int, _P, _SZ, _SZ, _P, _P, C.c_int]
         L.ref_decompress_chunks_mt.restype = _I64
         L.ref_decompress_chunks_mt.argtypes = [C.c_int, _P, _P, _SZ, _SZ, _P, C.c_int]
+        L.ref_zstd_compress.restype = _I64
+        L.ref_zstd_compress.argtypes = [_P, _SZ, _P, _SZ, C.c_int]
+        L.ref_zstd_decompress.restype = _I64
+        L.ref_zstd_decompress.argtypes = [_P, _SZ, _P, _SZ]
+        L.ref_zstd_version.restype = C.c_int
         _ref = L
     return _ref
 
 
-CODEC_ID = {"lz4": 0, "lz4fast": 0, "snappy": 1}
+CODEC_ID = {"lz4": 0, "lz4fast": 0, "snappy": 1, "zstd": 2}   # zstd: reference build only
 
 
 def lz4_compress(data: np.ndarray, acc: int = 1) -> bytes:
@@ -101,8 +106,8 @@ def compress_chunks(data: np.ndarray, codec: str, chunk: int, level: int = 1, us
     out = np.zeros(n + n // 6 + 16384 + 64 * k + 64, np.uint8)
     cs = np.zeros(k, np.uint64)
     c = CODEC_ID[codec]
-    lvl = level if codec == "lz4fast" else (1 if codec == "lz4" else 0)
-    if use_ref:
+    lvl = level if codec in ("lz4fast", "zstd") else (1 if codec == "lz4" else 0)
+    if use_ref or codec == "zstd":
         L = ref()
         tot = (L.ref_compress_chunks_mt(c, lvl, data.ctypes.data, n, chunk, out.ctypes.data, cs.ctypes.data, threads)
                if threads else L.ref_compress_chunks(c, lvl, data.ctypes.data, n, chunk, out.ctypes.data, cs.ctypes.data))
@@ -118,7 +123,7 @@ def decompress_chunks(packed: np.ndarray, csizes: np.ndarray, n: int, codec: str
     c = CODEC_ID[codec]
     packed = np.ascontiguousarray(packed)
     cs = np.ascontiguousarray(csizes, dtype=np.uint64)
-    if use_ref:
+    if use_ref or codec == "zstd":
         L = ref()
         r = (L.ref_decompress_chunks_mt(c, packed.ctypes.data, cs.ctypes.data, n, chunk, out.ctypes.data, threads)
              if threads else L.ref_decompress_chunks(c, packed.ctypes.data, cs.ctypes.data, n, chunk, out.ctypes.data))

@@ -1,0 +1,123 @@
+"""GPU zstd decoder (LZH_CODEC_ZSTD, decode_hip.hip zstdd::) on frames written by the REFERENCE
+zstd 1.5.2 with lzbench's zstd-row parameters (compressors.cpp:1745-1773): the committed golden
+frames, fresh frames over corpora x chunk sizes x levels (raw, RLE and compressed blocks,
+predefined / RLE / FSE / repeat tables, 1- and 4-stream Huffman literals, multi-block frames),
+edge sizes, and corrupted frames (no fault; an accepted frame decodes as the reference does).
+Parity is exact: the decoded bytes must equal the original input.  Run with -m gpu."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import lzbench_amd as L
+from test_zstd_golden import arrays, cases, corpus
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    torch.cuda.set_device(0)
+    return torch
+
+
+def gpu_decode(torch, packed, cs, n, chunk):
+    dc = L.DeviceCodec("zstd", n, chunk)
+    d_packed = torch.zeros(len(packed) + 256, dtype=torch.uint8, device="cuda")
+    if len(packed):
+        d_packed[:len(packed)].copy_(torch.from_numpy(np.array(packed, dtype=np.uint8)))
+    d_cs = torch.from_numpy(np.asarray(cs).astype(np.int32)).cuda()
+    dc.decompress(packed=d_packed, csizes=d_cs)
+    torch.cuda.synchronize()
+    return dc.status[:dc.k].cpu().numpy(), dc.out[:n].cpu().numpy()
+
+
+def expected_sizes(n, chunk):
+    k = (n + chunk - 1) // chunk
+    return np.array([min(chunk, n - i * chunk) for i in range(k)])
+
+
+@pytest.mark.parametrize("case", cases(), ids=lambda c: c["name"])
+def test_golden_frames(torch_cuda, case):
+    A = arrays()
+    data = corpus(case)
+    st, out = gpu_decode(torch_cuda, A[case["name"] + "/packed"], A[case["name"] + "/csizes"], len(data), case["chunk"])
+    assert (st == expected_sizes(len(data), case["chunk"])).all(), st
+    assert (out == data).all()
+
+
+@pytest.mark.parametrize("level", [1, 2, 3, 5, 9, 19])
+@pytest.mark.parametrize("chunk", [65536, 131072, 524288])
+@pytest.mark.parametrize("kind", ["text", "json", "binary", "mixed"])
+def test_reference_frames(torch_cuda, kind, chunk, level):
+    if not O.have_ref():
+        pytest.skip("reference build (oracle/_ref) not present")
+    if level >= 9 and chunk != 131072:
+        pytest.skip("slow CPU compression; one chunk size is enough")
+    data = L.datagen(kind, 3 << 20 if level < 9 else 1 << 20, 23 + level)
+    packed, cs = O.compress_chunks(data, "zstd", chunk, level)
+    st, out = gpu_decode(torch_cuda, packed, cs, len(data), chunk)
+    assert (st == expected_sizes(len(data), chunk)).all(), np.unique(st)
+    assert (out == data).all()
+
+
+@pytest.mark.parametrize("n", [1, 5, 13, 255, 4096 + 3, 131072 - 1, 131072 + 1, 3 * 131072 + 77])
+def test_edge_sizes(torch_cuda, n):
+    if not O.have_ref():
+        pytest.skip("reference build (oracle/_ref) not present")
+    data = L.datagen("text", n, 7)
+    packed, cs = O.compress_chunks(data, "zstd", 131072, 1)
+    st, out = gpu_decode(torch_cuda, packed, cs, n, 131072)
+    assert (st == expected_sizes(n, 131072)).all() and (out == data).all()
+
+
+def _corrupt(rng, s: bytes) -> bytes:
+    b = bytearray(s)
+    kind = int(rng.integers(0, 4))
+    if kind == 0:
+        for _ in range(int(rng.integers(1, 4))):
+            b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+    elif kind == 1:
+        i = int(rng.integers(0, len(b)))
+        b[i] ^= 1 << int(rng.integers(0, 8))
+    elif kind == 2:
+        b = b[: int(rng.integers(1, len(b)))]
+    else:
+        b += bytes(rng.integers(0, 256, int(rng.integers(1, 64))).astype(np.uint8))
+    return bytes(b)
+
+
+@pytest.mark.parametrize("corpus_kind", ["text", "json"])
+def test_corrupt_frames(torch_cuda, corpus_kind):
+    """1024 corrupted frames: the decoder never faults; a frame it accepts is one the reference
+    accepts, with the same bytes (it may reject more: verdict parity is not claimed for zstd)."""
+    if not O.have_ref():
+        pytest.skip("reference build (oracle/_ref) not present")
+    torch = torch_cuda
+    chunk = 32768
+    rng = np.random.default_rng(5 + len(corpus_kind))
+    data = L.datagen(corpus_kind, 8 * chunk, 31)
+    packed, cs = O.compress_chunks(data, "zstd", chunk, 1)
+    offs = np.concatenate([[0], np.cumsum(cs)]).astype(np.int64)
+    valid = [packed[offs[i]:offs[i + 1]].tobytes() for i in range(len(cs))]
+    streams = []
+    while len(streams) < 1024:
+        s = _corrupt(rng, valid[int(rng.integers(0, len(valid)))])
+        if 0 < len(s) != chunk:
+            streams.append(s)
+    blob = np.frombuffer(b"".join(streams), np.uint8)
+    st, out = gpu_decode(torch, blob, [len(s) for s in streams], len(streams) * chunk, chunk)
+    R = O.ref()
+    accepted = 0
+    for i, s in enumerate(streams):
+        if st[i] < 0:
+            continue
+        accepted += 1
+        src = np.frombuffer(s, np.uint8).copy()
+        dst = np.zeros(chunk + 64, np.uint8)
+        r = R.ref_zstd_decompress(src.ctypes.data, len(s), dst.ctypes.data, chunk)
+        assert r == st[i], f"stream {i}: gpu accepted {st[i]} bytes, reference {r}"
+        assert (out[i * chunk: i * chunk + r] == dst[:r]).all(), f"stream {i}: bytes differ"
+    assert accepted > 0
