@@ -573,6 +573,12 @@ constexpr int kErrCorrupt = -1, kErrUnsupported = -2;
 #endif
 // corrupt: -1, or (debug builds) -(10000 + source line) to locate the failing check
 #define ZC (LZH_ZSTD_DEBUG ? -(10000 + __LINE__) : kErrCorrupt)
+// phase clocks (debug builds with -DLZH_ZSTD_STATS=1; the launcher prints them)
+#ifndef LZH_ZSTD_STATS
+#define LZH_ZSTD_STATS 0
+#endif
+constexpr int kZClk = 8;
+#define ZCLK(F, i) do { if (LZH_ZSTD_STATS) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); (F).clk[i] += t_ - (F).clk_last; (F).clk_last = t_; } } while (0)
 constexpr int kBlockMax = 128 * 1024;
 constexpr int kHufLogMax = 11;          // the reference encoder's maximum (HUF_TABLELOG_DEFAULT)
 
@@ -594,12 +600,17 @@ __constant__ int8_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 
                                    1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
 __constant__ int8_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
+struct Cell { uint32_t x, y; };      // (an FSE decoding-table cell)
+
 // per-wave LDS
 struct Lds {
     uint8_t win[kW + 2 * LZH_WAVE];     // output window | start marks (groups::emit_group)
     uint16_t huf[1 << kHufLogMax];      // Huffman decoding table: symbol | nbBits << 8
-    uint32_t ll[512], ml[512], of[256]; // sequence FSE tables: symbol | nbBits << 8 | base << 16
-    uint32_t wt[64];                    // FSE table of the Huffman weights (accuracy <= 6)
+    // FSE decoding tables, one (x, y) pair per state: y = next-state base | nbBits << 16 |
+    // extra bits << 24; x = the symbol, or for LL/ML the baseline value and for OF the code
+    // (ZSTD_seqSymbol's fields, so a sequence needs no other table)
+    Cell ll[512], ml[512], of[256];
+    Cell wt[64];                       // FSE table of the Huffman weights (accuracy <= 6)
     uint8_t weights[256];
     int16_t norm[256];
     uint16_t next[256];
@@ -608,6 +619,10 @@ struct Lds {
 __device__ __forceinline__ uint32_t lds_u32(const LDSA uint32_t* p) { return uni(*(volatile const LDSA uint32_t*)p); }
 __device__ __forceinline__ uint32_t lds_u16(const LDSA uint16_t* p) { return uni(*(volatile const LDSA uint16_t*)p); }
 __device__ __forceinline__ uint32_t lds_u8(const LDSA uint8_t* p) { return uni(*(volatile const LDSA uint8_t*)p); }
+__device__ __forceinline__ Cell lds_cell(const LDSA Cell* p) {
+    const uint64_t v = *(volatile const LDSA uint64_t*)p;
+    return Cell{uni((uint32_t)v), uni((uint32_t)(v >> 32))};
+}
 __device__ __forceinline__ int hb32(uint32_t v) { return 31 - __builtin_clz(v); }   // v > 0
 
 // uniform little-endian reads from a forward register window (Win) over the frame
@@ -620,25 +635,23 @@ __device__ __forceinline__ uint32_t fword(Win& w, int pos, int lane) {   // byte
     return uni(__builtin_amdgcn_alignbyte(b, a, (uint32_t)x & 3u));
 }
 
-// Backward bitstream (RFC 8878 4.1 / bitstream.h BIT_DStream): bits [0, B) of the stream are
-// unread, the next field is bits [B - n, B) (most significant first).  c holds stream bits
-// [ce - 64, ce) (ce a multiple of 8; zeros below bit 0); source bytes come through a 512-byte
-// register window that slides down the stream.
+// Backward bitstream (RFC 8878 4.1 / bitstream.h BIT_DStream), wave-uniform.  Positions are
+// bit indices in the descriptor's byte space: the stream is bits [lo, P) still unread, the next
+// n-bit field is bits [P - n, P) (most significant first).  c holds the 64 bits from the
+// dword-aligned bit D8 (P - D8 in [32, 63] after a reload, so any field of <= 32 bits is in
+// c); source dwords come from a 512-byte register window (v_readlane) that slides down.
 struct BackBits {
     rsrc_t r;
-    int sh;
     int wb;              // descriptor offset of the window start (multiple of 4)
     uint32_t w0, w1;     // window dwords [wb, wb + 256), [wb + 256, wb + 512)
-    int s0;              // descriptor offset of stream byte 0
-    int B, ce;
+    int lo, P, D8;
     uint64_t c;
-    bool bad;
 
     __device__ __forceinline__ uint32_t dw(int D) const {
         const int d = (D - wb) >> 2;
-        return uni(d < 64 ? rdlane(w0, d) : rdlane(w1, d - 64));
+        return rdlane(d < 64 ? w0 : w1, d & 63);
     }
-    __device__ __forceinline__ void cover(int D0, int D1, int lane) {   // dwords [D0, D1) (<= 16 B)
+    __device__ __forceinline__ void cover(int D0, int D1, int lane) {   // bytes [D0, D1), D1 - D0 <= 256
         if (D0 >= wb && D1 <= wb + 512) return;
         if (D0 >= wb - 256 && D1 <= wb + 256) {
             w1 = w0;
@@ -650,53 +663,51 @@ struct BackBits {
         w0 = ld_b32(r, wb + 4 * lane);
         w1 = ld_b32(r, wb + 256 + 4 * lane);
     }
-    // the 8 stream bytes ending at byte e (e >= 8), little-endian
-    __device__ __forceinline__ uint64_t le64(int X, int lane) {
-        const int D = X & ~3;
-        cover(D, D + 12, lane);
-        const uint64_t lo = ((uint64_t)dw(D + 4) << 32) | dw(D);
-        const uint32_t hi = dw(D + 8);
-        const int s = 8 * (X & 3);
-        return s ? (lo >> s) | ((uint64_t)hi << (64 - s)) : lo;
+    __device__ __forceinline__ void reload(int lane) {
+        D8 = ((P - 32) >> 5) << 5;
+        const int D = D8 >> 3;
+        cover(D, D + 8, lane);
+        c = ((uint64_t)dw(D + 4) << 32) | dw(D);
     }
-    __device__ __forceinline__ void refill(int lane) {
-        if (B < 0) { bad = true; B = 0; }
-        const int e = (B + 7) >> 3;
-        if (e >= 8) c = le64(s0 + e - 8, lane);
-        else c = e ? le64(s0, lane) << (8 * (8 - e)) : 0ull;
-        ce = 8 * e;
-    }
-    // stream = descriptor bytes [start, start + size) of (r, sh); false if the end mark is missing
+    // stream = descriptor bytes [start, start + size) (start including the descriptor shift);
+    // false if empty or the end mark is missing
     __device__ __forceinline__ bool init(const Bytes& src, int start, int size, int lane) {
-        r = src.r; sh = src.sh; s0 = start + sh; bad = false;
+        r = src.r;
+        const int s0 = start + src.sh;
         wb = ((s0 + size + 3) & ~3) - 512;
         w0 = ld_b32(r, wb + 4 * lane);
         w1 = ld_b32(r, wb + 256 + 4 * lane);
+        lo = 8 * s0;
         if (size <= 0) return false;
         const int X = s0 + size - 1;
         const uint32_t last = (dw(X & ~3) >> (8 * (X & 3))) & 0xffu;
         if (last == 0) return false;
-        B = 8 * (size - 1) + hb32(last);
-        refill(lane);
+        P = 8 * X + hb32(last);
+        reload(lane);
         return true;
     }
-    // make sure n more bits can be peeked (n <= 32)
-    __device__ __forceinline__ void need(int n, int lane) { if (ce - B + n > 64) refill(lane); }
-    __device__ __forceinline__ uint32_t peek(int n) const {   // 1 <= n <= 32, after need(n)
-        return (uint32_t)((c << (ce - B)) >> (64 - n));
-    }
-    __device__ __forceinline__ uint32_t read(int n, int lane) {
-        if (n == 0) return 0;
-        need(n, lane);
-        const uint32_t v = peek(n);
-        B -= n;
+    __device__ __forceinline__ int left() const { return P - lo; }
+    // next n bits (0 <= n <= 32), consumed; bits below the stream start read as garbage
+    // (callers reject a stream that overruns)
+    __device__ __forceinline__ uint32_t get(int n, int lane) {
+        if (P - n < D8) reload(lane);
+        const uint32_t v = (uint32_t)((c >> (P - n - D8)) & ((1ull << n) - 1ull));
+        P -= n;
         return v;
     }
+    // next n bits (1 <= n <= 32) without consuming them, zero-padded below the stream start
+    __device__ __forceinline__ uint32_t peek(int n, int lane) {
+        if (P - n < D8) reload(lane);
+        uint32_t v = (uint32_t)((c >> (P - n - D8)) & ((1ull << n) - 1ull));
+        if (P - n < lo) v &= (uint32_t)(~0ull << (lo - (P - n)));
+        return v;
+    }
+    __device__ __forceinline__ void skip(int n) { P -= n; }
 };
 
 // FSE_readNCount (entropy_common.c:70-215) over the frame from byte pos: normalized counts
 // into L.norm[0..maxSym], returns the header size in bytes (<= 0: corrupt); *al = accuracy log
-__device__ int read_ncount(Win& fw, int pos, int end, int maxSym, int maxLog, LDSA Lds& L, int& al, int& nsym,
+__device__ __forceinline__ int read_ncount(Win& fw, int pos, int end, int maxSym, int maxLog, LDSA Lds& L, int& al, int& nsym,
                            int lane) {
     for (int i = lane; i < 256; i += LZH_WAVE) L.norm[i] = 0;
     int bit = 0;                                      // bits consumed from pos
@@ -755,14 +766,15 @@ __device__ int read_ncount(Win& fw, int pos, int end, int maxSym, int maxLog, LD
 }
 
 // FSE_buildDTable (fse_decompress.c:72-160; ZSTD_buildFSETable for the sequence tables):
-// symbols spread over the table, then each cell's next-state base and bit count
-__device__ void build_fse(LDSA uint32_t* T, int al, int nsym, LDSA Lds& L, int lane) {
+// symbols spread over the table, then each cell's next-state base and bit count.  Cells are
+// (symbol, next-state base | nbBits << 16).
+__device__ __forceinline__ void build_fse(LDSA Cell* T, int al, int nsym, LDSA Lds& L, int lane) {
     const int size = 1 << al, mask = size - 1;
     int high = size - 1;
     for (int s = 0; s < nsym; s++) {                  // low-probability symbols at the top
         const int n = (int16_t)lds_u16((const LDSA uint16_t*)&L.norm[s]);
         if (n == -1) {
-            if (lane == 0) T[high] = (uint32_t)s;
+            if (lane == 0) T[high].x = (uint32_t)s;
             high--;
         }
         if (lane == 0) L.next[s] = (uint16_t)(n == -1 ? 1 : n);
@@ -773,26 +785,40 @@ __device__ void build_fse(LDSA uint32_t* T, int al, int nsym, LDSA Lds& L, int l
     for (int s = 0; s < nsym; s++) {
         const int n = (int16_t)lds_u16((const LDSA uint16_t*)&L.norm[s]);
         for (int i = 0; i < n; i++) {
-            if (lane == 0) T[p] = (uint32_t)s;
+            if (lane == 0) T[p].x = (uint32_t)s;
             p = (p + step) & mask;
             while (p > high) p = (p + step) & mask;
         }
     }
     wave_lds_fence();
     for (int u = 0; u < size; u++) {
-        const uint32_t s = lds_u32(&T[u]) & 0xffu;
+        const uint32_t s = uni(((volatile const LDSA uint32_t*)T)[2 * u]);
         const uint32_t nx = lds_u16(&L.next[s]);
         if (lane == 0) L.next[s] = (uint16_t)(nx + 1);
         const int nb = al - hb32(nx);
         const uint32_t base = (nx << nb) - (uint32_t)size;
-        if (lane == 0) T[u] = s | ((uint32_t)nb << 8) | (base << 16);
+        if (lane == 0) T[u].y = base | ((uint32_t)nb << 16);
         wave_lds_fence();
     }
 }
 
+// sequence-table cells: symbol -> baseline value and extra-bit count (RFC 8878 3.1.1.3.2.1.1)
+__device__ __forceinline__ void seq_cells(LDSA Cell* T, int size, int which, int lane) {
+    for (int u = lane; u < size; u += LZH_WAVE) {
+        const uint32_t s = T[u].x, y = T[u].y & 0xffffffu;
+        uint32_t x, add;
+        if (which == 0) { x = kLLBase[s]; add = kLLBits[s]; }
+        else if (which == 2) { x = kMLBase[s]; add = kMLBits[s]; }
+        else { x = s; add = s; }
+        T[u].x = x;
+        T[u].y = y | (add << 24);
+    }
+    wave_lds_fence();
+}
+
 // sequence table for one of LL / OF / ML (ZSTD_buildSeqTable, zstd_decompress_block.c:~560):
 // mode 0 predefined, 1 RLE, 2 FSE-compressed, 3 repeat.  Returns bytes consumed, < 0 corrupt.
-__device__ int seq_table(Win& fw, int pos, int end, int mode, int which, LDSA uint32_t* T, int& al, bool& valid,
+__device__ __forceinline__ int seq_table(Win& fw, int pos, int end, int mode, int which, LDSA Cell* T, int& al, bool& valid,
                          LDSA Lds& L, int lane) {
     const int maxSym = which == 0 ? 35 : (which == 1 ? 31 : 52);
     const int maxLog = which == 1 ? 8 : 9;
@@ -803,6 +829,7 @@ __device__ int seq_table(Win& fw, int pos, int end, int mode, int which, LDSA ui
         wave_lds_fence();
         al = which == 1 ? 5 : 6;
         build_fse(T, al, n, L, lane);
+        seq_cells(T, 1 << al, which, lane);
         valid = true;
         return 0;
     }
@@ -810,8 +837,9 @@ __device__ int seq_table(Win& fw, int pos, int end, int mode, int which, LDSA ui
         if (pos >= end) return ZC;
         const int s = (int)fbyte(fw, pos, lane);
         if (s > maxSym) return ZC;
-        if (lane == 0) T[0] = (uint32_t)s;
+        if (lane == 0) { T[0].x = (uint32_t)s; T[0].y = 0u; }
         wave_lds_fence();
+        seq_cells(T, 1, which, lane);
         al = 0;
         valid = true;
         return 1;
@@ -822,6 +850,7 @@ __device__ int seq_table(Win& fw, int pos, int end, int mode, int which, LDSA ui
         if (h <= 0) return h < 0 ? h : ZC;
         if (pos + h > end) return ZC;
         build_fse(T, al, nsym, L, lane);
+        seq_cells(T, 1 << al, which, lane);
         valid = true;
         return h;
     }
@@ -830,7 +859,7 @@ __device__ int seq_table(Win& fw, int pos, int end, int mode, int which, LDSA ui
 
 // Huffman tree description (HUF_readStats, entropy_common.c:271-334; HUF_readDTableX1,
 // huf_decompress.c:342-470) at pos.  Returns bytes consumed (< 0 corrupt), *tl = table log.
-__device__ int read_huf(Win& fw, const Bytes& src, int pos, int end, LDSA Lds& L, int& tl, int lane) {
+__device__ __forceinline__ int read_huf(Win& fw, const Bytes& src, int pos, int end, LDSA Lds& L, int& tl, int lane) {
     if (pos >= end) return ZC;
     const int hb = (int)fbyte(fw, pos, lane);
     int n, used;
@@ -854,22 +883,18 @@ __device__ int read_huf(Win& fw, const Bytes& src, int pos, int end, LDSA Lds& L
         if (!bb.init(src, pos + 1 + h, hb - h, lane)) return ZC;
         // two interleaved states (fse_decompress.c:199-250): after each symbol's state
         // update, an exhausted stream ends with one more symbol from the other state
-        uint32_t st[2];
-        st[0] = bb.read(al, lane);
-        st[1] = bb.read(al, lane);
+        uint32_t s1 = bb.get(al, lane), s2 = bb.get(al, lane);
         n = 0;
         for (int k = 0;; k ^= 1) {
             if (n > 253) return ZC;
-            const uint32_t e = lds_u32(&L.wt[st[k]]);
-            if (lane == 0) L.weights[n] = (uint8_t)(e & 0xffu);
+            const Cell e = lds_cell(&L.wt[k ? s2 : s1]);
+            if (lane == 0) L.weights[n] = (uint8_t)e.x;
             n++;
-            const int nb = (int)((e >> 8) & 0xffu);
-            bb.need(nb, lane);
-            st[k] = (e >> 16) + (nb ? bb.peek(nb) : 0u);
-            bb.B -= nb;
-            if (bb.B < 0) {
-                const uint32_t e2 = lds_u32(&L.wt[st[k ^ 1]]);
-                if (lane == 0) L.weights[n] = (uint8_t)(e2 & 0xffu);
+            const uint32_t ns = (e.y & 0xffffu) + bb.get((int)((e.y >> 16) & 0xffu), lane);
+            if (k) s2 = ns; else s1 = ns;
+            if (bb.left() < 0) {
+                const Cell e2 = lds_cell(&L.wt[k ? s1 : s2]);
+                if (lane == 0) L.weights[n] = (uint8_t)e2.x;
                 n++;
                 break;
             }
@@ -921,18 +946,17 @@ __device__ int read_huf(Win& fw, const Bytes& src, int pos, int end, LDSA Lds& L
 }
 
 // literals of one Huffman stream set into out[dst .. dst + rs): 1 or 4 streams (1X1 / 4X1)
-__device__ int huf_streams(const Bytes& src, int pos, int csize, int nstreams, const Bytes& out, int dst, int rs,
+__device__ __forceinline__ int huf_streams(const Bytes& src, int pos, int csize, int nstreams, const Bytes& out, int dst, int rs,
                             int tl, LDSA Lds& L, int lane) {
     if (nstreams == 1) {
         BackBits b;
         if (!b.init(src, pos, csize, lane)) return ZC;
         for (int i = 0; i < rs; i++) {
-            b.need(tl, lane);
-            const uint32_t e = lds_u16(&L.huf[b.peek(tl)]);
-            b.B -= (int)(e >> 8);
+            const uint32_t e = lds_u16(&L.huf[b.peek(tl, lane)]);
+            b.skip((int)(e >> 8));
             if (lane == 0) out.st8(dst + i, e & 0xffu);
         }
-        return (b.B == 0 && !b.bad) ? 0 : ZC;
+        return b.left() == 0 ? 0 : ZC;
     }
     if (csize < 10) return ZC;
     Win fw;
@@ -950,21 +974,19 @@ __device__ int huf_streams(const Bytes& src, int pos, int csize, int nstreams, c
         !b3.init(src, p1 + z1 + z2 + z3, z4, lane))
         return ZC;
     for (int i = 0; i < seg; i++) {
-        b0.need(tl, lane); b1.need(tl, lane); b2.need(tl, lane);
-        const uint32_t e0 = lds_u16(&L.huf[b0.peek(tl)]);
-        const uint32_t e1 = lds_u16(&L.huf[b1.peek(tl)]);
-        const uint32_t e2 = lds_u16(&L.huf[b2.peek(tl)]);
-        b0.B -= (int)(e0 >> 8); b1.B -= (int)(e1 >> 8); b2.B -= (int)(e2 >> 8);
+        const uint32_t e0 = lds_u16(&L.huf[b0.peek(tl, lane)]);
+        const uint32_t e1 = lds_u16(&L.huf[b1.peek(tl, lane)]);
+        const uint32_t e2 = lds_u16(&L.huf[b2.peek(tl, lane)]);
+        b0.skip((int)(e0 >> 8)); b1.skip((int)(e1 >> 8)); b2.skip((int)(e2 >> 8));
         uint32_t e3 = 0;
         if (i < last) {
-            b3.need(tl, lane);
-            e3 = lds_u16(&L.huf[b3.peek(tl)]);
-            b3.B -= (int)(e3 >> 8);
+            e3 = lds_u16(&L.huf[b3.peek(tl, lane)]);
+            b3.skip((int)(e3 >> 8));
         }
         const uint32_t v = lane == 0 ? e0 : (lane == 1 ? e1 : (lane == 2 ? e2 : e3));
         if (lane < 3 || (lane == 3 && i < last)) out.st8(dst + lane * seg + i, v & 0xffu);
     }
-    return (b0.B == 0 && b1.B == 0 && b2.B == 0 && b3.B == 0 && !(b0.bad || b1.bad || b2.bad || b3.bad)) ? 0 : ZC;
+    return (b0.left() == 0 && b1.left() == 0 && b2.left() == 0 && b3.left() == 0) ? 0 : ZC;
 }
 
 struct FrameState {
@@ -972,10 +994,11 @@ struct FrameState {
     int llA, ofA, mlA;                  // accuracy logs of the current tables
     bool llV, ofV, mlV, hufV;           // tables valid for "repeat" / treeless modes
     int hufTl;
+    uint64_t clk[kZClk], clk_last;      // (LZH_ZSTD_STATS)
 };
 
 // one compressed block [bs, be) of the frame; output continues at op (returns new op, < 0 error)
-__device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& lw, owin::Sink& O, LDSA Lds& L,
+__device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& lw, owin::Sink& O, LDSA Lds& L,
                             FrameState& F, int bs, int be, int op, int fcs, int lane) {
     // ---- literals section (ZSTD_decodeLiteralsBlock)
     const uint32_t b0 = fbyte(fw, bs, lane);
@@ -1014,7 +1037,9 @@ __device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& l
         int p = bs + hsz;
         if (ltype == 2) {
             int tl = 0;
+            ZCLK(F, 0);
             const int u = read_huf(fw, rin, p, bs + hsz + cs, L, tl, lane);
+            ZCLK(F, 1);
             if (u < 0) return u;
             F.hufV = true;
             F.hufTl = tl;
@@ -1024,7 +1049,9 @@ __device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& l
         }
         lsrc = lout;
         lpos = fcs - rs;
+        ZCLK(F, 0);
         const int hr = huf_streams(rin, p, bs + hsz + cs - p, sf == 0 ? 1 : 4, O.out, lpos, rs, F.hufTl, L, lane);
+        ZCLK(F, 2);
         if (hr < 0) return hr;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // literal stores visible to the window loads
         seqpos = bs + hsz + cs;
@@ -1051,6 +1078,7 @@ __device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& l
         if (p >= be) return ZC;
         const uint32_t modes = fbyte(fw, p++, lane);
         if (modes & 3u) return ZC;
+        ZCLK(F, 0);
         int u = seq_table(fw, p, be, (int)(modes >> 6), 0, L.ll, F.llA, F.llV, L, lane);
         if (u < 0) return ZC;
         p += u;
@@ -1061,48 +1089,46 @@ __device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& l
         if (u < 0) return ZC;
         p += u;
         // ---- sequences (ZSTD_decodeSequence), executed a group at a time
+        ZCLK(F, 3);
         BackBits sb;
         if (!sb.init(rin, p, be - p, lane)) return ZC;
-        uint32_t sLL = sb.read(F.llA, lane), sOF = sb.read(F.ofA, lane), sML = sb.read(F.mlA, lane);
+        uint32_t sLL = sb.get(F.llA, lane), sOF = sb.get(F.ofA, lane), sML = sb.get(F.mlA, lane);
         int k = 0, glit = 0, gout = 0;                // group: members, literal bytes, output bytes
         uint32_t g_lit = 0, g_ml = 0, g_off = 0, g_ex = 0, g_lrel = 0;
         bool pend_big = false;
         int big_ll = 0, big_ml = 0, big_off = 0;
         for (int i = 0; i < nseq; i++) {
-            const uint32_t eLL = lds_u32(&L.ll[sLL]), eOF = lds_u32(&L.of[sOF]), eML = lds_u32(&L.ml[sML]);
-            const int ofc = (int)(eOF & 0xffu), mlc = (int)(eML & 0xffu), llc = (int)(eLL & 0xffu);
+            const Cell eL = lds_cell(&L.ll[sLL]), eO = lds_cell(&L.of[sOF]), eM = lds_cell(&L.ml[sML]);
+            const int ofc = (int)eO.x;
             int off;
-            const int ll0 = llc == 0;
+            const int ll0 = eL.x == 0;                // (only literal-length code 0 has baseline 0)
             if (ofc > 1) {
-                off = (int)((1u << ofc) - 3u + sb.read(ofc, lane));
+                off = (int)((1u << ofc) - 3u + sb.get(ofc, lane));
                 F.rep2 = F.rep1; F.rep1 = F.rep0; F.rep0 = off;
+            } else if (ofc == 0) {
+                off = ll0 ? F.rep1 : F.rep0;
+                if (ll0) { F.rep1 = F.rep0; F.rep0 = off; }
             } else {
-                const int idx = ofc + ll0 + (int)(ofc ? sb.read(1, lane) : 0u);   // 0..3
-                if (ofc == 0) {
-                    off = ll0 ? F.rep1 : F.rep0;
-                    if (ll0) { F.rep1 = F.rep0; F.rep0 = off; }
-                } else {
-                    int t = idx == 3 ? F.rep0 - 1 : (idx == 1 ? F.rep1 : F.rep2);
-                    t += t == 0;                      // (as the reference: offset 0 becomes 1)
-                    if (idx != 1) F.rep2 = F.rep1;
-                    F.rep1 = F.rep0;
-                    F.rep0 = off = t;
-                }
+                const int idx = 1 + ll0 + (int)sb.get(1, lane);   // 1..3
+                int t = idx == 3 ? F.rep0 - 1 : (idx == 1 ? F.rep1 : F.rep2);
+                t += t == 0;                          // (as the reference: offset 0 becomes 1)
+                if (idx != 1) F.rep2 = F.rep1;
+                F.rep1 = F.rep0;
+                F.rep0 = off = t;
             }
-            const int ml = (int)kMLBase[mlc] + (int)sb.read(kMLBits[mlc], lane);
-            const int ll = (int)kLLBase[llc] + (int)sb.read(kLLBits[llc], lane);
+            const int ml = (int)eM.x + (int)sb.get((int)(eM.y >> 24), lane);
+            const int ll = (int)eL.x + (int)sb.get((int)(eL.y >> 24), lane);
             if (i + 1 < nseq) {                       // state updates: LL, ML, OF
-                sLL = (eLL >> 16) + sb.read((int)((eLL >> 8) & 0xffu), lane);
-                sML = (eML >> 16) + sb.read((int)((eML >> 8) & 0xffu), lane);
-                sOF = (eOF >> 16) + sb.read((int)((eOF >> 8) & 0xffu), lane);
+                sLL = (eL.y & 0xffffu) + sb.get((int)((eL.y >> 16) & 0xffu), lane);
+                sML = (eM.y & 0xffffu) + sb.get((int)((eM.y >> 16) & 0xffu), lane);
+                sOF = (eO.y & 0xffffu) + sb.get((int)((eO.y >> 16) & 0xffu), lane);
+                if (sb.left() < 0) return ZC;
             } else {
                 // the reference also updates the states after the last sequence and then accepts
                 // an exhausted or overrun stream (ZSTD_decompressSequences_body: reload >= completed)
-                const int extra = (int)((eLL >> 8) & 0xffu) + (int)((eML >> 8) & 0xffu) + (int)((eOF >> 8) & 0xffu);
-                if (sb.B > extra) return ZC;
-                sb.B = 0;
+                const int extra = (int)(((eL.y >> 16) & 0xffu) + ((eM.y >> 16) & 0xffu) + ((eO.y >> 16) & 0xffu));
+                if (sb.left() > extra || sb.left() < 0) return ZC;
             }
-            if (sb.B < 0 || sb.bad) return ZC;
             // validity (ZSTD_execSequence): literals available, offset within the output, room
             const int o0 = op + gout;                 // output position of this sequence
             if (ll > rs - lp - glit || off > o0 + ll || (int64_t)o0 + ll + ml > (int64_t)(fcs - (rs - lp - glit - ll)))
@@ -1114,8 +1140,10 @@ __device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& l
                     const int ip = lpos + lp;
                     if (!lw.covers(ip, ip + glit + 16)) lw.load(ip, lane);
                     const uint64_t keep = k == LZH_WAVE ? ~0ull : ((1ull << k) - 1ull);
+                    ZCLK(F, 4);
                     groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kW, ip, op, gout, keep, (int)g_ex,
                                        g_lit | (g_ml << 16), g_lrel, (int)g_off, lane);
+                    ZCLK(F, 5);
                     op += gout;
                     lp += glit;
                     k = 0; glit = 0; gout = 0;
@@ -1124,11 +1152,13 @@ __device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& l
                 big_ll = ll; big_ml = ml; big_off = off;
             }
             if (pend_big) {                           // a long sequence on its own
+                ZCLK(F, 4);
                 O.literals(lw, lsrc, lpos + lp, op, big_ll, lane);
                 op += big_ll;
                 lp += big_ll;
                 O.match(op, big_off, big_ml, lane);
                 op += big_ml;
+                ZCLK(F, 6);
                 pend_big = false;
                 continue;
             }
@@ -1145,8 +1175,10 @@ __device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& l
             const int ip = lpos + lp;
             if (!lw.covers(ip, ip + glit + 16)) lw.load(ip, lane);
             const uint64_t keep = k == LZH_WAVE ? ~0ull : ((1ull << k) - 1ull);
+            ZCLK(F, 4);
             groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kW, ip, op, gout, keep, (int)g_ex, g_lit | (g_ml << 16),
                                g_lrel, (int)g_off, lane);
+            ZCLK(F, 5);
             op += gout;
             lp += glit;
         }
@@ -1166,8 +1198,8 @@ __device__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& l
 // one frame in rin[0, cs) -> out[0, cap): returns the decoded size or an error code
 // lout: the output region for reading decoded literals back (whole dwords: its range ends at
 // the dword holding the last byte, so no load that straddles the end reads back as zero)
-__device__ int decode_frame(const Bytes& rin, const Bytes& lout, int cs, owin::Sink& O, LDSA Lds& L, int cap,
-                            int lane) {
+__device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout, int cs, owin::Sink& O, LDSA Lds& L, int cap,
+                            int lane, unsigned long long* stats) {
     Win fw;
     fw.bind(rin);
     fw.load(0, lane);
@@ -1196,7 +1228,8 @@ __device__ int decode_frame(const Bytes& rin, const Bytes& lout, int cs, owin::S
     p += fsz;
     if (fcs > (uint64_t)cap) return ZC;
     const int n = (int)fcs;
-    FrameState F{1, 4, 8, 0, 0, 0, false, false, false, false, 0};
+    FrameState F{1, 4, 8, 0, 0, 0, false, false, false, false, 0, {0, 0, 0, 0, 0, 0, 0, 0}, 0};
+    if (LZH_ZSTD_STATS) F.clk_last = __builtin_amdgcn_s_memtime();
     Win lw;
     lw.bind(rin);
     lw.load(0, lane);
@@ -1232,6 +1265,9 @@ __device__ int decode_frame(const Bytes& rin, const Bytes& lout, int cs, owin::S
         }
         if (last) break;
     }
+    ZCLK(F, 7);
+    if (LZH_ZSTD_STATS && stats && lane == 0)
+        for (int i = 0; i < kZClk; i++) atomicAdd(&stats[i], (unsigned long long)F.clk[i]);
     if (op != n || p != cs) return ZC;
     return op;
 }
@@ -1241,7 +1277,7 @@ __device__ int decode_frame(const Bytes& rin, const Bytes& lout, int cs, owin::S
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                            const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
-                           int32_t* status, uint32_t chunk0) {
+                           int32_t* status, uint32_t chunk0, unsigned long long* stats) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_raw[(sizeof(zstdd::Lds) + 3) / 4];
     LDSA zstdd::Lds& L = *(LDSA zstdd::Lds*)lds_raw;
     const int lane = threadIdx.x;
@@ -1264,7 +1300,7 @@ lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, cons
         owin::Sink O{(LDSA uint8_t*)L.win, rout, 0, 0};
         Bytes lout;
         lout.init(out + ooff, (uint64_t)part + 3);
-        r = zstdd::decode_frame(rin, lout, cs, O, L, part, lane);
+        r = zstdd::decode_frame(rin, lout, cs, O, L, part, lane, stats);
         if (r > 0) O.flush(r, lane);
     }
     if (lane == 0) status[chunk] = r;
@@ -1284,7 +1320,26 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
                                       const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                       int32_t* status, uint32_t nchunks, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
+    unsigned long long* stats = nullptr;
+#if LZH_ZSTD_STATS
+    static unsigned long long* d_stats = nullptr;
+    if (!d_stats) (void)hipMalloc(&d_stats, zstdd::kZClk * sizeof(unsigned long long));
+    (void)hipMemsetAsync(d_stats, 0, zstdd::kZClk * sizeof(unsigned long long), s);
+    stats = d_stats;
+#endif
     hipLaunchKernelGGL(lzh_zstd_decompress_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets,
-                       csizes, n_total, chunk_size, out, status, 0u);
+                       csizes, n_total, chunk_size, out, status, 0u, stats);
+#if LZH_ZSTD_STATS
+    unsigned long long h[zstdd::kZClk];
+    (void)hipMemcpyAsync(h, d_stats, sizeof(h), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    unsigned long long tot = 0;
+    for (int i = 0; i < zstdd::kZClk; i++) tot += h[i];
+    static const char* names[zstdd::kZClk] = {"headers", "huf_table", "huf_streams", "seq_tables", "seq_decode",
+                                              "emit_group", "long_seq", "tail"};
+    fprintf(stderr, "zstd clocks per chunk %.0f:", (double)tot / nchunks);
+    for (int i = 0; i < zstdd::kZClk; i++) fprintf(stderr, " %s %.1f%%", names[i], 100.0 * h[i] / (tot ? tot : 1));
+    fprintf(stderr, "\n");
+#endif
     return hipGetLastError();
 }
