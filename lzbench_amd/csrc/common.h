@@ -48,6 +48,9 @@ __device__ __forceinline__ uint64_t ld_u40(rsrc_t r, int pos) {
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+// this lane's bit of a wave-uniform lane mask (the inverse of ballot: one v_cndmask on the SGPR
+// pair instead of a 64-bit shift, mask and compare per lane)
+__device__ __forceinline__ bool lane_on(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 __device__ __forceinline__ int ffs64(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ int rdlanei(int v, int l) { return (int)__builtin_amdgcn_readlane((uint32_t)v, l); }

@@ -259,7 +259,7 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 __device__ __forceinline__ void emit_group(const Win& w, owin::Sink& O, LDSA uint8_t* mark, int ip, int op,
                                            int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
                                            int off, int lane) {
-    const bool kmem = (keep >> lane) & 1ull;
+    const bool kmem = lane_on(keep);
     int carry = 63 - __builtin_clzll(keep);                      // (pass 0 always has a start at 0)
     // Branch-free pass body: lanes that have nothing to store write to harmless places (the mark
     // scratch's second half, or output bytes past `total` / of this pass that a later round or
@@ -311,7 +311,7 @@ __device__ __forceinline__ void emit_group(const Win& w, owin::Sink& O, LDSA uin
         uint64_t dm = ballot(act && done) | ~ballot(act);
         for (int r = 0; r < LZH_WAVE && ~dm; r++) {
             const int sl = src - pbase;
-            const bool ready = !((dm >> lane) & 1ull) && ((dm >> (sl & 63)) & 1ull);
+            const bool ready = !lane_on(dm) && ((dm >> (sl & 63)) & 1ull);
             const uint32_t vv = O.get(src);
             v = ready ? vv : v;
             O.put(op + ob, v);
@@ -370,7 +370,7 @@ __device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* 
         // ---- the real chain from lane 0
         const uint64_t M = chain_members(link, lane);
         // ---- acceptance rules per member (as lz4_one); the chain ends before the first failure
-        const bool mem = (M >> lane) & 1ull;
+        const bool mem = lane_on(M);
         const int L = mem ? lit + ml : 0;
         const int incl = wave_incl_scan(L);
         const int excl = incl - L;
@@ -388,8 +388,10 @@ __device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* 
         const int lastk = 63 - __builtin_clzll(keep);
         const int total = rdlanei(incl, lastk);
         const int ip_next = ip + rdlanei(pe - ip, lastk);
+#ifndef LZH_ABL_NOEMIT
         emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)ml << 16), (uint32_t)(p1 - ip),
                    off, lane);
+#endif
         op += total;
         ip = ip_next;
     }
@@ -455,7 +457,7 @@ __device__ int snappy_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_
         // link: next tag lane; 255 = not parsed here; 254 = the stream ends after this tag
         const int link = (cplx || !inwin || x >= cs) ? 255 : (nx >= cs ? 254 : nx - ip);
         const uint64_t M = chain_members(link, lane);
-        const bool mem = (M >> lane) & 1ull;
+        const bool mem = lane_on(M);
         const int L = mem ? len : 0;
         const int incl = wave_incl_scan(L);
         const int excl = incl - L;

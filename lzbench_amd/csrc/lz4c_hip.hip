@@ -246,7 +246,7 @@ __device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const B
             O.put(op + ob, 0xffu);
             wave_lds_fence();
             const int stl = (int)st;
-            if (((mem >> lane) & 1ull) && stl >= pass * LZH_WAVE && stl < (pass + 1) * LZH_WAVE)
+            if (lane_on(mem) && stl >= pass * LZH_WAVE && stl < (pass + 1) * LZH_WAVE)
                 O.put(op + stl, (uint32_t)lane);
             wave_lds_fence();
             const int mv = (int)O.get(op + ob);
@@ -478,7 +478,7 @@ __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t los
             LZ_STAT(3, __builtin_popcountll(pr_m));                                                \
             const uint64_t below_ = (1ull << lane) - 1ull;                                         \
             const int p_ = pr_base + lane;                                                         \
-            const bool mem_ = (pr_m >> lane) & 1ull;                                               \
+            const bool mem_ = lane_on(pr_m);                                               \
             const uint64_t mb_ = pr_m & below_;                                                    \
             const int jp_ = mb_ ? 63 - __builtin_clzll(mb_) : lane;                                \
             const int ep_ = (int)lane_gather((uint32_t)pr_e, jp_);                                 \
@@ -757,7 +757,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     if (!(coll & E)) break;
                     const uint64_t mk = grp & below & I;
                     const int kt = mk ? 63 - __builtin_clzll(mk) : -1;
-                    const bool fix = ((E >> lane) & 1ull) && kt != ak;
+                    const bool fix = lane_on(E) && kt != ak;
                     if (!ballot(fix)) break;
                     LZ_STAT(2, 1);
                     const bool far = fix && kt >= 0 && kt != prev;
@@ -816,7 +816,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         pins = -1;
                     }
                     // table: the last inserted lane of each slot, or the slot's old value
-                    const bool inI = (I >> lane) & 1ull;
+                    const bool inI = lane_on(I);
                     if (LZH_BRFREE && vmask == ~0ull) {
                         // every lane stores its slot's final value (all lanes of a slot agree):
                         // the slot's last inserted lane, else its old value

@@ -242,7 +242,7 @@ __device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const B
             mark[lane] = 0xff;
             wave_lds_fence();
             const int stl = (int)st;
-            if (((mem >> lane) & 1ull) && stl >= pb && stl < pb + LZH_WAVE) mark[stl - pb] = (uint8_t)lane;
+            if (lane_on(mem) && stl >= pb && stl < pb + LZH_WAVE) mark[stl - pb] = (uint8_t)lane;
             wave_lds_fence();
             const int mv = (int)mark[lane];
             const uint64_t smask = ballot(mv != 0xff);
@@ -512,7 +512,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                         const int j = mle ? 63 - __builtin_clzll(mle) : lane;
                         const int ej = (int)lane_gather((uint32_t)e, j);
                         bool pr;
-                        if (!mle) pr = (P0 >> lane) & 1ull;
+                        if (!mle) pr = lane_on(P0);
                         else if (lane == j) pr = true;
                         else pr = lane >= ej && ((after_copy(ej) >> lane) & 1ull);
                         E = ballot(pr && (!endp || lane < eL));
@@ -522,7 +522,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     if (!(coll & E)) break;
                     const uint64_t mk = grp & below & I;
                     const int kt = mk ? 63 - __builtin_clzll(mk) : -1;
-                    const bool fix = ((E >> lane) & 1ull) && kt != ak;
+                    const bool fix = lane_on(E) && kt != ak;
                     if (!ballot(fix)) break;
                     SN_STAT(2, 1);
                     const bool far = fix && kt >= 0 && kt != prev;
@@ -543,7 +543,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 // ---- records (literal from the previous copy's end, or next_emit)
                 if (Mm) {
                     SN_STAT(3, __builtin_popcountll(Mm));
-                    const bool mem = (Mm >> lane) & 1ull;
+                    const bool mem = lane_on(Mm);
                     const uint64_t mb = Mm & below;
                     const int jp = mb ? 63 - __builtin_clzll(mb) : lane;
                     const int ep = (int)lane_gather((uint32_t)e, jp);
@@ -571,7 +571,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 if (endp) break;                                         // remainder from next_emit
                 // table: the last inserted lane of each slot, or the slot's old value
                 {
-                    const bool inI = (I >> lane) & 1ull;
+                    const bool inI = lane_on(I);
                     if (!losers) {
                         if (!inI) T.put(h, old);
                     } else {
