@@ -16,17 +16,35 @@
 
 namespace {
 
+#ifndef LZH_DEC_RING
+#define LZH_DEC_RING 1
+#endif
+constexpr int kRingBytes = 512 + 16;   // LDS copy of a window: ring over offsets mod 512 + mirror
 
-struct Win {
+// Register window over a byte stream (512 bytes in two VGPRs across the wave) with an LDS copy
+// (ring indexed by descriptor offset mod 512, its first 16 bytes mirrored past the end): uniform
+// reads use v_readlane on the registers, per-lane reads one LDS load instead of cross-lane
+// permutes of both registers.
+template <bool kRing>
+struct WinT {
     rsrc_t r;
     int sh;       // descriptor offset of stream byte 0
     int wb;       // descriptor offset (4-aligned) of the window start
     uint32_t w0, w1;
-    __device__ __forceinline__ void bind(const Bytes& b) { r = b.r; sh = b.sh; }
+    LDSA uint8_t* ring;
+    __device__ __forceinline__ void bind(const Bytes& b, LDSA uint8_t* rg) { r = b.r; sh = b.sh; ring = rg; }
+    __device__ __forceinline__ void put_ring(int D, uint32_t v) const {
+        if (!(LZH_DEC_RING && kRing)) return;
+        const int i = D & 511;
+        *(volatile LDSA uint32_t*)(ring + i) = v;
+        if (i < 16) *(volatile LDSA uint32_t*)(ring + 512 + i) = v;
+    }
     __device__ __forceinline__ void load(int pos, int lane) {
         wb = (pos + sh) & ~3;
         w0 = ld_b32(r, wb + 4 * lane);
         w1 = ld_b32(r, wb + 256 + 4 * lane);
+        put_ring(wb + 4 * lane, w0);
+        put_ring(wb + 256 + 4 * lane, w1);
     }
     // make stream bytes [pos, pos+16) addressable
     __device__ __forceinline__ void ensure(int pos, int lane) {
@@ -36,6 +54,7 @@ struct Win {
             w0 = w1;
             wb += 256;
             w1 = ld_b32(r, wb + 256 + 4 * lane);
+            put_ring(wb + 256 + 4 * lane, w1);
             return;
         }
         load(pos, lane);
@@ -50,6 +69,11 @@ struct Win {
     // per-lane 4 bytes at stream position pos (pos .. pos+3 inside the window)
     __device__ __forceinline__ uint32_t lane_word(int pos) const {
         const int x = pos + sh;
+        if (LZH_DEC_RING && kRing) {
+            const int a = x & 508;
+            const uint32_t lo = *(volatile const LDSA uint32_t*)(ring + a), hi = *(volatile const LDSA uint32_t*)(ring + a + 4);
+            return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)x & 3u);
+        }
         const int d = (x - wb) >> 2;
         const uint32_t a0 = lane_gather(w0, d & 63), a1 = lane_gather(w1, d & 63);
         const uint32_t b0 = lane_gather(w0, (d + 1) & 63), b1 = lane_gather(w1, (d + 1) & 63);
@@ -59,11 +83,15 @@ struct Win {
     // per-lane byte at stream position pos (inside the window) via cross-lane permute
     __device__ __forceinline__ uint32_t lane_byte(int pos) const {
         const int x = pos + sh;
+        if (LZH_DEC_RING && kRing) return ((volatile const LDSA uint8_t*)ring)[x & 511];
         const int d = (x - wb) >> 2;
         const uint32_t a = lane_gather(w0, d & 63), b = lane_gather(w1, d & 63);
         return ((d < 64 ? a : b) >> (8 * (x & 3))) & 0xffu;
     }
 };
+
+typedef WinT<true> Win;     // lz4 / snappy decoders
+typedef WinT<false> ZWin;   // zstd (its LDS budget has no room for rings: 8 waves per CU)
 
 __device__ __forceinline__ void copy_raw(const Bytes& in, const Bytes& out, int len, int lane) {
     copy_span(in, 0, out, 0, len, lane, LZH_WAVE);
@@ -118,7 +146,8 @@ struct Sink {
     }
 
     // literal run in[src, src+len) -> op
-    __device__ __forceinline__ void literals(const Win& w, const Bytes& in, int src, int op, int len, int lane) {
+    template <class W>
+    __device__ __forceinline__ void literals(const W& w, const Bytes& in, int src, int op, int len, int lane) {
         if (len > 8 * LZH_WAVE) {
             // bulk: straight to global memory; the window restarts after the run
             flush(op, lane);
@@ -252,15 +281,31 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
+#ifndef LZH_DEC_DPPOWN
+#define LZH_DEC_DPPOWN 0   // (DPP prefix-max owner: measured neutral for lz4, 1 % slower for snappy)
+#endif
+// Wave-wide inclusive prefix maximum (DPP; -1 is the identity for the marks below).
+__device__ __forceinline__ int wave_incl_max(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));   // row_shr:1
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));   // row_shr:2
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));   // row_shr:4
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));   // row_shr:8
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return x;
+}
+
 // Assemble a group's output [op, op + total): sequence k (member lane k, output start excl) is
 // litk literal bytes from stream position ip + lrel, then mlk match bytes copied from offset offk
 // (byte-by-byte semantics); a literal-only member has mlk = 0, a copy-only member litk = 0.
 // One output byte per lane per pass; the owner is the last start mark at or before the byte.
-__device__ __forceinline__ void emit_group(const Win& w, owin::Sink& O, LDSA uint8_t* mark, int ip, int op,
+template <class W>
+__device__ __forceinline__ void emit_group(const W& w, owin::Sink& O, LDSA uint8_t* mark, int ip, int op,
                                            int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
                                            int off, int lane) {
     const bool kmem = lane_on(keep);
     int carry = 63 - __builtin_clzll(keep);                      // (pass 0 always has a start at 0)
+    const uint32_t xl = ((uint32_t)excl << 10) | lrel;           // (lrel < 1024, excl < 2^22)
     // Branch-free pass body: lanes that have nothing to store write to harmless places (the mark
     // scratch's second half, or output bytes past `total` / of this pass that a later round or
     // group overwrites before any flush), so no exec-mask juggling per conditional access.
@@ -272,14 +317,23 @@ __device__ __forceinline__ void emit_group(const Win& w, owin::Sink& O, LDSA uin
         mark[mine ? excl - pb : LZH_WAVE + lane] = (uint8_t)lane;
         wave_lds_fence();
         const int mv = (int)mark[lane];
-        const uint64_t S = ballot(mv != 0xff);
-        const uint64_t le = S & ((2ull << lane) - 1ull);
-        const int js = le ? 63 - __builtin_clzll(le) : lane;
-        const int own_here = (int)lane_gather((uint32_t)mv, js);
-        const int k = le ? own_here : carry;
+        int k;
+        if (LZH_DEC_DPPOWN) {
+            // members' lane ids grow with their output starts: the owner is a prefix maximum
+            const int km = wave_incl_max(mv == 0xff ? -1 : mv);
+            k = km >= 0 ? km : carry;
+        } else {
+            const uint64_t S = ballot(mv != 0xff);
+            const uint64_t le = S & ((2ull << lane) - 1ull);
+            const int js = le ? 63 - __builtin_clzll(le) : lane;
+            const int own_here = (int)lane_gather((uint32_t)mv, js);
+            k = le ? own_here : carry;
+        }
         carry = rdlanei(k, 63);
-        const uint32_t a = lane_gather(pA, k), b = lane_gather(lrel, k);
-        const int ek = (int)lane_gather((uint32_t)excl, k);
+        const uint32_t a = lane_gather(pA, k);
+        const uint32_t xk = lane_gather(xl, k);
+        const uint32_t b = xk & 1023u;
+        const int ek = (int)(xk >> 10);
         const int offk = (int)lane_gather((uint32_t)off, k);
         const int litk = (int)(a & 0xffffu);
         const int ob = pb + lane;
@@ -342,11 +396,12 @@ __device__ __forceinline__ uint64_t chain_members(int link, int lane) {
     return ballot(x == lane && link != 255);
 }
 
-__device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
+__device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* mark, LDSA uint8_t* ring, int cap,
+                          int lane) {
     if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
     if (cs <= 0) return -1;
     Win w;
-    w.bind(in);
+    w.bind(in, ring);
     w.load(0, lane);
     int ip = 0, op = 0;
     for (int guard = 0; guard <= cs; guard++) {
@@ -404,9 +459,10 @@ __device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* 
 // of snappy_decode below (snappy.cc:848-952) are checked per member against the prefix sum, and
 // the group is cut before the first failure (which, like 2..4-byte literal lengths, runs through
 // the checked per-tag path).
-__device__ int snappy_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* mark, int cap, int lane) {
+__device__ int snappy_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* mark, LDSA uint8_t* ring, int cap,
+                             int lane) {
     Win w;
-    w.bind(in);
+    w.bind(in, ring);
     w.load(0, lane);
     int ip = 0;
     uint32_t ulen = 0;
@@ -521,7 +577,8 @@ extern "C" __global__ void __launch_bounds__(64)
 lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                          const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                          int32_t* status, uint32_t chunk0) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + 2 * LZH_WAVE];   // output window | start marks
+    // output window | start marks | input ring
+    __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + 2 * LZH_WAVE + kRingBytes];
     const int lane = threadIdx.x;
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t ooff = chunk * chunk_size;
@@ -539,8 +596,10 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
         r = part;
     } else {
         owin::Sink O{(LDSA uint8_t*)win, rout, 0, 0};
-        r = codec == 0 ? groups::lz4_decode(rin, cs, O, (LDSA uint8_t*)win + owin::kW, part, lane)
-                       : groups::snappy_decode(rin, cs, O, (LDSA uint8_t*)win + owin::kW, part, lane);
+        LDSA uint8_t* mark = (LDSA uint8_t*)win + owin::kW;
+        LDSA uint8_t* ring = mark + 2 * LZH_WAVE;
+        r = codec == 0 ? groups::lz4_decode(rin, cs, O, mark, ring, part, lane)
+                       : groups::snappy_decode(rin, cs, O, mark, ring, part, lane);
         if (r > 0) O.flush(r, lane);
     }
     if (lane == 0) status[chunk] = r;
@@ -628,8 +687,8 @@ __device__ __forceinline__ Cell lds_cell(const LDSA Cell* p) {
 __device__ __forceinline__ int hb32(uint32_t v) { return 31 - __builtin_clz(v); }   // v > 0
 
 // uniform little-endian reads from a forward register window (Win) over the frame
-__device__ __forceinline__ uint32_t fbyte(Win& w, int pos, int lane) { w.ensure(pos, lane); return uni(w.byte(pos)); }
-__device__ __forceinline__ uint32_t fword(Win& w, int pos, int lane) {   // bytes pos..pos+3
+__device__ __forceinline__ uint32_t fbyte(ZWin& w, int pos, int lane) { w.ensure(pos, lane); return uni(w.byte(pos)); }
+__device__ __forceinline__ uint32_t fword(ZWin& w, int pos, int lane) {   // bytes pos..pos+3
     w.ensure(pos, lane);
     const int x = pos + w.sh, d = (x - w.wb) >> 2;
     const uint32_t a = d < 64 ? rdlane(w.w0, d) : rdlane(w.w1, d - 64);
@@ -709,7 +768,7 @@ struct BackBits {
 
 // FSE_readNCount (entropy_common.c:70-215) over the frame from byte pos: normalized counts
 // into L.norm[0..maxSym], returns the header size in bytes (<= 0: corrupt); *al = accuracy log
-__device__ __forceinline__ int read_ncount(Win& fw, int pos, int end, int maxSym, int maxLog, LDSA Lds& L, int& al, int& nsym,
+__device__ __forceinline__ int read_ncount(ZWin& fw, int pos, int end, int maxSym, int maxLog, LDSA Lds& L, int& al, int& nsym,
                            int lane) {
     for (int i = lane; i < 256; i += LZH_WAVE) L.norm[i] = 0;
     int bit = 0;                                      // bits consumed from pos
@@ -820,7 +879,7 @@ __device__ __forceinline__ void seq_cells(LDSA Cell* T, int size, int which, int
 
 // sequence table for one of LL / OF / ML (ZSTD_buildSeqTable, zstd_decompress_block.c:~560):
 // mode 0 predefined, 1 RLE, 2 FSE-compressed, 3 repeat.  Returns bytes consumed, < 0 corrupt.
-__device__ __forceinline__ int seq_table(Win& fw, int pos, int end, int mode, int which, LDSA Cell* T, int& al, bool& valid,
+__device__ __forceinline__ int seq_table(ZWin& fw, int pos, int end, int mode, int which, LDSA Cell* T, int& al, bool& valid,
                          LDSA Lds& L, int lane) {
     const int maxSym = which == 0 ? 35 : (which == 1 ? 31 : 52);
     const int maxLog = which == 1 ? 8 : 9;
@@ -861,7 +920,7 @@ __device__ __forceinline__ int seq_table(Win& fw, int pos, int end, int mode, in
 
 // Huffman tree description (HUF_readStats, entropy_common.c:271-334; HUF_readDTableX1,
 // huf_decompress.c:342-470) at pos.  Returns bytes consumed (< 0 corrupt), *tl = table log.
-__device__ __forceinline__ int read_huf(Win& fw, const Bytes& src, int pos, int end, LDSA Lds& L, int& tl, int lane) {
+__device__ __forceinline__ int read_huf(ZWin& fw, const Bytes& src, int pos, int end, LDSA Lds& L, int& tl, int lane) {
     if (pos >= end) return ZC;
     const int hb = (int)fbyte(fw, pos, lane);
     int n, used;
@@ -961,8 +1020,8 @@ __device__ __forceinline__ int huf_streams(const Bytes& src, int pos, int csize,
         return b.left() == 0 ? 0 : ZC;
     }
     if (csize < 10) return ZC;
-    Win fw;
-    fw.bind(src);
+    ZWin fw;
+    fw.bind(src, nullptr);
     fw.load(pos, lane);
     const int z1 = (int)(fword(fw, pos, lane) & 0xffffu), z2 = (int)(fword(fw, pos + 2, lane) & 0xffffu),
               z3 = (int)(fword(fw, pos + 4, lane) & 0xffffu);
@@ -1000,7 +1059,7 @@ struct FrameState {
 };
 
 // one compressed block [bs, be) of the frame; output continues at op (returns new op, < 0 error)
-__device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout, Win& fw, Win& lw, owin::Sink& O, LDSA Lds& L,
+__device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout, ZWin& fw, ZWin& lw, owin::Sink& O, LDSA Lds& L,
                             FrameState& F, int bs, int be, int op, int fcs, int lane) {
     // ---- literals section (ZSTD_decodeLiteralsBlock)
     const uint32_t b0 = fbyte(fw, bs, lane);
@@ -1058,7 +1117,7 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // literal stores visible to the window loads
         seqpos = bs + hsz + cs;
     }
-    lw.bind(lsrc);
+    lw.bind(lsrc, nullptr);
     lw.load(lpos, lane);
 
     // ---- sequences section header (ZSTD_decodeSeqHeaders)
@@ -1202,8 +1261,8 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
 // the dword holding the last byte, so no load that straddles the end reads back as zero)
 __device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout, int cs, owin::Sink& O, LDSA Lds& L, int cap,
                             int lane, unsigned long long* stats) {
-    Win fw;
-    fw.bind(rin);
+    ZWin fw;
+    fw.bind(rin, nullptr);
     fw.load(0, lane);
     if (cs < 9) return ZC;
     const uint32_t magic = fword(fw, 0, lane);
@@ -1232,8 +1291,8 @@ __device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout,
     const int n = (int)fcs;
     FrameState F{1, 4, 8, 0, 0, 0, false, false, false, false, 0, {0, 0, 0, 0, 0, 0, 0, 0}, 0};
     if (LZH_ZSTD_STATS) F.clk_last = __builtin_amdgcn_s_memtime();
-    Win lw;
-    lw.bind(rin);
+    ZWin lw;
+    lw.bind(rin, nullptr);
     lw.load(0, lane);
     int op = 0;
     for (int guard = 0; guard <= cs; guard++) {
