@@ -570,15 +570,10 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 }
                 if (endp) break;                                         // remainder from next_emit
                 // table: the last inserted lane of each slot, or the slot's old value
-                {
-                    const bool inI = lane_on(I);
-                    if (!losers) {
-                        if (!inI) T.put(h, old);
-                    } else {
-                        const uint64_t gi = grp & I;
-                        const bool wr = gi == 0 || (inI && (gi & ~((2ull << lane) - 1ull)) == 0);
-                        if (wr) T.put(h, inI ? (uint32_t)p : old);
-                    }
+                {   // every lane stores its slot's final value, all lanes of a slot agreeing (a run
+                    // batch's 64 probes are all valid): no exec-mask juggling around the store
+                    const uint64_t gi = grp & I;
+                    T.put(h, gi ? (uint32_t)(base + 63 - __builtin_clzll(gi)) : old);
                     wave_lds_fence();
                 }
                 if (Mm) {
