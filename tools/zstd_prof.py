@@ -23,3 +23,10 @@ for _ in range(a.reps):
 ok = bool((dc.out[:n].cpu().numpy() == data).all())
 print(f"zstd decode {a.corpus} {a.mib} MiB -b{a.chunk >> 10} l{a.level}: ratio {len(packed) / n:.3f} ok={ok} "
       f"{min(ts):.2f} ms -> {n / min(ts) / 1e6:.1f} GB/s", flush=True)
+if os.environ.get("ZSTD_CPU"):
+    import time
+    for th in (1, 16):
+        t = time.perf_counter()
+        r, out = O.decompress_chunks(packed, cs, n, "zstd", a.chunk, threads=th if th > 1 else 0)
+        dt = time.perf_counter() - t
+        print(f"reference zstd 1.5.2 decode on the host, {th} thread(s): {n / dt / 1e6:.0f} MB/s (ok={r == n})", flush=True)
