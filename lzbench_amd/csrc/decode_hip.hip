@@ -661,16 +661,20 @@ __constant__ int8_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 
                                    1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
 __constant__ int8_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
-struct Cell { uint32_t x, y; };      // (an FSE decoding-table cell)
+// FSE decoding-table cell, 32 bits: next-state base (9) | nbBits << 9 (4) | extra bits << 13 (5)
+// | symbol << 18 (6).  For LL/ML the symbol is the length code (its baseline comes from a constant
+// table off the state chain), for OF the offset code (= its extra-bit count).
+typedef uint32_t Cell;
+__device__ __forceinline__ uint32_t c_next(Cell c) { return c & 511u; }
+__device__ __forceinline__ int c_nb(Cell c) { return (int)((c >> 9) & 15u); }
+__device__ __forceinline__ int c_add(Cell c) { return (int)((c >> 13) & 31u); }
+__device__ __forceinline__ uint32_t c_sym(Cell c) { return c >> 18; }
 
 // per-wave LDS
 struct Lds {
     uint8_t win[kW + 2 * LZH_WAVE];     // output window | start marks (groups::emit_group)
     uint16_t huf[1 << kHufLogMax];      // Huffman decoding table: symbol | nbBits << 8
-    // FSE decoding tables, one (x, y) pair per state: y = next-state base | nbBits << 16 |
-    // extra bits << 24; x = the symbol, or for LL/ML the baseline value and for OF the code
-    // (ZSTD_seqSymbol's fields, so a sequence needs no other table)
-    Cell ll[512], ml[512], of[256];
+    Cell ll[512], ml[512], of[256];     // sequence FSE tables (ZSTD_seqSymbol's fields, packed)
     Cell wt[64];                       // FSE table of the Huffman weights (accuracy <= 6)
     uint8_t weights[256];
     int16_t norm[256];
@@ -680,10 +684,7 @@ struct Lds {
 __device__ __forceinline__ uint32_t lds_u32(const LDSA uint32_t* p) { return uni(*(volatile const LDSA uint32_t*)p); }
 __device__ __forceinline__ uint32_t lds_u16(const LDSA uint16_t* p) { return uni(*(volatile const LDSA uint16_t*)p); }
 __device__ __forceinline__ uint32_t lds_u8(const LDSA uint8_t* p) { return uni(*(volatile const LDSA uint8_t*)p); }
-__device__ __forceinline__ Cell lds_cell(const LDSA Cell* p) {
-    const uint64_t v = *(volatile const LDSA uint64_t*)p;
-    return Cell{uni((uint32_t)v), uni((uint32_t)(v >> 32))};
-}
+__device__ __forceinline__ Cell lds_cell(const LDSA Cell* p) { return uni(*(volatile const LDSA uint32_t*)p); }
 __device__ __forceinline__ int hb32(uint32_t v) { return 31 - __builtin_clz(v); }   // v > 0
 
 // uniform little-endian reads from a forward register window (Win) over the frame
@@ -835,7 +836,7 @@ __device__ __forceinline__ void build_fse(LDSA Cell* T, int al, int nsym, LDSA L
     for (int s = 0; s < nsym; s++) {                  // low-probability symbols at the top
         const int n = (int16_t)lds_u16((const LDSA uint16_t*)&L.norm[s]);
         if (n == -1) {
-            if (lane == 0) T[high].x = (uint32_t)s;
+            if (lane == 0) T[high] = (uint32_t)s << 18;
             high--;
         }
         if (lane == 0) L.next[s] = (uint16_t)(n == -1 ? 1 : n);
@@ -846,19 +847,19 @@ __device__ __forceinline__ void build_fse(LDSA Cell* T, int al, int nsym, LDSA L
     for (int s = 0; s < nsym; s++) {
         const int n = (int16_t)lds_u16((const LDSA uint16_t*)&L.norm[s]);
         for (int i = 0; i < n; i++) {
-            if (lane == 0) T[p].x = (uint32_t)s;
+            if (lane == 0) T[p] = (uint32_t)s << 18;
             p = (p + step) & mask;
             while (p > high) p = (p + step) & mask;
         }
     }
     wave_lds_fence();
     for (int u = 0; u < size; u++) {
-        const uint32_t s = uni(((volatile const LDSA uint32_t*)T)[2 * u]);
+        const uint32_t s = uni(((volatile const LDSA uint32_t*)T)[u]) >> 18;
         const uint32_t nx = lds_u16(&L.next[s]);
         if (lane == 0) L.next[s] = (uint16_t)(nx + 1);
         const int nb = al - hb32(nx);
         const uint32_t base = (nx << nb) - (uint32_t)size;
-        if (lane == 0) T[u].y = base | ((uint32_t)nb << 16);
+        if (lane == 0) T[u] = (s << 18) | ((uint32_t)nb << 9) | base;
         wave_lds_fence();
     }
 }
@@ -866,13 +867,9 @@ __device__ __forceinline__ void build_fse(LDSA Cell* T, int al, int nsym, LDSA L
 // sequence-table cells: symbol -> baseline value and extra-bit count (RFC 8878 3.1.1.3.2.1.1)
 __device__ __forceinline__ void seq_cells(LDSA Cell* T, int size, int which, int lane) {
     for (int u = lane; u < size; u += LZH_WAVE) {
-        const uint32_t s = T[u].x, y = T[u].y & 0xffffffu;
-        uint32_t x, add;
-        if (which == 0) { x = kLLBase[s]; add = kLLBits[s]; }
-        else if (which == 2) { x = kMLBase[s]; add = kMLBits[s]; }
-        else { x = s; add = s; }
-        T[u].x = x;
-        T[u].y = y | (add << 24);
+        const uint32_t c = T[u], s = c >> 18;
+        const uint32_t add = which == 0 ? kLLBits[s] : (which == 2 ? kMLBits[s] : s);
+        T[u] = c | (add << 13);
     }
     wave_lds_fence();
 }
@@ -898,7 +895,7 @@ __device__ __forceinline__ int seq_table(ZWin& fw, int pos, int end, int mode, i
         if (pos >= end) return ZC;
         const int s = (int)fbyte(fw, pos, lane);
         if (s > maxSym) return ZC;
-        if (lane == 0) { T[0].x = (uint32_t)s; T[0].y = 0u; }
+        if (lane == 0) T[0] = (uint32_t)s << 18;
         wave_lds_fence();
         seq_cells(T, 1, which, lane);
         al = 0;
@@ -949,13 +946,13 @@ __device__ __forceinline__ int read_huf(ZWin& fw, const Bytes& src, int pos, int
         for (int k = 0;; k ^= 1) {
             if (n > 253) return ZC;
             const Cell e = lds_cell(&L.wt[k ? s2 : s1]);
-            if (lane == 0) L.weights[n] = (uint8_t)e.x;
+            if (lane == 0) L.weights[n] = (uint8_t)c_sym(e);
             n++;
-            const uint32_t ns = (e.y & 0xffffu) + bb.get((int)((e.y >> 16) & 0xffu), lane);
+            const uint32_t ns = c_next(e) + bb.get(c_nb(e), lane);
             if (k) s2 = ns; else s1 = ns;
             if (bb.left() < 0) {
                 const Cell e2 = lds_cell(&L.wt[k ? s1 : s2]);
-                if (lane == 0) L.weights[n] = (uint8_t)e2.x;
+                if (lane == 0) L.weights[n] = (uint8_t)c_sym(e2);
                 n++;
                 break;
             }
@@ -1160,9 +1157,10 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
         int big_ll = 0, big_ml = 0, big_off = 0;
         for (int i = 0; i < nseq; i++) {
             const Cell eL = lds_cell(&L.ll[sLL]), eO = lds_cell(&L.of[sOF]), eM = lds_cell(&L.ml[sML]);
-            const int ofc = (int)eO.x;
+            const int ofc = (int)c_sym(eO);
             int off;
-            const int ll0 = eL.x == 0;                // (only literal-length code 0 has baseline 0)
+            const int llc = (int)c_sym(eL), mlc = (int)c_sym(eM);
+            const int ll0 = llc == 0;                 // (only literal-length code 0 has baseline 0)
             if (ofc > 1) {
                 off = (int)((1u << ofc) - 3u + sb.get(ofc, lane));
                 F.rep2 = F.rep1; F.rep1 = F.rep0; F.rep0 = off;
@@ -1177,17 +1175,17 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
                 F.rep1 = F.rep0;
                 F.rep0 = off = t;
             }
-            const int ml = (int)eM.x + (int)sb.get((int)(eM.y >> 24), lane);
-            const int ll = (int)eL.x + (int)sb.get((int)(eL.y >> 24), lane);
+            const int ml = (int)kMLBase[mlc] + (int)sb.get(c_add(eM), lane);
+            const int ll = (int)kLLBase[llc] + (int)sb.get(c_add(eL), lane);
             if (i + 1 < nseq) {                       // state updates: LL, ML, OF
-                sLL = (eL.y & 0xffffu) + sb.get((int)((eL.y >> 16) & 0xffu), lane);
-                sML = (eM.y & 0xffffu) + sb.get((int)((eM.y >> 16) & 0xffu), lane);
-                sOF = (eO.y & 0xffffu) + sb.get((int)((eO.y >> 16) & 0xffu), lane);
+                sLL = c_next(eL) + sb.get(c_nb(eL), lane);
+                sML = c_next(eM) + sb.get(c_nb(eM), lane);
+                sOF = c_next(eO) + sb.get(c_nb(eO), lane);
                 if (sb.left() < 0) return ZC;
             } else {
                 // the reference also updates the states after the last sequence and then accepts
                 // an exhausted or overrun stream (ZSTD_decompressSequences_body: reload >= completed)
-                const int extra = (int)(((eL.y >> 16) & 0xffu) + ((eM.y >> 16) & 0xffu) + ((eO.y >> 16) & 0xffu));
+                const int extra = c_nb(eL) + c_nb(eM) + c_nb(eO);
                 if (sb.left() > extra || sb.left() < 0) return ZC;
             }
             // validity (ZSTD_execSequence): literals available, offset within the output, room
