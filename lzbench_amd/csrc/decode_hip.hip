@@ -111,19 +111,21 @@ namespace owin {
 #endif
 constexpr int kW = LZH_DEC_KW;   // LDS output window bytes (power of two)
 
-struct Sink {
+template <int KW>
+struct SinkT {
+    static constexpr int kWin = KW;
     LDSA uint8_t* b;
     Bytes out;
     int flushed;      // output bytes [0, flushed) are in global memory
     int ringlo;       // output bytes [ringlo, op) are in the window (bulk literal runs bypass it)
     __device__ __forceinline__ void put(int pos, uint32_t v) const {
-        ((volatile LDSA uint8_t*)b)[(pos + out.sh) & (kW - 1)] = (uint8_t)v;
+        ((volatile LDSA uint8_t*)b)[(pos + out.sh) & (KW - 1)] = (uint8_t)v;
     }
     __device__ __forceinline__ uint32_t get(int pos) const {
-        return ((volatile const LDSA uint8_t*)b)[(pos + out.sh) & (kW - 1)];
+        return ((volatile const LDSA uint8_t*)b)[(pos + out.sh) & (KW - 1)];
     }
     __device__ __forceinline__ uint32_t dword(int X) const {
-        return ((volatile const LDSA uint32_t*)b)[(X & (kW - 1)) >> 2];
+        return ((volatile const LDSA uint32_t*)b)[(X & (KW - 1)) >> 2];
     }
     // global <- window bytes [flushed, upto)
     __device__ __forceinline__ void flush(int upto, int lane) {
@@ -169,7 +171,7 @@ struct Sink {
     // out[op + t] = out[op - off + t] for t < len (byte by byte semantics), 0 < off <= op
     __device__ __forceinline__ void match(int op, int off, int len, int lane) {
         const int src0 = op - off;
-        if (src0 >= ringlo && off <= kW - LZH_WAVE) {
+        if (src0 >= ringlo && off <= KW - LZH_WAVE) {
             for (int base = 0; base < len; base += LZH_WAVE) {
                 const int t = base + lane;
                 const int s = off >= LZH_WAVE ? src0 + t : src0 + (int)((uint32_t)t % (uint32_t)off);
@@ -192,6 +194,8 @@ struct Sink {
         maybe_flush(op + len, lane);
     }
 };
+
+typedef SinkT<kW> Sink;
 
 }  // namespace owin
 
@@ -299,8 +303,8 @@ __device__ __forceinline__ int wave_incl_max(int x) {
 // litk literal bytes from stream position ip + lrel, then mlk match bytes copied from offset offk
 // (byte-by-byte semantics); a literal-only member has mlk = 0, a copy-only member litk = 0.
 // One output byte per lane per pass; the owner is the last start mark at or before the byte.
-template <class W>
-__device__ __forceinline__ void emit_group(const W& w, owin::Sink& O, LDSA uint8_t* mark, int ip, int op,
+template <class W, class SinkType>
+__device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t* mark, int ip, int op,
                                            int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
                                            int off, int lane) {
     const bool kmem = lane_on(keep);
@@ -349,7 +353,7 @@ __device__ __forceinline__ void emit_group(const W& w, owin::Sink& O, LDSA uint8
             src = (!is_lit && mu >= offk) ? mstart - offk + md : src;
         }
         const int pbase = op + pb;
-        const bool near = !is_lit && src >= O.ringlo && src >= pbase + LZH_WAVE - kW;
+        const bool near = !is_lit && src >= O.ringlo && src >= pbase + LZH_WAVE - SinkType::kWin;
         const bool inpass = !is_lit && src >= pbase;
         const uint32_t g = O.get(src);
         uint32_t v = is_lit ? lb : g;
@@ -627,7 +631,8 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
 // are rejected without faulting (verdicts on corrupt input are not pinned to the reference's).
 namespace zstdd {
 
-using owin::kW;
+constexpr int kZW = 2048;               // LDS output window (zstd offsets are mostly far anyway)
+typedef owin::SinkT<kZW> ZSink;
 constexpr int kErrCorrupt = -1, kErrUnsupported = -2;
 #ifndef LZH_ZSTD_DEBUG
 #define LZH_ZSTD_DEBUG 0
@@ -672,7 +677,7 @@ __device__ __forceinline__ uint32_t c_sym(Cell c) { return c >> 18; }
 
 // per-wave LDS
 struct Lds {
-    uint8_t win[kW + 2 * LZH_WAVE];     // output window | start marks (groups::emit_group)
+    uint8_t win[kZW + 2 * LZH_WAVE];     // output window | start marks (groups::emit_group)
     uint16_t huf[1 << kHufLogMax];      // Huffman decoding table: symbol | nbBits << 8
     Cell ll[512], ml[512], of[256];     // sequence FSE tables (ZSTD_seqSymbol's fields, packed)
     Cell wt[64];                       // FSE table of the Huffman weights (accuracy <= 6)
@@ -1056,7 +1061,7 @@ struct FrameState {
 };
 
 // one compressed block [bs, be) of the frame; output continues at op (returns new op, < 0 error)
-__device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout, ZWin& fw, ZWin& lw, owin::Sink& O, LDSA Lds& L,
+__device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout, ZWin& fw, ZWin& lw, ZSink& O, LDSA Lds& L,
                             FrameState& F, int bs, int be, int op, int fcs, int lane) {
     // ---- literals section (ZSTD_decodeLiteralsBlock)
     const uint32_t b0 = fbyte(fw, bs, lane);
@@ -1200,7 +1205,7 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
                     if (!lw.covers(ip, ip + glit + 16)) lw.load(ip, lane);
                     const uint64_t keep = k == LZH_WAVE ? ~0ull : ((1ull << k) - 1ull);
                     ZCLK(F, 4);
-                    groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kW, ip, op, gout, keep, (int)g_ex,
+                    groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kZW, ip, op, gout, keep, (int)g_ex,
                                        g_lit | (g_ml << 16), g_lrel, (int)g_off, lane);
                     ZCLK(F, 5);
                     op += gout;
@@ -1235,7 +1240,7 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
             if (!lw.covers(ip, ip + glit + 16)) lw.load(ip, lane);
             const uint64_t keep = k == LZH_WAVE ? ~0ull : ((1ull << k) - 1ull);
             ZCLK(F, 4);
-            groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kW, ip, op, gout, keep, (int)g_ex, g_lit | (g_ml << 16),
+            groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kZW, ip, op, gout, keep, (int)g_ex, g_lit | (g_ml << 16),
                                g_lrel, (int)g_off, lane);
             ZCLK(F, 5);
             op += gout;
@@ -1257,7 +1262,7 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
 // one frame in rin[0, cs) -> out[0, cap): returns the decoded size or an error code
 // lout: the output region for reading decoded literals back (whole dwords: its range ends at
 // the dword holding the last byte, so no load that straddles the end reads back as zero)
-__device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout, int cs, owin::Sink& O, LDSA Lds& L, int cap,
+__device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout, int cs, ZSink& O, LDSA Lds& L, int cap,
                             int lane, unsigned long long* stats) {
     ZWin fw;
     fw.bind(rin, nullptr);
@@ -1356,7 +1361,7 @@ lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, cons
         copy_raw(rin, rout, part, lane);
         r = part;
     } else {
-        owin::Sink O{(LDSA uint8_t*)L.win, rout, 0, 0};
+        zstdd::ZSink O{(LDSA uint8_t*)L.win, rout, 0, 0};
         Bytes lout;
         lout.init(out + ooff, (uint64_t)part + 3);
         r = zstdd::decode_frame(rin, lout, cs, O, L, part, lane, stats);
