@@ -38,6 +38,9 @@ constexpr int kOut = 512;             // bytes of LDS output ring per wave
 #ifndef LZH_BRFREE
 #define LZH_BRFREE 1
 #endif
+#ifndef LZH_PACKOS
+#define LZH_PACKOS 1
+#endif
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -238,6 +241,9 @@ __device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const B
     const int a0 = rdlanei((int)anc, first), a1 = rdlanei((int)anc, last) + rdlanei((int)lit, last);
     if (tot <= 4 * LZH_WAVE && R.has(a0, a1)) {
         int carry = first;
+        // offset (< 2^16) and output start (< 256 on this path) in one gathered word (packing
+        // lit | mlx << 8 as well measured 0.3 % slower)
+        const uint32_t os = LZH_PACKOS ? (off | (st << 16)) : 0u;
         for (int pass = 0; pass * LZH_WAVE < tot; pass++) {
             const int ob = pass * LZH_WAVE + lane;
             // owner of output byte ob: the last member starting at or before it.  Start marks go
@@ -256,8 +262,16 @@ __device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const B
             const int k = le ? own : carry;
             carry = rdlanei(k, 63);
             const int a = (int)lane_gather(anc, k), l = (int)lane_gather(lit, k);
-            const int o = (int)lane_gather(off, k), m = (int)lane_gather(mlx, k);
-            const int t = ob - (int)lane_gather(st, k);
+            const int m = (int)lane_gather(mlx, k);
+            int o, t;
+            if (LZH_PACKOS) {
+                const uint32_t osk = lane_gather(os, k);
+                o = (int)(osk & 0xffffu);
+                t = ob - (int)(osk >> 16);
+            } else {
+                o = (int)lane_gather(off, k);
+                t = ob - (int)lane_gather(st, k);
+            }
             const SeqLayout S(l, true, m);
             const uint32_t lb = R.byte(a + t - S.lit0);
             if (ob < tot) O.put(op + ob, S.byte(t, lb, o));
