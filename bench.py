@@ -7,18 +7,28 @@ raw-store rule), then decompress every chunk from the packed stream.  Inputs are
 HBM when the timed region starts.  value = comp+decomp MB/s (MB = 1e6 B, lzbench.cpp:104-106)
 = bytes processed by all ranks / (max over ranks of the timed wall time).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one
-process per GPU, each compresses its own 1 GiB shard of independent chunks (weak scaling,
-no data-path collective; the only cross-rank traffic is the barrier and the max-time
-reduction on the control plane).
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
+GPU, each owns a contiguous 1 GiB shard of the chunk list (weak scaling).  The only exchange is
+the host-side gather of SURVEY.md 8(e): after the timed region the ranks all-gather their packed
+totals (a few bytes, control plane), and each copies its packed slab straight into one shared
+host buffer at its chunk-order offset; that gather is timed and reported (`gather`).  No
+collective touches the data path.
 
-Also reported: the roofline of the dominant kernel (the LZ4 compress kernel, HIP events on
-the stream it runs on), and the reference CPU codec (oracle/_ref, lz4 1.9.3 built from the
-reference sources) timed on this host on a bounded sample of the same input (rank 0, N=1).
+Also reported (rank 0):
+  roofline / roofline_decompress  the codec kernels, HIP events on the stream they run on
+  bit_exact                       the whole packed stream + compr_sizes vs the reference digest
+                                  (tests/golden/fullsize.json) when the workload has one
+  cpu_baseline                    the reference codec (oracle/_ref, built from the reference
+                                  sources) on this host, 1 thread, lzbench semantics (N=1 only)
+  cpu_baseline_all_cores          the same on every host core this process may use
+  e2e                             host-to-host through the batched lzbench rows
+                                  (lzbench_hip_compress_batch / _decompress_batch) on the same
+                                  input, beside the hipMemcpy round-trip bound (PCIe; never value)
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -30,11 +40,51 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-METRIC = "comp+decomp MB/s, lz4 -b64 on 1 GiB; ratio + bit-exact vs CPU ref"
+BASELINE_METRIC = "comp+decomp MB/s, lz4 -b64 on 1 GiB; ratio + bit-exact vs CPU ref"
+COMPRESS_KERNEL = {"lz4": "lzh_lz4_compress_v2_kernel", "lz4fast": "lzh_lz4_compress_v2_kernel",
+                   "snappy": "lzh_snappy_compress_v2_kernel", "zstd": "lzh_zstd_compress_kernel"}
+DECOMPRESS_KERNEL = {"zstd": "lzh_zstd_decompress_kernel"}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def size_label(n):
+    return f"{n >> 30} GiB" if n % (1 << 30) == 0 else f"{n >> 20} MiB"
+
+
+def metric_for(codec, chunk_kib, n, corpus, level):
+    """BASELINE.json's metric string for the north-star workload; the same wording naming the
+    codec, chunk size and corpus for every other workload."""
+    if codec == "lz4" and chunk_kib == 64 and n == 1 << 30 and corpus == "text":
+        return BASELINE_METRIC
+    name = codec if codec not in ("lz4fast", "zstd") else f"{codec},{level}"
+    return f"comp+decomp MB/s, {name} -b{chunk_kib} on {size_label(n)} {corpus}; ratio + bit-exact vs CPU ref"
+
+
+def host_cpus():
+    """(threads usable by this process, description): the affinity mask capped by the cgroup CPU
+    quota (a GPU box exposes the whole machine in os.cpu_count() but grants a share of it)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(aff, quota) if quota else aff
+    return usable, {"model": model, "nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
+                    "threads_used_all_cores": usable}
 
 
 def cpu_baseline(sample: np.ndarray, codec: str, chunk: int, level: int, iters: int, threads: int):
@@ -43,7 +93,7 @@ def cpu_baseline(sample: np.ndarray, codec: str, chunk: int, level: int, iters: 
     present (kind 'reference'), else the repo's C restatement (kind 'port')."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    use_ref = O.have_ref()
+    use_ref = O.have_ref() or codec == "zstd"
     n = len(sample)
     best_c = best_d = float("inf")
     packed = cs = None
@@ -51,40 +101,151 @@ def cpu_baseline(sample: np.ndarray, codec: str, chunk: int, level: int, iters: 
         t = time.perf_counter()
         packed, cs = O.compress_chunks(sample, codec, chunk, level, use_ref=use_ref, threads=threads)
         best_c = min(best_c, time.perf_counter() - t)
+    r, out = None, None
     for _ in range(iters):
         t = time.perf_counter()
         r, out = O.decompress_chunks(packed, cs, n, codec, chunk, use_ref=use_ref, threads=threads)
         best_d = min(best_d, time.perf_counter() - t)
     ok = r == n and bool((out == sample).all())
+    lib = {"lz4": "lz4 1.9.3", "lz4fast": "lz4 1.9.3", "snappy": "snappy 1.1.8", "zstd": "zstd 1.5.2"}[codec]
     return {
         "value": round(n / (best_c + best_d) / 1e6, 2),
         "unit": "MB/s",
         "cores": max(threads, 1),
         "kind": "reference" if use_ref else "port",
-        "sample": f"first {n >> 20} MiB of the same corpus, -b{chunk >> 10}, best of {iters} compress + {iters} "
-                  f"decompress passes ({'lz4 1.9.3/snappy 1.1.8 compiled from the reference sources' if use_ref else 'oracle C restatement'})",
+        "sample": f"{size_label(n)} = the whole per-GPU input, -b{chunk >> 10}, best of {iters} compress + {iters} "
+                  f"decompress passes ({lib + ' compiled from the reference sources' if use_ref else 'oracle C restatement'}"
+                  f", {max(threads, 1)} thread{'s' if threads > 1 else ''})",
         "comp_MBps": round(n / best_c / 1e6, 2),
         "decomp_MBps": round(n / best_d / 1e6, 2),
         "roundtrip_ok": ok,
-    }, packed, cs
+    }
 
 
-def traffic_for(kernel):
+def traffic_for(kernel, workload):
     """HBM-side bytes per dispatch of `kernel` from the committed PMC profile (profiles/traffic.json,
     written by tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes on the
     same workload), or None when no profile covers this kernel/workload."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
-            k = json.load(f)["kernels"].get(kernel)
+            t = json.load(f)
+        if t.get("workload_key") != workload:
+            return None
+        k = t["kernels"].get(kernel)
         return None if k is None else int(k["traffic_bytes_per_dispatch"])
     except (OSError, KeyError, ValueError):
         return None
 
 
-def kernel_name(codec):
-    """Compressor kernel the C-ABI launches for `codec` (api.cpp lzh_compress_kernel_only)."""
-    return "lzh_snappy_compress_v2_kernel" if codec == "snappy" else "lzh_lz4_compress_v2_kernel"
+def fullsize_digest(corpus, codec, chunk, level, n, seed):
+    path = os.path.join(ROOT, "tests", "golden", "fullsize.json")
+    try:
+        for e in json.load(open(path)):
+            lvl = level if codec in ("lz4fast", "zstd") else (1 if codec == "lz4" else 0)
+            if (e["corpus"], e["codec"], e["chunk"], e["level"], e["size"], e["seed"]) == (corpus, codec, chunk, lvl, n, seed):
+                return e
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def sha(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def e2e_rows(L, host, codec, chunk, level, ngpus, iters):
+    """Host-to-host through the batched lzbench rows (what lzbench_hip -b runs): best of `iters`
+    compress_batch and decompress_batch passes, and the hipMemcpy round trip (H2D + D2H of the
+    same bytes, pinned) as the PCIe bound beside them."""
+    import torch
+    n = len(host)
+    cs = L.chunk_sizes_for(n, chunk)
+    out = np.empty(L.get_compress_bound(n) + 64, np.uint8)
+    comp = np.zeros(len(cs), np.uint64)
+    back = np.empty(n + L.PAD_SIZE, np.uint8)
+    lvl = level if codec in ("lz4fast", "zstd") else (1 if codec == "lz4" else 0)
+    lib = L.lib()
+    best_c = best_d = float("inf")
+    tot = 0
+    with L._Row(codec, chunk, lvl, ngpus) as row:
+        for _ in range(iters):
+            t = time.perf_counter()
+            tot = lib.lzbench_hip_compress_batch(host.ctypes.data, cs.ctypes.data, len(cs), out.ctypes.data, len(out),
+                                                 comp.ctypes.data, lvl, ngpus, row.wm)
+            best_c = min(best_c, time.perf_counter() - t)
+        for _ in range(iters):
+            t = time.perf_counter()
+            r = lib.lzbench_hip_decompress_batch(out.ctypes.data, comp.ctypes.data, cs.ctypes.data, len(cs),
+                                                 back.ctypes.data, len(back), lvl, ngpus, row.wm)
+            best_d = min(best_d, time.perf_counter() - t)
+    ok = tot > 0 and r == n and bool((back[:n] == host).all())
+    pin = torch.from_numpy(host).pin_memory()
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    hb = torch.empty(n, dtype=torch.uint8).pin_memory()
+    best_m = float("inf")
+    for _ in range(iters):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        dev.copy_(pin, non_blocking=True)
+        hb.copy_(dev, non_blocking=True)
+        torch.cuda.synchronize()
+        best_m = min(best_m, time.perf_counter() - t)
+    del pin, dev, hb
+    return {
+        "comp_MBps": round(n / best_c / 1e6, 2),
+        "decomp_MBps": round(n / best_d / 1e6, 2),
+        "comp+decomp_MBps": round(n / (best_c + best_d) / 1e6, 2),
+        "hipMemcpy_roundtrip_MBps": round(n / best_m / 1e6, 2),
+        "ngpus": ngpus,
+        "roundtrip_ok": ok,
+        "bytes": n,
+        "note": "host pageable buffers (page-locked once per row), H2D + kernels + D2H pipelined over "
+                "128 MiB sub-batches; best of %d passes; PCIe-bound, reported beside value, never as value" % iters,
+    }
+
+
+def gather_to_host(torch, dist, codec_obj, rank, world):
+    """SURVEY 8(e)'s single host-side gather: the ranks exchange packed totals (control plane),
+    then each copies its packed slab into one shared host buffer (/dev/shm) at its chunk-order
+    offset.  Returns {ms, bytes, GBps} (max over ranks)."""
+    import mmap
+    total = codec_obj.packed_total()
+    tt = torch.tensor([total], dtype=torch.int64)
+    alltot = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(alltot, tt)
+    sizes = [int(x.item()) for x in alltot]
+    base = sum(sizes[:rank])
+    grand = sum(sizes)
+    path = f"/dev/shm/lzh_bench_gather_{os.environ.get('MASTER_PORT', '0')}"
+    if rank == 0:
+        with open(path, "wb") as f:
+            f.truncate(grand)
+    dist.barrier()
+    fd = os.open(path, os.O_RDWR)
+    mm = mmap.mmap(fd, grand)
+    host = torch.frombuffer(mm, dtype=torch.uint8)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = time.perf_counter()
+    host[base:base + total].copy_(codec_obj.packed[:total])
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    del host
+    mm.close()
+    os.close(fd)
+    dist.barrier()
+    if rank == 0:
+        os.unlink(path)
+    ms = float(el.item()) * 1e3
+    return {"ms": round(ms, 3), "bytes": grand, "GBps": round(grand / (ms * 1e-3) / 1e9, 2),
+            "how": "all_gather of packed totals, then each rank D2H-copies its slab into one shared host buffer "
+                   "at its chunk-order offset (pageable mmap); timed after the timed region, max over ranks"}
 
 
 def main():
@@ -92,15 +253,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--codec", default="lz4", choices=["lz4", "lz4fast", "snappy"])
-    ap.add_argument("--level", type=int, default=1, help="lz4fast acceleration")
+    ap.add_argument("--codec", default="lz4", choices=["lz4", "lz4fast", "snappy", "zstd"])
+    ap.add_argument("--level", type=int, default=1, help="lz4fast acceleration / zstd level")
     ap.add_argument("--chunk-kib", type=int, default=64)
     ap.add_argument("--size-mib", type=int, default=1024, help="input bytes per GPU")
     ap.add_argument("--corpus", default="text", choices=["text", "json", "mixed", "random", "binary"])
-    ap.add_argument("--cpu-sample-mib", type=int, default=256)
-    ap.add_argument("--cpu-iters", type=int, default=3)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = 1 thread (lzbench semantics)")
+    ap.add_argument("--cpu-iters", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--backend", default="gloo", help="control-plane process group (no data-path collective)")
     args = ap.parse_args()
 
@@ -119,8 +279,9 @@ def main():
 
     n = args.size_mib << 20
     chunk = args.chunk_kib << 10
+    seed = 12345 + rank
     t = time.perf_counter()
-    host = L.datagen(args.corpus, n, seed=12345 + rank)
+    host = L.datagen(args.corpus, n, seed=seed)
     log(f"[rank {rank}] generated {n >> 20} MiB {args.corpus} in {time.perf_counter() - t:.1f}s")
     d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda")
     d_in[:n].copy_(torch.from_numpy(host))
@@ -167,31 +328,45 @@ def main():
     roundtrip_ok = bool(torch.equal(codec.out[:n], d_in[:n])) and bool((codec.status >= 0).all().item())
     ratio = comp_total / n
 
-    # bit-exactness vs the CPU reference on a sample: the packed prefix of the first m chunks
-    # must equal the reference chunk loop's output for those chunks, sizes included
     result_extra = {}
+    if dist:
+        result_extra["gather"] = gather_to_host(torch, dist, codec, rank, world)
+
+    # bit-exactness of the WHOLE output vs the reference chunk loop's digest
+    dig = fullsize_digest(args.corpus, args.codec, chunk, args.level, n, seed)
+    if rank == 0:
+        if dig is not None:
+            cs64 = codec.csizes.cpu().numpy().astype("<u8")
+            result_extra["bit_exact"] = bool(comp_total == dig["packed_bytes"] and sha(cs64) == dig["csizes_sha256"]
+                                             and sha(codec.packed[:comp_total].cpu().numpy()) == dig["packed_sha256"])
+            result_extra["bit_exact_bytes"] = n
+            result_extra["bit_exact_against"] = "tests/golden/fullsize.json (reference chunk loop, oracle/_ref)"
+        else:
+            result_extra["bit_exact"] = None
+            result_extra["bit_exact_against"] = "no committed reference digest for this workload"
+
     cpu = None
+    usable, cpuinfo = host_cpus()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        m = min(args.cpu_sample_mib << 20, n) // chunk * chunk or n
-        sample = host[:m]
-        cpu, ref_packed, ref_cs = cpu_baseline(sample, args.codec, chunk, args.level, args.cpu_iters,
-                                               args.cpu_threads)
-        if args.cpu_threads == 0:
-            cpu_mt, _, _ = cpu_baseline(sample, args.codec, chunk, args.level, 1, min(16, os.cpu_count() or 1))
-            result_extra["cpu_baseline_all_cores"] = cpu_mt
-        gcs = codec.csizes[: len(ref_cs)].cpu().numpy().astype(np.uint64)
-        gpk = codec.packed[: len(ref_packed)].cpu().numpy()
-        result_extra["bit_exact_sample"] = bool((gcs == ref_cs).all() and (gpk == ref_packed).all())
-        result_extra["bit_exact_sample_bytes"] = int(m)
+        cpu = cpu_baseline(host, args.codec, chunk, args.level, args.cpu_iters, 0)
+        result_extra["cpu_baseline_all_cores"] = cpu_baseline(host, args.codec, chunk, args.level, args.cpu_iters,
+                                                              usable)
+    result_extra["host_cpu"] = cpuinfo
+    if rank == 0 and world == 1 and not args.no_e2e and args.codec != "zstd":
+        del d_in
+        torch.cuda.empty_cache()
+        result_extra["e2e"] = e2e_rows(L, host, args.codec, chunk, args.level, 1, 3)
 
     algo_bytes = n + comp_total                      # compress reads N, writes C
     achieved = algo_bytes / (k_ms * 1e-3) / 1e9
     dec_achieved = algo_bytes / (d_ms * 1e-3) / 1e9   # decompress reads C, writes N
-    default_workload = args.codec == "lz4" and args.chunk_kib == 64 and args.corpus == "text" and args.size_mib == 1024
+    wkey = f"{args.codec}/{args.level}/{args.chunk_kib}/{args.corpus}/{n}"
     total_bytes = world * n * args.steps
     value = total_bytes / elapsed / 1e6
+    kname = COMPRESS_KERNEL[args.codec]
+    dname = DECOMPRESS_KERNEL.get(args.codec, "lzh_decompress_v2_kernel")
     res = {
-        "metric": METRIC,
+        "metric": metric_for(args.codec, args.chunk_kib, n, args.corpus, args.level),
         "value": round(value, 2),
         "unit": "MB/s",
         "n_gpus": world,
@@ -203,14 +378,15 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": f"synthetic {args.corpus} corpus (SURVEY.md 8(d) stand-in; enwik8/Silesia unavailable offline), "
-                f"generated per rank, resident in HBM",
+                f"generated per rank (seed 12345 + rank), resident in HBM",
         "config": {
-            "workload": f"{args.codec} -b{args.chunk_kib} on {n >> 20} MiB {args.corpus} per GPU, comp+decomp pass",
+            "workload": f"{args.codec}{',' + str(args.level) if args.codec in ('lz4fast', 'zstd') else ''} "
+                        f"-b{args.chunk_kib} on {size_label(n)} {args.corpus} per GPU, comp+decomp pass",
             "codec": args.codec,
             "chunk_kib": args.chunk_kib,
             "bytes_per_gpu": n,
             "chunks_per_gpu": int(codec.k),
-            "parallelism": f"chunk-sharded x{world} (independent shards, no collective)",
+            "parallelism": f"chunk-sharded x{world} (contiguous shard per GPU, host-side gather, no collective)",
         },
         "roofline": {
             "bound": "hbm",
@@ -218,9 +394,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic_for(kernel_name(args.codec)) if default_workload else None,
-            "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE + WRITE_SIZE, raw KiB x 1024, per launch)",
-            "kernel": kernel_name(args.codec),
+            "traffic": traffic_for(kname, wkey),
+            "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE + WRITE_SIZE, separate passes, per launch)",
+            "kernel": kname,
             "kernel_ms": round(k_ms, 3),
             "algorithmic_bytes_per_launch": int(algo_bytes),
         },
@@ -230,8 +406,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(dec_achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic_for("lzh_decompress_v2_kernel") if default_workload else None,
-            "kernel": "lzh_decompress_v2_kernel",
+            "traffic": traffic_for(dname, wkey),
+            "kernel": dname,
             "kernel_ms": round(d_ms, 3),
         },
         "cpu_baseline": cpu,

@@ -112,6 +112,7 @@ int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t 
         return LZH_OK;
     }
     if (temp_bytes < lzh_compress_temp_bytes(codec, n, chunk_size) || !d_temp) return LZH_ESPACE;
+    if (packed_cap < lzh_max_packed_bytes(codec, n, chunk_size)) return LZH_ESPACE;
     int rc = lzh_compress_kernel_only(codec, level, d_in, n, in_readable, chunk_size, d_temp, d_csizes, hip_stream);
     if (rc) return rc;
     return lzh_compress_finish_async(codec, d_in, n, in_readable, chunk_size, d_temp, d_csizes, d_packed, packed_cap,
@@ -124,6 +125,8 @@ int lzh_compress_finish_async(int codec, const void* d_in, size_t n, size_t in_r
     hipStream_t s = (hipStream_t)hip_stream;
     if (!chunk_size || !d_stage || !d_csizes || !d_packed || !d_offsets) return LZH_EARG;
     if (codec != LZH_CODEC_LZ4 && codec != LZH_CODEC_SNAPPY) return LZH_EARG;
+    // the sizes are only known on the device: the worst case must fit (no silent truncation)
+    if (packed_cap < lzh_max_packed_bytes(codec, n, chunk_size)) return LZH_ESPACE;
     const size_t k = lzh_num_chunks(n, chunk_size);
     const size_t stride = lzh_stage_stride(codec, chunk_size);
     LZH_CHECK(lzh_launch_scan(d_csizes, k, d_offsets, nullptr, s));
@@ -171,11 +174,19 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
         size_t want = align_up(bytes + 4096, 1 << 20);
-        if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return -1; }
+        if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; (void)hipGetLastError(); return -1; }
         cap = want;
         return 0;
     }
     void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+// the calling thread's current device is restored on every exit path of a row function
+// (lzbench's process -- or a torch rank -- keeps allocating on the device it selected)
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() { if (hipGetDevice(&prev) != hipSuccess) prev = -1; }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
 struct Dev {
@@ -204,7 +215,7 @@ struct LzhCtx {
     uint32_t magic = 0x4c5a4858;  // "LZHX"
     int codec = 0;
     size_t chunk_size = 0;
-    std::vector<Dev> devs;
+    std::vector<Dev> devs;        // logical shards (may outnumber the physical devices)
     std::vector<HostReg> regs;    // host ranges page-locked by this row (lzbench reuses its buffers)
 };
 
@@ -225,27 +236,49 @@ void ensure_pinned(LzhCtx* c, const void* p, size_t n) {
     else (void)hipGetLastError();
 }
 
+void ctx_free(LzhCtx* c) {
+    DeviceGuard guard;
+    for (Dev& d : c->devs) {
+        (void)hipSetDevice(d.id);
+        d.in.release(); d.packed.release(); d.temp.release(); d.temp2.release(); d.csizes.release(); d.offsets.release();
+        d.status.release();
+        if (d.h_cs) (void)hipHostFree(d.h_cs);
+        if (d.s) (void)hipStreamDestroy(d.s);
+        if (d.s2) (void)hipStreamDestroy(d.s2);
+        if (d.sin) (void)hipStreamDestroy(d.sin);
+        if (d.sout) (void)hipStreamDestroy(d.sout);
+    }
+    for (const HostReg& r : c->regs) (void)hipHostUnregister(r.p);
+    c->magic = 0;
+    delete c;
+}
+
+// ngpus logical shards (lzbench's additional_param of the row) starting at the caller's current
+// device; shard g runs on device (current + g) mod count, so ngpus larger than the visible device
+// count is legal (several shards share a device on their own streams; results are identical)
 char* ctx_new(int codec, size_t chunk_size, size_t ngpus) {
+    DeviceGuard guard;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
         fprintf(stderr, "lzbench_hip: no HIP device available\n");
         return nullptr;
     }
     if (ngpus == 0) ngpus = 1;
-    if ((int)ngpus > count) ngpus = (size_t)count;
+    if (ngpus > 64) ngpus = 64;
+    const int base = guard.prev >= 0 ? guard.prev : 0;
     LzhCtx* c = new LzhCtx();
     c->codec = codec;
     c->chunk_size = chunk_size;
     c->devs.resize(ngpus);
     for (size_t g = 0; g < ngpus; g++) {
         Dev& d = c->devs[g];
-        d.id = (int)g;
-        if (hipSetDevice((int)g) != hipSuccess || hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking) != hipSuccess ||
+        d.id = (int)((base + g) % (size_t)count);
+        if (hipSetDevice(d.id) != hipSuccess || hipStreamCreateWithFlags(&d.s, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&d.s2, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&d.sin, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&d.sout, hipStreamNonBlocking) != hipSuccess) {
-            fprintf(stderr, "lzbench_hip: cannot open device %zu\n", g);
-            delete c;
+            fprintf(stderr, "lzbench_hip: cannot open device %d\n", d.id);
+            ctx_free(c);
             return nullptr;
         }
     }
@@ -253,10 +286,13 @@ char* ctx_new(int codec, size_t chunk_size, size_t ngpus) {
 }
 
 // chunks per pipelined sub-batch: ~128 MiB of input and at least 1 024 chunks (a full grid round
-// of the widest-LDS kernel); consecutive sub-batches alternate between two kernel streams so a
-// grid's tail overlaps the next grid
-size_t sub_batch_chunks(size_t chunk) {
-    return std::max<size_t>(1024, ((size_t)128 << 20) / std::max<size_t>(chunk, 1));
+// of the widest-LDS kernel); consecutive sub-batches of a device alternate between two kernel
+// streams so a grid's tail overlaps the next grid.  With several shards the sub-batch shrinks
+// until every shard owns at least two.
+size_t sub_batch_chunks(size_t chunk, size_t k, size_t G) {
+    size_t sbk = std::max<size_t>(1024, ((size_t)128 << 20) / std::max<size_t>(chunk, 1));
+    if (G > 1) sbk = std::min(sbk, std::max<size_t>(1, (k + 2 * G - 1) / (2 * G)));
+    return sbk;
 }
 
 struct Events {
@@ -272,68 +308,94 @@ struct Events {
     ~Events() { for (hipEvent_t e : ev) (void)hipEventDestroy(e); }
 };
 
+// Sharding plan of one run (k chunks of `chunk` bytes covering n bytes): sub-batch j = chunks
+// [j*sbk, min(k, (j+1)*sbk)) goes to shard j mod G as that shard's local slot j / G.  Every
+// shard owns a contiguous set of index ranges, and the sub-batches finish roughly in index order
+// across all shards, so the host gather (which must place sub-batch j after everything before
+// it, lzbench.cpp:266-298 packing) can copy each one out as soon as its sizes land instead of
+// waiting for whole shards in shard order.
+struct Plan {
+    size_t k, sbk, nsb, G;
+    size_t chunk, n;
+    size_t c_begin(size_t j) const { return j * sbk; }
+    size_t c_count(size_t j) const { return std::min(sbk, k - j * sbk); }
+    size_t b_begin(size_t j) const { return j * sbk * chunk; }
+    size_t b_count(size_t j) const { return std::min(n, (j * sbk + c_count(j)) * chunk) - b_begin(j); }
+    size_t shard(size_t j) const { return j % G; }
+    size_t slot(size_t j) const { return j / G; }
+    size_t slots(size_t g) const { return nsb > g ? (nsb - g + G - 1) / G : 0; }
+};
+
+Plan make_plan(size_t ndev, size_t n, size_t chunk) {
+    Plan p;
+    p.n = n;
+    p.chunk = chunk;
+    p.k = lzh_num_chunks(n, chunk);
+    p.G = std::max<size_t>(1, std::min(ndev, p.k));
+    p.sbk = sub_batch_chunks(chunk, p.k, p.G);
+    p.nsb = (p.k + p.sbk - 1) / p.sbk;
+    p.G = std::min(p.G, p.nsb);
+    return p;
+}
+
 // process one run: chunks [0, k) of uniform size `chunk` (last ragged) covering n bytes of
-// host input; results appended at out (capacity outcap). Returns packed bytes or < 0.
-// Each GPU takes a contiguous chunk range; within it, sub-batches are pipelined over three
-// streams (host->device copy | compress + scan + pack | device->host copy), and the packed
-// sub-batches are gathered to `out` in chunk order as their sizes come back.
+// host input; results appended at out (capacity outcap). Returns packed bytes, 0 when the
+// packed output does not fit outcap, < 0 on error.  Per shard, sub-batches are pipelined over
+// three streams (host->device copy | compress + scan + pack | device->host copy).
 int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t chunk, uint8_t* out, size_t outcap,
                      size_t* compr_sizes) {
-    const size_t k = lzh_num_chunks(n, chunk);
-    const size_t G = std::min(c->devs.size(), k);
-    const size_t sbk = sub_batch_chunks(chunk);
-    std::vector<size_t> c0(G + 1);
-    for (size_t g = 0; g <= G; g++) c0[g] = k * g / G;
+    DeviceGuard guard;
+    const Plan P = make_plan(c->devs.size(), n, chunk);
+    const size_t sb_in = std::min(n, P.sbk * chunk);                   // largest sub-batch input
+    const size_t sb_packed = align_up(lzh_max_packed_bytes(c->codec, sb_in, chunk) + 64, 256);
+    const size_t sb_temp = lzh_compress_temp_bytes(c->codec, sb_in, chunk);
     ensure_pinned(c, in, n);
     ensure_pinned(c, out, outcap);
-    std::vector<Events> evin(G), evk(G);
-    const size_t sb_packed = align_up(lzh_max_packed_bytes(c->codec, sbk * chunk, chunk) + 64, 256);
-    for (size_t g = 0; g < G; g++) {
+    for (size_t g = 0; g < P.G; g++) {
         Dev& d = c->devs[g];
+        const size_t m = P.slots(g);
         if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
-        const size_t off = c0[g] * chunk, nn = std::min(n, c0[g + 1] * chunk) - off, kk = c0[g + 1] - c0[g];
-        const size_t nsub = (kk + sbk - 1) / sbk;
-        if (d.in.ensure(nn + 64) || d.packed.ensure(nsub * sb_packed) ||
-            d.temp.ensure(lzh_compress_temp_bytes(c->codec, std::min(nn, sbk * chunk), chunk)) ||
-            (nsub > 1 && d.temp2.ensure(lzh_compress_temp_bytes(c->codec, std::min(nn, sbk * chunk), chunk))) ||
-            d.csizes.ensure(kk * 4 + 64) || d.offsets.ensure((kk + nsub) * 8 + 64) || d.ensure_host(kk))
+        if (d.in.ensure(m * sb_in + 64) || d.packed.ensure(m * sb_packed) || d.temp.ensure(sb_temp) ||
+            (m > 1 && d.temp2.ensure(sb_temp)) || d.csizes.ensure(m * P.sbk * 4 + 64) ||
+            d.offsets.ensure(m * (P.sbk + 1) * 8 + 64) || d.ensure_host(m * P.sbk))
             return LZH_ESPACE;
-        for (size_t i = 0; i < nsub; i++) {
-            const size_t ci = i * sbk, ck = std::min(sbk, kk - ci);
-            const size_t ro = ci * chunk, rn = std::min(nn, (ci + ck) * chunk) - ro;
-            hipEvent_t e_in = evin[g].get(i), e_k = evk[g].get(i);
-            if (!e_in || !e_k) return LZH_EHIP;
-            LZH_CHECK(hipMemcpyAsync((uint8_t*)d.in.p + ro, in + off + ro, rn, hipMemcpyHostToDevice, d.sin));
-            LZH_CHECK(hipEventRecord(e_in, d.sin));
-            hipStream_t ks = (i & 1) ? d.s2 : d.s;
-            DevBuf& tb = (i & 1) ? d.temp2 : d.temp;
-            LZH_CHECK(hipStreamWaitEvent(ks, e_in, 0));
-            int rc = lzh_compress_async(c->codec, level, (uint8_t*)d.in.p + ro, rn, rn + 64, chunk,
-                                        (uint8_t*)d.packed.p + i * sb_packed, sb_packed, (uint32_t*)d.csizes.p + ci,
-                                        (uint64_t*)d.offsets.p + ci + i, tb.p, tb.cap, ks);
-            if (rc) return rc;
-            LZH_CHECK(hipMemcpyAsync(d.h_cs + ci, (uint32_t*)d.csizes.p + ci, ck * 4, hipMemcpyDeviceToHost, ks));
-            LZH_CHECK(hipEventRecord(e_k, ks));
-        }
+    }
+    Events evin, evk;
+    for (size_t j = 0; j < P.nsb; j++) {     // issue every sub-batch, round-robin over the shards
+        Dev& d = c->devs[P.shard(j)];
+        const size_t l = P.slot(j), ck = P.c_count(j), rn = P.b_count(j);
+        if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
+        hipEvent_t e_in = evin.get(j), e_k = evk.get(j);
+        if (!e_in || !e_k) return LZH_EHIP;
+        uint8_t* din = (uint8_t*)d.in.p + l * sb_in;
+        LZH_CHECK(hipMemcpyAsync(din, in + P.b_begin(j), rn, hipMemcpyHostToDevice, d.sin));
+        hipStream_t ks = (l & 1) ? d.s2 : d.s;
+        DevBuf& tb = (l & 1) ? d.temp2 : d.temp;
+        LZH_CHECK(hipEventRecord(e_in, d.sin));
+        LZH_CHECK(hipStreamWaitEvent(ks, e_in, 0));
+        uint32_t* dcs = (uint32_t*)d.csizes.p + l * P.sbk;
+        int rc = lzh_compress_async(c->codec, level, din, rn, rn + 64, chunk, (uint8_t*)d.packed.p + l * sb_packed,
+                                    sb_packed, dcs, (uint64_t*)d.offsets.p + l * (P.sbk + 1), tb.p, tb.cap, ks);
+        if (rc) return rc;
+        LZH_CHECK(hipMemcpyAsync(d.h_cs + l * P.sbk, dcs, ck * 4, hipMemcpyDeviceToHost, ks));
+        LZH_CHECK(hipEventRecord(e_k, ks));
     }
     size_t base = 0;
     bool fits = true;
-    for (size_t g = 0; g < G; g++) {   // host-side gather in chunk order
-        Dev& d = c->devs[g];
+    for (size_t j = 0; j < P.nsb; j++) {     // host-side gather in chunk order
+        Dev& d = c->devs[P.shard(j)];
+        const size_t l = P.slot(j), ck = P.c_count(j), c0 = P.c_begin(j);
         if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
-        const size_t kk = c0[g + 1] - c0[g], nsub = (kk + sbk - 1) / sbk;
-        for (size_t i = 0; i < nsub; i++) {
-            const size_t ci = i * sbk, ck = std::min(sbk, kk - ci);
-            LZH_CHECK(hipEventSynchronize(evk[g].get(i)));
-            size_t tot = 0;
-            for (size_t j = 0; j < ck; j++) { compr_sizes[c0[g] + ci + j] = d.h_cs[ci + j]; tot += d.h_cs[ci + j]; }
-            if (!fits || base + tot > outcap) { fits = false; continue; }   // lzbench: cannot store
-            LZH_CHECK(hipStreamWaitEvent(d.sout, evk[g].get(i), 0));
-            LZH_CHECK(hipMemcpyAsync(out + base, (uint8_t*)d.packed.p + i * sb_packed, tot, hipMemcpyDeviceToHost, d.sout));
-            base += tot;
-        }
+        LZH_CHECK(hipEventSynchronize(evk.get(j)));
+        size_t tot = 0;
+        const uint32_t* hs = d.h_cs + l * P.sbk;
+        for (size_t i = 0; i < ck; i++) { compr_sizes[c0 + i] = hs[i]; tot += hs[i]; }
+        if (!fits || base + tot > outcap) { fits = false; continue; }   // lzbench: cannot store
+        LZH_CHECK(hipStreamWaitEvent(d.sout, evk.get(j), 0));
+        LZH_CHECK(hipMemcpyAsync(out + base, (uint8_t*)d.packed.p + l * sb_packed, tot, hipMemcpyDeviceToHost, d.sout));
+        base += tot;
     }
-    for (size_t g = 0; g < G; g++) {
+    for (size_t g = 0; g < P.G; g++) {
         if (hipSetDevice(c->devs[g].id) != hipSuccess || hipStreamSynchronize(c->devs[g].sout) != hipSuccess ||
             hipStreamSynchronize(c->devs[g].s) != hipSuccess || hipStreamSynchronize(c->devs[g].s2) != hipSuccess)
             return LZH_EHIP;
@@ -341,65 +403,75 @@ int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t c
     return fits ? (int64_t)base : 0;
 }
 
+// Inverse of run_compress over the same plan.  Returns the decoded byte count (== n) or < 0:
+// a chunk whose decoder reports anything but its own size is malformed (LZH_ECORRUPT), which
+// keeps lzbench's length check (lzbench.cpp:433-437) honest for short decodes.
 int64_t run_decompress(LzhCtx* c, const uint8_t* in, const size_t* compr_sizes, size_t n, size_t chunk, uint8_t* out) {
-    const size_t k = lzh_num_chunks(n, chunk);
-    const size_t G = std::min(c->devs.size(), k);
-    const size_t sbk = sub_batch_chunks(chunk);
-    std::vector<size_t> c0(G + 1);
-    for (size_t g = 0; g <= G; g++) c0[g] = k * g / G;
+    DeviceGuard guard;
+    const Plan P = make_plan(c->devs.size(), n, chunk);
+    const size_t k = P.k;
     std::vector<size_t> coff(k + 1, 0);
     for (size_t i = 0; i < k; i++) coff[i + 1] = coff[i] + compr_sizes[i];
+    size_t sb_cin = 0;                        // largest compressed sub-batch
+    for (size_t j = 0; j < P.nsb; j++)
+        sb_cin = std::max(sb_cin, coff[P.c_begin(j) + P.c_count(j)] - coff[P.c_begin(j)]);
+    sb_cin = align_up(sb_cin + 64, 256);
+    const size_t sb_out = std::min(n, P.sbk * chunk);
+    const size_t sb_temp = lzh_decompress_temp_bytes(c->codec, sb_out, chunk);
     ensure_pinned(c, in, coff[k]);
     ensure_pinned(c, out, n);
-    std::vector<Events> evin(G), evk(G);
-    for (size_t g = 0; g < G; g++) {
+    for (size_t g = 0; g < P.G; g++) {
         Dev& d = c->devs[g];
+        const size_t m = P.slots(g);
         if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
-        const size_t kk = c0[g + 1] - c0[g], nsub = (kk + sbk - 1) / sbk;
-        const size_t off = c0[g] * chunk, nn = std::min(n, c0[g + 1] * chunk) - off;
-        const size_t pin = coff[c0[g + 1]] - coff[c0[g]];
-        if (d.in.ensure(pin + 64) || d.packed.ensure(nn + 64) || d.csizes.ensure(kk * 4 + 64) ||
-            d.status.ensure(kk * 4 + 64) ||
-            d.temp.ensure(lzh_decompress_temp_bytes(c->codec, std::min(nn, sbk * chunk), chunk)) ||
-            d.temp2.ensure(lzh_decompress_temp_bytes(c->codec, std::min(nn, sbk * chunk), chunk)) ||
-            d.ensure_host(2 * kk))
+        if (d.in.ensure(m * sb_cin) || d.packed.ensure(m * sb_out + 64) || d.csizes.ensure(m * P.sbk * 4 + 64) ||
+            d.status.ensure(m * P.sbk * 4 + 64) || d.temp.ensure(sb_temp) || d.temp2.ensure(sb_temp) ||
+            d.ensure_host(2 * m * P.sbk))
             return LZH_ESPACE;
-        uint32_t* h_in = d.h_cs;          // sizes in
-        int32_t* h_st = (int32_t*)d.h_cs + kk;   // statuses out
-        for (size_t i = 0; i < kk; i++) h_in[i] = (uint32_t)compr_sizes[c0[g] + i];
-        for (size_t i = 0; i < nsub; i++) {
-            const size_t ci = i * sbk, ck = std::min(sbk, kk - ci);
-            const size_t ro = ci * chunk, rn = std::min(nn, (ci + ck) * chunk) - ro;
-            const size_t po = coff[c0[g] + ci] - coff[c0[g]], pn = coff[c0[g] + ci + ck] - coff[c0[g] + ci];
-            hipEvent_t e_in = evin[g].get(i), e_k = evk[g].get(i);
-            if (!e_in || !e_k) return LZH_EHIP;
-            LZH_CHECK(hipMemcpyAsync((uint8_t*)d.in.p + po, in + coff[c0[g]] + po, pn, hipMemcpyHostToDevice, d.sin));
-            LZH_CHECK(hipMemcpyAsync((uint32_t*)d.csizes.p + ci, h_in + ci, ck * 4, hipMemcpyHostToDevice, d.sin));
-            LZH_CHECK(hipEventRecord(e_in, d.sin));
-            hipStream_t ks = (i & 1) ? d.s2 : d.s;
-            DevBuf& tb = (i & 1) ? d.temp2 : d.temp;
-            LZH_CHECK(hipStreamWaitEvent(ks, e_in, 0));
-            int rc = lzh_decompress_async(c->codec, (uint8_t*)d.in.p + po, pn + 64, (const uint32_t*)d.csizes.p + ci,
-                                          nullptr, rn, chunk, (uint8_t*)d.packed.p + ro, (int32_t*)d.status.p + ci,
-                                          tb.p, tb.cap, ks);
-            if (rc) return rc;
-            LZH_CHECK(hipEventRecord(e_k, ks));
-            LZH_CHECK(hipStreamWaitEvent(d.sout, e_k, 0));
-            LZH_CHECK(hipMemcpyAsync(h_st + ci, (int32_t*)d.status.p + ci, ck * 4, hipMemcpyDeviceToHost, d.sout));
-            LZH_CHECK(hipMemcpyAsync(out + off + ro, (uint8_t*)d.packed.p + ro, rn, hipMemcpyDeviceToHost, d.sout));
-        }
     }
-    int64_t sum = 0;
-    bool bad = false;
-    for (size_t g = 0; g < G; g++) {
+    Events evin, evk;
+    for (size_t j = 0; j < P.nsb; j++) {
+        Dev& d = c->devs[P.shard(j)];
+        const size_t l = P.slot(j), m = P.slots(P.shard(j)), ck = P.c_count(j), c0 = P.c_begin(j);
+        const size_t rn = P.b_count(j), po = coff[c0], pn = coff[c0 + ck] - po;
+        if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
+        hipEvent_t e_in = evin.get(j), e_k = evk.get(j);
+        if (!e_in || !e_k) return LZH_EHIP;
+        uint32_t* h_in = d.h_cs + l * P.sbk;                  // sizes in
+        for (size_t i = 0; i < ck; i++) h_in[i] = (uint32_t)compr_sizes[c0 + i];
+        uint8_t* din = (uint8_t*)d.in.p + l * sb_cin;
+        uint32_t* dcs = (uint32_t*)d.csizes.p + l * P.sbk;
+        int32_t* dst = (int32_t*)d.status.p + l * P.sbk;
+        uint8_t* dout = (uint8_t*)d.packed.p + l * sb_out;
+        LZH_CHECK(hipMemcpyAsync(din, in + po, pn, hipMemcpyHostToDevice, d.sin));
+        LZH_CHECK(hipMemcpyAsync(dcs, h_in, ck * 4, hipMemcpyHostToDevice, d.sin));
+        LZH_CHECK(hipEventRecord(e_in, d.sin));
+        hipStream_t ks = (l & 1) ? d.s2 : d.s;
+        DevBuf& tb = (l & 1) ? d.temp2 : d.temp;
+        LZH_CHECK(hipStreamWaitEvent(ks, e_in, 0));
+        int rc = lzh_decompress_async(c->codec, din, pn + 64, dcs, nullptr, rn, chunk, dout, dst, tb.p, tb.cap, ks);
+        if (rc) return rc;
+        LZH_CHECK(hipEventRecord(e_k, ks));
+        LZH_CHECK(hipStreamWaitEvent(d.sout, e_k, 0));
+        int32_t* h_st = (int32_t*)d.h_cs + m * P.sbk + l * P.sbk;   // statuses out
+        LZH_CHECK(hipMemcpyAsync(h_st, dst, ck * 4, hipMemcpyDeviceToHost, d.sout));
+        LZH_CHECK(hipMemcpyAsync(out + P.b_begin(j), dout, rn, hipMemcpyDeviceToHost, d.sout));
+    }
+    for (size_t g = 0; g < P.G; g++) {
         Dev& d = c->devs[g];
         if (hipSetDevice(d.id) != hipSuccess || hipStreamSynchronize(d.sout) != hipSuccess ||
             hipStreamSynchronize(d.s) != hipSuccess || hipStreamSynchronize(d.s2) != hipSuccess)
             return LZH_EHIP;
-        const size_t kk = c0[g + 1] - c0[g];
-        const int32_t* h_st = (const int32_t*)d.h_cs + kk;
-        for (size_t i = 0; i < kk; i++) {
-            if (h_st[i] < 0) bad = true;
+    }
+    int64_t sum = 0;
+    bool bad = false;
+    for (size_t j = 0; j < P.nsb; j++) {
+        const Dev& d = c->devs[P.shard(j)];
+        const size_t l = P.slot(j), m = P.slots(P.shard(j)), ck = P.c_count(j), c0 = P.c_begin(j);
+        const int32_t* h_st = (const int32_t*)d.h_cs + m * P.sbk + l * P.sbk;
+        for (size_t i = 0; i < ck; i++) {
+            const int64_t part = (int64_t)std::min(chunk, n - (c0 + i) * chunk);
+            if (h_st[i] != part) bad = true;
             sum += h_st[i];
         }
     }
@@ -420,8 +492,7 @@ int64_t one_chunk_decompress(int codec_expect, char* in, size_t insize, char* ou
     if (!c || c->codec != codec_expect) return 0;
     size_t cs = insize;
     const size_t chunk = std::max<size_t>(outsize, 1);
-    int64_t r = run_decompress(c, (const uint8_t*)in, &cs, outsize, chunk, (uint8_t*)out);
-    return r < 0 ? r : (int64_t)outsize;
+    return run_decompress(c, (const uint8_t*)in, &cs, outsize, chunk, (uint8_t*)out);
 }
 
 }  // namespace
@@ -434,20 +505,7 @@ char* lzbench_hip_memcpy_init(size_t chunk_size, size_t level, size_t ngpus) { (
 
 void lzbench_hip_deinit(char* wm) {
     LzhCtx* c = ctx_of(wm);
-    if (!c) return;
-    for (Dev& d : c->devs) {
-        (void)hipSetDevice(d.id);
-        d.in.release(); d.packed.release(); d.temp.release(); d.temp2.release(); d.csizes.release(); d.offsets.release();
-        d.status.release();
-        if (d.h_cs) (void)hipHostFree(d.h_cs);
-        if (d.s) (void)hipStreamDestroy(d.s);
-        if (d.s2) (void)hipStreamDestroy(d.s2);
-        if (d.sin) (void)hipStreamDestroy(d.sin);
-        if (d.sout) (void)hipStreamDestroy(d.sout);
-    }
-    for (const HostReg& r : c->regs) (void)hipHostUnregister(r.p);
-    c->magic = 0;
-    delete c;
+    if (c) ctx_free(c);
 }
 
 int64_t lzbench_hip_lz4_compress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
@@ -468,6 +526,7 @@ int64_t lzbench_hip_snappy_decompress(char* in, size_t insize, char* out, size_t
 int64_t lzbench_hip_memcpy(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
     LzhCtx* c = ctx_of(wm);
     if (!c || outsize < insize) return 0;
+    DeviceGuard guard;
     Dev& d = c->devs[0];
     if (hipSetDevice(d.id) != hipSuccess || d.in.ensure(insize + 64)) return 0;
     ensure_pinned(c, in, insize);

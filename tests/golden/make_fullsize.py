@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""tests/golden/make_fullsize.py -- sha256 digests of the REFERENCE chunk loop at BASELINE.json's
+full sizes (1 GiB per GPU), so the GPU output of the bench workloads is compared whole, byte for
+byte, not by sampled chunks.
+
+Run in the build container (needs oracle/_ref/libref.so: lz4 1.9.3 / snappy 1.1.8 / zstd 1.5.2
+compiled from /root/reference by `make -C oracle ref`).  Inputs are regenerated deterministically
+by lzbench_amd.datagen (seed 12345 = bench.py's rank-0 input), so only digests are stored.
+
+Writes fullsize.json: [{corpus, size, seed, codec, chunk, level, input_sha256, packed_sha256,
+csizes_sha256, packed_bytes}], csizes hashed as little-endian u64 (lzbench's size_t array).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(HERE))
+
+import lzbench_amd as L          # noqa: E402  (datagen only)
+import oracle_lib as O           # noqa: E402
+
+# (corpus, codec, chunk, level): the north star, config 3 at 1 GiB, config 4's per-GPU share,
+# config 5's codec at its chunk size on a 1 GiB per-GPU share
+WORKLOADS = [
+    ("text", "lz4", 65536, 1),
+    ("mixed", "snappy", 262144, 0),
+    ("json", "lz4", 65536, 1),
+    ("json", "snappy", 65536, 0),
+    ("mixed", "zstd", 131072, 1),
+]
+SIZE = 1 << 30
+SEED = 12345
+
+
+def sha(*arrays) -> str:
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def main():
+    if not O.have_ref():
+        sys.exit("oracle/_ref/libref.so missing: run `make -C oracle ref` (needs /root/reference)")
+    only = set(sys.argv[1:])
+    path = os.path.join(HERE, "fullsize.json")
+    out = json.load(open(path)) if os.path.exists(path) else []
+    have = {(e["corpus"], e["codec"], e["chunk"], e["level"]) for e in out}
+    datas = {}
+    for corpus, codec, chunk, level in WORKLOADS:
+        if (corpus, codec, chunk, level) in have or (only and codec not in only):
+            continue
+        if corpus not in datas:
+            datas = {corpus: L.datagen(corpus, SIZE, seed=SEED)}
+        data = datas[corpus]
+        packed, cs = O.compress_chunks(data, codec, chunk, level, use_ref=True, threads=8)
+        e = {"corpus": corpus, "size": SIZE, "seed": SEED, "codec": codec, "chunk": chunk, "level": level,
+             "input_sha256": sha(data), "packed_sha256": sha(packed), "csizes_sha256": sha(cs.astype("<u8")),
+             "packed_bytes": int(len(packed)), "ratio_pct": round(100 * len(packed) / SIZE, 3)}
+        print(e, flush=True)
+        out.append(e)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

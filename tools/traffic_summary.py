@@ -17,5 +17,6 @@ for f in glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"), recu
             res[kern][name + "_bytes_per_dispatch"] = v / max(1, len(d[(kern, name)])) * 1024.0
 for k, v in res.items():
     v["traffic_bytes_per_dispatch"] = v.get("FETCH_SIZE_bytes_per_dispatch", 0.0) + v.get("WRITE_SIZE_bytes_per_dispatch", 0.0)
-json.dump({"workload": "lz4 -b64, 1 GiB synthetic text, tools/prof_kernels.py", "kernels": res}, open(os.path.join(out, "traffic.json"), "w"), indent=1)
+wkey = sys.argv[2] if len(sys.argv) > 2 else "lz4/1/64/text/1073741824"   # bench.py's workload key
+json.dump({"workload": "tools/prof_kernels.py " + wkey, "workload_key": wkey, "kernels": res}, open(os.path.join(out, "traffic.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))
