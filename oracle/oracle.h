@@ -37,8 +37,16 @@ size_t oracle_snappy_bound(size_t n);
  * Returns the uncompressed size on success, -1 on malformed input. cap = output capacity. */
 int64_t oracle_snappy_uncompress(const uint8_t* src, size_t csize, uint8_t* dst, size_t cap);
 
+/* zstd 1.5.2 frame compression as lzbench's zstd rows call it (ZSTD_getParams(level, n, 0) with
+ * contentSizeFlag, ZSTD_compress_advanced; reference _lzbench/compressors.cpp:1745-1770), for the
+ * fast-strategy levels (-131072..-1, 1, 2; level 2 only where it is fast).  dst needs
+ * oracle_zstd_bound(n) + 64 bytes.  Returns the frame size, or -1 for an unsupported level. */
+int64_t oracle_zstd_compress(const uint8_t* src, size_t n, uint8_t* dst, int level);
+size_t oracle_zstd_bound(size_t n);
+
 /* lzbench chunk loop (reference _lzbench/lzbench.cpp:266-298): compress every chunk,
- * store raw when clen<=0 || clen==part, pack contiguously. codec: 0=lz4 1=snappy.
+ * store raw when clen<=0 || clen==part, pack contiguously. codec: 0=lz4 1=snappy 2=zstd
+ * (compression only).
  * level: lz4 acceleration (0 or 1 -> default). Returns total packed bytes. */
 int64_t oracle_compress_chunks(int codec, int level, const uint8_t* in, size_t n,
                                size_t chunk_size, uint8_t* out, uint64_t* csizes);

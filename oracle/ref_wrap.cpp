@@ -60,7 +60,7 @@ int ref_zstd_version(void) { return (int)ZSTD_versionNumber(); }
 
 static int64_t one_compress(int codec, int level, const char* in, size_t part, char* out, size_t outpart) {
     if (codec == 2) {
-        const int64_t r = ref_zstd_compress(in, part, out, outpart, level < 1 ? 1 : level);
+        const int64_t r = ref_zstd_compress(in, part, out, outpart, level);   /* zstd_fast rows pass -5..-1 */
         return r < 0 ? 0 : r;
     }
     if (codec == 0) {

@@ -99,15 +99,19 @@ def snappy_compress(data: np.ndarray) -> bytes:
     return out[:r].tobytes()
 
 
-def compress_chunks(data: np.ndarray, codec: str, chunk: int, level: int = 1, use_ref: bool = False, threads: int = 0):
-    """lzbench_compress over uniform chunks with the CPU checker. Returns (packed, csizes)."""
+def compress_chunks(data: np.ndarray, codec: str, chunk: int, level: int = 1, use_ref=None, threads: int = 0):
+    """lzbench_compress over uniform chunks with the CPU checker. Returns (packed, csizes).
+    use_ref None: the restatement for lz4/snappy, the reference build for zstd when present
+    (the restatement covers zstd's fast-strategy levels only: oracle/zstd1_oracle.c)."""
     n = len(data)
     k = max((n + chunk - 1) // chunk, 1)
     out = np.zeros(n + n // 6 + 16384 + 64 * k + 64, np.uint8)
     cs = np.zeros(k, np.uint64)
     c = CODEC_ID[codec]
     lvl = level if codec in ("lz4fast", "zstd") else (1 if codec == "lz4" else 0)
-    if use_ref or codec == "zstd":
+    if use_ref is None:
+        use_ref = codec == "zstd" and have_ref()
+    if use_ref:
         L = ref()
         tot = (L.ref_compress_chunks_mt(c, lvl, data.ctypes.data, n, chunk, out.ctypes.data, cs.ctypes.data, threads)
                if threads else L.ref_compress_chunks(c, lvl, data.ctypes.data, n, chunk, out.ctypes.data, cs.ctypes.data))
