@@ -42,7 +42,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BASELINE_METRIC = "comp+decomp MB/s, lz4 -b64 on 1 GiB; ratio + bit-exact vs CPU ref"
 COMPRESS_KERNEL = {"lz4": "lzh_lz4_compress_v2_kernel", "lz4fast": "lzh_lz4_compress_v2_kernel",
-                   "snappy": "lzh_snappy_compress_v2_kernel", "zstd": "lzh_zstd_compress_kernel"}
+                   "snappy": "lzh_snappy_compress_v2_kernel",
+                   "zstd": "lzh_zstd_match_kernel+lzh_zstd_entropy_kernel"}
 DECOMPRESS_KERNEL = {"zstd": "lzh_zstd_decompress_kernel"}
 
 
@@ -352,7 +353,7 @@ def main():
         result_extra["cpu_baseline_all_cores"] = cpu_baseline(host, args.codec, chunk, args.level, args.cpu_iters,
                                                               usable)
     result_extra["host_cpu"] = cpuinfo
-    if rank == 0 and world == 1 and not args.no_e2e and args.codec != "zstd":
+    if rank == 0 and world == 1 and not args.no_e2e:
         del d_in
         torch.cuda.empty_cache()
         result_extra["e2e"] = e2e_rows(L, host, args.codec, chunk, args.level, 1, 3)

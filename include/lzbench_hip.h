@@ -41,8 +41,10 @@
 extern "C" {
 #endif
 
-/* LZH_CODEC_ZSTD: decode only (zstd 1.5.2 frames as lzbench's zstd rows write them, one frame
- * per chunk: content size present, no dictionary, no checksum), lzh_decompress_async only */
+/* LZH_CODEC_ZSTD: zstd 1.5.2 frames as lzbench's zstd rows write them, one frame per chunk
+ * (ZSTD_getParams(level, chunk, 0) + content size, no dictionary, no checksum).  Compression:
+ * the fast-strategy levels (zstd 1, 2 where fast, zstd_fast -1..-5), bit-exact with the reference;
+ * other levels return LZH_EARG.  Decoding: any frame of that shape. */
 enum { LZH_CODEC_LZ4 = 0, LZH_CODEC_SNAPPY = 1, LZH_CODEC_MEMCPY = 2, LZH_CODEC_ZSTD = 3 };
 enum { LZH_OK = 0, LZH_EARG = -1, LZH_EHIP = -2, LZH_ESPACE = -3, LZH_ECORRUPT = -4 };
 
@@ -50,6 +52,7 @@ enum { LZH_OK = 0, LZH_EARG = -1, LZH_EHIP = -2, LZH_ESPACE = -3, LZH_ECORRUPT =
 char*   lzbench_hip_lz4_init(size_t chunk_size, size_t level, size_t ngpus);
 char*   lzbench_hip_snappy_init(size_t chunk_size, size_t level, size_t ngpus);
 char*   lzbench_hip_memcpy_init(size_t chunk_size, size_t level, size_t ngpus);
+char*   lzbench_hip_zstd_init(size_t chunk_size, size_t level, size_t ngpus);
 void    lzbench_hip_deinit(char* workmem);
 /* lz4: LZ4_compress_default semantics; lz4fast: level = acceleration (LZ4_compress_fast) */
 int64_t lzbench_hip_lz4_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
@@ -57,6 +60,10 @@ int64_t lzbench_hip_lz4fast_compress(char* in, size_t insize, char* out, size_t 
 int64_t lzbench_hip_lz4_decompress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
 int64_t lzbench_hip_snappy_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
 int64_t lzbench_hip_snappy_decompress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+/* zstd: lzbench_zstd_compress / _decompress semantics (compressors.cpp:1745-1778); level as the
+ * zstd / zstd_fast rows pass it (size_t of a possibly negative int) */
+int64_t lzbench_hip_zstd_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+int64_t lzbench_hip_zstd_decompress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
 /* hipMemcpy plumbing row: host -> HBM -> host round trip of the chunk */
 int64_t lzbench_hip_memcpy(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
 
@@ -80,7 +87,7 @@ size_t lzh_decompress_temp_bytes(int codec, size_t n, size_t chunk_size);
 size_t lzh_num_chunks(size_t n, size_t chunk_size);
 
 /* d_csizes: nchunks u32 (out); d_offsets: nchunks+1 u64 (out; [nchunks] = packed total).
- * level: lz4 acceleration (<=1 -> LZ4_compress_default); ignored by snappy. */
+ * level: lz4 acceleration (<=1 -> LZ4_compress_default); zstd level; ignored by snappy. */
 int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t in_readable, size_t chunk_size,
                        void* d_packed, size_t packed_cap, uint32_t* d_csizes, uint64_t* d_offsets,
                        void* d_temp, size_t temp_bytes, void* hip_stream);

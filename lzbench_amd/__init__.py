@@ -33,7 +33,7 @@ DATAGEN_PATH = os.path.join(_HERE, "libdatagen.so")
 
 LZH_CODEC_LZ4, LZH_CODEC_SNAPPY, LZH_CODEC_MEMCPY, LZH_CODEC_ZSTD = 0, 1, 2, 3
 CODECS = {"lz4": LZH_CODEC_LZ4, "lz4fast": LZH_CODEC_LZ4, "snappy": LZH_CODEC_SNAPPY, "memcpy": LZH_CODEC_MEMCPY,
-          "zstd": LZH_CODEC_ZSTD}   # zstd: decode only (DeviceCodec.decompress)
+          "zstd": LZH_CODEC_ZSTD, "zstd_fast": LZH_CODEC_ZSTD}
 PAD_SIZE = 16 * 1024          # lzbench.h:14
 
 
@@ -59,6 +59,9 @@ SIGNATURES = {
     "lzbench_hip_lz4_init": (_P, [_SZ, _SZ, _SZ]),
     "lzbench_hip_snappy_init": (_P, [_SZ, _SZ, _SZ]),
     "lzbench_hip_memcpy_init": (_P, [_SZ, _SZ, _SZ]),
+    "lzbench_hip_zstd_init": (_P, [_SZ, _SZ, _SZ]),
+    "lzbench_hip_zstd_compress": _COMPRESS_FUNC,
+    "lzbench_hip_zstd_decompress": _COMPRESS_FUNC,
     "lzbench_hip_deinit": (None, [_P]),
     "lzbench_hip_lz4_compress": _COMPRESS_FUNC,
     "lzbench_hip_lz4fast_compress": _COMPRESS_FUNC,
@@ -147,6 +150,13 @@ COMP_DESC = (
     CompressorDesc("hip_snappy", "2020-07-11", 0, 0, 1, 0, "lzbench_hip_snappy_compress",
                    "lzbench_hip_snappy_decompress", "lzbench_hip_snappy_init", "lzbench_hip_deinit",
                    "lzbench_hip_compress_batch", "lzbench_hip_decompress_batch"),
+    # zstd / zstd_fast rows (lzbench.h:209-210) restricted to the fast-strategy levels
+    CompressorDesc("hip_zstd", "1.5.2", 1, 2, 1, 0, "lzbench_hip_zstd_compress", "lzbench_hip_zstd_decompress",
+                   "lzbench_hip_zstd_init", "lzbench_hip_deinit",
+                   "lzbench_hip_compress_batch", "lzbench_hip_decompress_batch"),
+    CompressorDesc("hip_zstd_fast", "1.5.2", -5, -1, 1, 0, "lzbench_hip_zstd_compress", "lzbench_hip_zstd_decompress",
+                   "lzbench_hip_zstd_init", "lzbench_hip_deinit",
+                   "lzbench_hip_compress_batch", "lzbench_hip_decompress_batch"),
 )
 
 
@@ -180,7 +190,7 @@ class _Row:
 
     def __init__(self, codec: str, chunk_size: int, level: int = 0, ngpus: int = 1):
         L = lib()
-        base = "memcpy" if codec == "memcpy" else ("snappy" if codec == "snappy" else "lz4")
+        base = {"memcpy": "memcpy", "snappy": "snappy", "zstd": "zstd", "zstd_fast": "zstd"}.get(codec, "lz4")
         self.desc = find_compressor("hipMemcpy" if codec == "memcpy" else codec)
         self.wm = getattr(L, f"lzbench_hip_{base}_init")(chunk_size, level, ngpus)
         if not self.wm:
@@ -199,6 +209,14 @@ class _Row:
         self.close()
 
 
+def _row_level(codec: str, level: int) -> int:
+    """The level argument lzbench passes for the row: lz4fast acceleration, zstd level (zstd_fast
+    rows are negative), 1 for lz4 (LZ4_compress_default), 0 for snappy; size_t on the wire."""
+    if codec in ("lz4fast", "zstd", "zstd_fast"):
+        return level & 0xFFFFFFFFFFFFFFFF
+    return 1 if codec == "lz4" else 0
+
+
 def compress_chunks(data, codec: str = "lz4", chunk_size: int = 65536, level: int = 0, ngpus: int = 1,
                     chunk_sizes=None) -> Tuple[np.ndarray, np.ndarray]:
     """lzbench_compress over the chunk list on the GPU(s). Returns (packed bytes, compr_sizes)."""
@@ -207,7 +225,7 @@ def compress_chunks(data, codec: str = "lz4", chunk_size: int = 65536, level: in
                               dtype=np.uint64)
     out = np.zeros(get_compress_bound(len(src)) + 64, dtype=np.uint8)
     compr = np.zeros(len(cs), dtype=np.uint64)
-    lvl = level if codec == "lz4fast" else (1 if codec == "lz4" else 0)
+    lvl = _row_level(codec, level)
     with _Row(codec, chunk_size, lvl, ngpus) as row:
         total = lib().lzbench_hip_compress_batch(src.ctypes.data, cs.ctypes.data, len(cs), out.ctypes.data,
                                                  len(out), compr.ctypes.data, lvl, ngpus, row.wm)
@@ -243,7 +261,7 @@ class DeviceCodec:
         import torch
         self.torch = torch
         self.codec = CODECS[codec]
-        self.level = level if codec == "lz4fast" else (1 if codec == "lz4" else 0)
+        self.level = level if codec in ("lz4fast", "zstd", "zstd_fast") else (1 if codec == "lz4" else 0)
         self.n, self.chunk_size = n, chunk_size
         L = lib()
         self.k = L.lzh_num_chunks(n, chunk_size)

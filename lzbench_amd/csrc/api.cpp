@@ -34,7 +34,7 @@ static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 extern "C" {
 
-const char* lzh_version(void) { return "lzbench_hip 0.1 (lz4 1.9.3 / snappy 1.1.8 bit-exact, gfx950)"; }
+const char* lzh_version(void) { return "lzbench_hip 0.2 (lz4 1.9.3 / snappy 1.1.8 / zstd 1.5.2 fast levels bit-exact, gfx950)"; }
 
 size_t lzh_datagen(int kind, uint64_t seed, void* buf, size_t n) { return lzb_datagen(kind, seed, (uint8_t*)buf, n); }
 
@@ -61,7 +61,13 @@ size_t lzh_max_packed_bytes(int codec, size_t n, size_t chunk_size) {
 size_t lzh_compress_temp_bytes(int codec, size_t n, size_t chunk_size) {
     size_t k = lzh_num_chunks(n, chunk_size);
     if (codec == LZH_CODEC_MEMCPY) return 256;
-    return align_up(k * lzh_stage_stride(codec, chunk_size), 256) + 256;
+    size_t t = align_up(k * lzh_stage_stride(codec, chunk_size), 256) + 256;
+    if (codec == LZH_CODEC_ZSTD) {   // per-frame scratch of the two zstd kernels (zstdc_hip.hip), worst level
+        size_t fs = 0;
+        for (int lv : {1, 2, -1, -2}) fs = std::max(fs, lzh_zstd_scratch_stride(chunk_size, lv));
+        t += k * fs + 256;
+    }
+    return t;
 }
 
 size_t lzh_decompress_temp_bytes(int codec, size_t n, size_t chunk_size) {
@@ -82,6 +88,11 @@ int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, s
     } else if (codec == LZH_CODEC_SNAPPY) {
         LZH_CHECK(lzh_launch_snappy_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
                                                 stride, d_csizes, (uint32_t)k, s));
+    } else if (codec == LZH_CODEC_ZSTD) {
+        if (!lzh_zstd_level_ok(level, chunk_size)) return LZH_EARG;
+        uint8_t* scratch = (uint8_t*)d_stage + align_up(k * stride, 256) + 256;
+        LZH_CHECK(lzh_launch_zstd_compress((const uint8_t*)d_in, n, in_readable, chunk_size, level, (uint8_t*)d_stage,
+                                           stride, d_csizes, (uint32_t)k, scratch, s));
     } else {
         return LZH_EARG;
     }
@@ -99,7 +110,6 @@ int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t 
     hipStream_t s = (hipStream_t)hip_stream;
     if (!chunk_size || !d_packed || !d_csizes || !d_offsets || (n && !d_in)) return LZH_EARG;
     if (in_readable < n) return LZH_EARG;
-    if (codec == LZH_CODEC_ZSTD) return LZH_EARG;                     // (decode only this round)
     const size_t k = lzh_num_chunks(n, chunk_size);
     if (codec == LZH_CODEC_MEMCPY) {
         if (packed_cap < n) return LZH_ESPACE;
@@ -124,7 +134,7 @@ int lzh_compress_finish_async(int codec, const void* d_in, size_t n, size_t in_r
                               uint64_t* d_offsets, void* hip_stream) {
     hipStream_t s = (hipStream_t)hip_stream;
     if (!chunk_size || !d_stage || !d_csizes || !d_packed || !d_offsets) return LZH_EARG;
-    if (codec != LZH_CODEC_LZ4 && codec != LZH_CODEC_SNAPPY) return LZH_EARG;
+    if (codec != LZH_CODEC_LZ4 && codec != LZH_CODEC_SNAPPY && codec != LZH_CODEC_ZSTD) return LZH_EARG;
     // the sizes are only known on the device: the worst case must fit (no silent truncation)
     if (packed_cap < lzh_max_packed_bytes(codec, n, chunk_size)) return LZH_ESPACE;
     const size_t k = lzh_num_chunks(n, chunk_size);
@@ -502,6 +512,7 @@ extern "C" {
 char* lzbench_hip_lz4_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_LZ4, chunk_size, ngpus); }
 char* lzbench_hip_snappy_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_SNAPPY, chunk_size, ngpus); }
 char* lzbench_hip_memcpy_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_MEMCPY, chunk_size, ngpus); }
+char* lzbench_hip_zstd_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_ZSTD, chunk_size, ngpus); }
 
 void lzbench_hip_deinit(char* wm) {
     LzhCtx* c = ctx_of(wm);
@@ -522,6 +533,12 @@ int64_t lzbench_hip_snappy_compress(char* in, size_t insize, char* out, size_t o
 }
 int64_t lzbench_hip_snappy_decompress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
     return one_chunk_decompress(LZH_CODEC_SNAPPY, in, insize, out, outsize, wm);
+}
+int64_t lzbench_hip_zstd_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t, char* wm) {
+    return one_chunk_compress(LZH_CODEC_ZSTD, in, insize, out, outsize, level, wm);
+}
+int64_t lzbench_hip_zstd_decompress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
+    return one_chunk_decompress(LZH_CODEC_ZSTD, in, insize, out, outsize, wm);
 }
 int64_t lzbench_hip_memcpy(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
     LzhCtx* c = ctx_of(wm);

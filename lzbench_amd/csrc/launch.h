@@ -22,3 +22,8 @@ hipError_t lzh_launch_pack(const uint8_t* in, uint64_t n_total, uint64_t in_read
                            const uint8_t* stage, uint64_t stride, const uint32_t* csizes, const uint64_t* offsets,
                            uint8_t* packed, uint64_t packed_cap, uint32_t nchunks, hipStream_t s);
 hipError_t lzh_launch_memcpy(const void* src, void* dst, uint64_t n, hipStream_t s);
+hipError_t lzh_launch_zstd_compress(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                                    int level, uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
+                                    uint8_t* scratch, hipStream_t s);
+size_t lzh_zstd_scratch_stride(size_t chunk_size, int level);
+int lzh_zstd_level_ok(int level, size_t chunk_size);

@@ -518,7 +518,7 @@ static size_t huf_compress_weights(u8* out, const u8* w, u32 wn) {
     s16 norm[13];
     if (fse_normalize(norm, tl, cnt, wn, maxs, 0)) return 0;
     size_t h = fse_write_ncount(out, norm, maxs, tl);
-    static fse_ct ct;
+    fse_ct ct;
     fse_build(&ct, norm, maxs, tl);
     if (wn <= 2) return 0;
     bitw b;
@@ -685,7 +685,7 @@ static size_t encode_sequences(u8* out, const zseq* seq, size_t nbSeq) {
         ofc[i] = (u8)hb32(seq[i].off);
         mlc[i] = (u8)ml_code(seq[i].ml - 3);
     }
-    static fse_ct ct[3];
+    fse_ct ct[3];   /* (on the stack: the _mt chunk loops call this from several threads) */
     const u8* codes[3] = {llc, ofc, mlc};
     const u32 maxTab[3] = {35, 31, 52}, fseLog[3] = {9, 8, 9}, defLog[3] = {6, 5, 6}, defMax[3] = {35, 28, 52};
     const s16* defNorm[3] = {LL_DEF, OF_DEF, ML_DEF};
