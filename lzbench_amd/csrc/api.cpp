@@ -16,8 +16,17 @@
 #include <algorithm>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "../../include/lzbench_hip.h"
 #include "launch.h"
+
+// rocprof-visible ranges around each stage's launches (rocprofv3 --marker-trace); a range covers
+// the enqueue of the stage on the host, the kernels themselves show in --kernel-trace
+struct Range {
+    explicit Range(const char* n) { roctxRangePushA(n); }
+    ~Range() { roctxRangePop(); }
+};
 
 extern "C" size_t lzb_datagen(int kind, uint64_t seed, uint8_t* buf, size_t n);
 
@@ -82,6 +91,7 @@ int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, s
     const size_t k = lzh_num_chunks(n, chunk_size);
     if (k > 0xffffffffu || chunk_size > 0x7fff0000u) return LZH_EARG;
     const size_t stride = lzh_stage_stride(codec, chunk_size);
+    Range range("lzh:compress_kernel");
     if (codec == LZH_CODEC_LZ4) {
         LZH_CHECK(lzh_launch_lz4_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, level < 1 ? 1 : level,
                                              (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
@@ -139,6 +149,7 @@ int lzh_compress_finish_async(int codec, const void* d_in, size_t n, size_t in_r
     if (packed_cap < lzh_max_packed_bytes(codec, n, chunk_size)) return LZH_ESPACE;
     const size_t k = lzh_num_chunks(n, chunk_size);
     const size_t stride = lzh_stage_stride(codec, chunk_size);
+    Range range("lzh:scan_pack");
     LZH_CHECK(lzh_launch_scan(d_csizes, k, d_offsets, nullptr, s));
     LZH_CHECK(lzh_launch_pack((const uint8_t*)d_in, n, in_readable, chunk_size, (const uint8_t*)d_stage, stride,
                               d_csizes, d_offsets, (uint8_t*)d_packed, packed_cap, (uint32_t)k, s));
@@ -154,6 +165,7 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
     if (codec == LZH_CODEC_ZSTD && chunk_size > (1u << 30)) return LZH_EARG;
     const size_t k = lzh_num_chunks(n, chunk_size);
     if (n == 0) return LZH_OK;
+    Range range("lzh:decompress");
     const uint64_t* offs = d_offsets;
     if (!offs) {
         if (!d_temp || temp_bytes < lzh_decompress_temp_bytes(codec, n, chunk_size)) return LZH_ESPACE;
@@ -355,6 +367,7 @@ Plan make_plan(size_t ndev, size_t n, size_t chunk) {
 int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t chunk, uint8_t* out, size_t outcap,
                      size_t* compr_sizes) {
     DeviceGuard guard;
+    Range range("lzh:row_compress");
     const Plan P = make_plan(c->devs.size(), n, chunk);
     const size_t sb_in = std::min(n, P.sbk * chunk);                   // largest sub-batch input
     const size_t sb_packed = align_up(lzh_max_packed_bytes(c->codec, sb_in, chunk) + 64, 256);
@@ -418,6 +431,7 @@ int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t c
 // keeps lzbench's length check (lzbench.cpp:433-437) honest for short decodes.
 int64_t run_decompress(LzhCtx* c, const uint8_t* in, const size_t* compr_sizes, size_t n, size_t chunk, uint8_t* out) {
     DeviceGuard guard;
+    Range range("lzh:row_decompress");
     const Plan P = make_plan(c->devs.size(), n, chunk);
     const size_t k = P.k;
     std::vector<size_t> coff(k + 1, 0);

@@ -2,7 +2,8 @@
 // codec rows of liblzbench_hip.so.
 //
 // Mirrors the reference driver's semantics (/root/reference/_lzbench/lzbench.cpp):
-//   * options -b -c -e -i -t -u -o -p -s -v -x -z -l -j and the "--compress-only" switch
+//   * options -b -c -e -i -t -u -o -p -s -v -x -z -l -j and the "--compress-only" switch; -x
+//     leaves the process priority alone, otherwise it is raised as SET_HIGH_PRIORITY does
 //     (option parsing lzbench.cpp:824-934, usage :731-758)
 //   * compressor_desc_t table with memcpy at index 0 (lzbench.h:113-219), name/level lookup
 //     with '/' and ',' separated lists and aliases (lzbench.cpp:479-534)
@@ -20,6 +21,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -95,14 +97,19 @@ static compressor_desc_t comp_desc[] = {
      lzbench_hip_lz4_init, lzbench_hip_deinit, lzbench_hip_compress_batch, lzbench_hip_decompress_batch},
     {"hip_snappy", "2020-07-11", 0, 0, 1, 0, lzbench_hip_snappy_compress, lzbench_hip_snappy_decompress,
      lzbench_hip_snappy_init, lzbench_hip_deinit, lzbench_hip_compress_batch, lzbench_hip_decompress_batch},
+    // zstd / zstd_fast rows (lzbench.h:209-210) at the fast-strategy levels the GPU compressor covers
+    {"hip_zstd", "1.5.2", 1, 2, 1, 0, lzbench_hip_zstd_compress, lzbench_hip_zstd_decompress, lzbench_hip_zstd_init,
+     lzbench_hip_deinit, lzbench_hip_compress_batch, lzbench_hip_decompress_batch},
+    {"hip_zstd_fast", "1.5.2", -5, -1, 1, 0, lzbench_hip_zstd_compress, lzbench_hip_zstd_decompress,
+     lzbench_hip_zstd_init, lzbench_hip_deinit, lzbench_hip_compress_batch, lzbench_hip_decompress_batch},
 };
 static const int kRows = (int)(sizeof(comp_desc) / sizeof(comp_desc[0]));
 
 struct alias_t { const char* name; const char* params; };
 static const alias_t aliases[] = {
-    {"hip", "hipMemcpy/hip_lz4/hip_lz4fast,3,17/hip_snappy"},
-    {"fast", "lz4/lz4fast,3,17/hip_lz4/hip_lz4fast,3,17/hip_snappy"},
-    {"all", "lz4/lz4fast,3,17/hipMemcpy/hip_lz4/hip_lz4fast,3,17/hip_snappy"},
+    {"hip", "hipMemcpy/hip_lz4/hip_lz4fast,3,17/hip_snappy/hip_zstd,1"},
+    {"fast", "lz4/lz4fast,3,17/hip_lz4/hip_lz4fast,3,17/hip_snappy/hip_zstd_fast,-1/hip_zstd,1"},
+    {"all", "lz4/lz4fast,3,17/hipMemcpy/hip_lz4/hip_lz4fast,3,17/hip_snappy/hip_zstd_fast/hip_zstd"},
 };
 
 // ---- parameters and results (lzbench.h:83-105) ------------------------------------------
@@ -393,7 +400,7 @@ static void usage(params_t* P) {
     fprintf(stderr, " -s#   use only compressors with compression speed over # MB (default = %u MB)\n", P->cspeed);
     fprintf(stderr, " -tX,Y set min. time in seconds for compression and decompression (default = %.0f, %.0f)\n",
             P->cmintime / 1000.0, P->dmintime / 1000.0);
-    fprintf(stderr, " -v    disable progress information\n -x    (accepted, no effect)\n -z    show (de)compression times instead of speed\n");
+    fprintf(stderr, " -v    disable progress information\n -x    disable real-time process priority\n -z    show (de)compression times instead of speed\n");
 }
 
 static int read_file(const char* fn, std::vector<uint8_t>& out) {
@@ -435,6 +442,7 @@ static void bench_buffer(params_t* P, std::vector<size_t>& fs, const std::vector
     if (P->results.empty()) {   // implicit memcpy row first (lzbench.cpp:685-697)
         params_t Q = *P;
         Q.cmintime = Q.dmintime = 0;
+        Q.c_iters = Q.d_iters = 0;
         Q.cloop_time = Q.dloop_time = DEFAULT_LOOP_TIME;
         std::vector<size_t> one(1, insize);
         bench_one(&Q, one, &comp_desc[0], 0, in, insize, comp, compsize, dec);
@@ -449,7 +457,7 @@ int main(int argc, char** argv) {
     params_t* P = &params;
     const char* list = "hip";
     int sort_col = 0;
-    bool join = false, recursive = false;
+    bool join = false, recursive = false, real_time = true;
     int ngpu = 0;
     g_gpu = hipGetDeviceCount(&ngpu) == hipSuccess && ngpu > 0;
     load_sys_lz4();
@@ -488,7 +496,7 @@ int main(int argc, char** argv) {
             }
             case 'u': P->dmintime = 1000ull * num; P->dloop_time = P->dmintime ? DEFAULT_LOOP_TIME : 0; break;
             case 'v': P->verbose = (int)num; break;
-            case 'x': break;
+            case 'x': real_time = false; break;
             case 'z': P->show_speed = 0; break;
             case 'l':
                 printf("\nAvailable compressors for -e option:\n");
@@ -510,6 +518,9 @@ int main(int argc, char** argv) {
         argc--;
     }
     if (argc < 2) { usage(P); return 1; }
+    // SET_HIGH_PRIORITY unless -x (util.h:106, lzbench.cpp:948); needs privileges, so a refusal
+    // (EACCES / EPERM) leaves the default priority, as in the reference
+    if (real_time) (void)setpriority(PRIO_PROCESS, 0, -20);
     LZB_PRINT(2, PROGNAME " 1.8-hip (lzbench chunk loop, MI355X codec rows; %d GPU%s visible)\n\n", ngpu, ngpu == 1 ? "" : "s");
     print_header(P);
 
