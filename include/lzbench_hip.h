@@ -104,6 +104,12 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
 int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, size_t in_readable,
                              size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream);
 
+/* One stage of lzh_compress_kernel_only (profiling, roofline of one kernel): stage_mask bit 0 =
+ * the parse kernel (LZ4: sequence records; snappy / zstd: the whole codec), bit 1 = the LZ4
+ * block-emission kernel (records -> staging slots and sizes).  Both bits = lzh_compress_kernel_only. */
+int lzh_compress_kernel_stage(int codec, int level, int stage_mask, const void* d_in, size_t n, size_t in_readable,
+                              size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream);
+
 /* The rest of lzh_compress_async after lzh_compress_kernel_only: scan the per-chunk sizes
  * into d_offsets and pack the staged streams (or the raw input) into d_packed. */
 int lzh_compress_finish_async(int codec, const void* d_in, size_t n, size_t in_readable, size_t chunk_size,

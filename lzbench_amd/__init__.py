@@ -79,6 +79,7 @@ SIGNATURES = {
     "lzh_compress_async": (C.c_int, [C.c_int, C.c_int, _P, _SZ, _SZ, _SZ, _P, _SZ, _P, _P, _P, _SZ, _P]),
     "lzh_decompress_async": (C.c_int, [C.c_int, _P, _SZ, _P, _P, _SZ, _SZ, _P, _P, _P, _SZ, _P]),
     "lzh_compress_kernel_only": (C.c_int, [C.c_int, C.c_int, _P, _SZ, _SZ, _SZ, _P, _P, _P]),
+    "lzh_compress_kernel_stage": (C.c_int, [C.c_int, C.c_int, C.c_int, _P, _SZ, _SZ, _SZ, _P, _P, _P]),
     "lzh_compress_finish_async": (C.c_int, [C.c_int, _P, _SZ, _SZ, _SZ, _P, _P, _P, _SZ, _P, _P]),
     "lzh_datagen": (_SZ, [C.c_int, C.c_uint64, _P, _SZ]),
     "lzh_version": (C.c_char_p, []),
@@ -294,6 +295,14 @@ class DeviceCodec:
                                             self._stream())
         if rc:
             raise RuntimeError(f"lzh_compress_kernel_only failed ({rc})")
+
+    def compress_stage(self, d_in, stage_mask: int) -> None:
+        """One stage of compress_kernel_only (1 = parse kernel, 2 = LZ4 emission kernel)."""
+        rc = lib().lzh_compress_kernel_stage(self.codec, self.level, stage_mask, d_in.data_ptr(), self.n, d_in.numel(),
+                                             self.chunk_size, self.ctemp.data_ptr(), self.csizes.data_ptr(),
+                                             self._stream())
+        if rc:
+            raise RuntimeError(f"lzh_compress_kernel_stage failed ({rc})")
 
     def compress_finish(self, d_in) -> None:
         rc = lib().lzh_compress_finish_async(self.codec, d_in.data_ptr(), self.n, d_in.numel(), self.chunk_size,

@@ -41,6 +41,10 @@ extern "C" size_t lzb_datagen(int kind, uint64_t seed, uint8_t* buf, size_t n);
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// LZ4 chunks up to this size compress in two kernels (parse -> 8-byte sequence records -> emit);
+// larger ones (24-bit record fields) in the single kernel that assembles the block itself
+static const size_t kLz4SplitMax = (size_t)16 << 20;
+
 extern "C" {
 
 const char* lzh_version(void) { return "lzbench_hip 0.2 (lz4 1.9.3 / snappy 1.1.8 / zstd 1.5.2 fast levels bit-exact, gfx950)"; }
@@ -71,6 +75,8 @@ size_t lzh_compress_temp_bytes(int codec, size_t n, size_t chunk_size) {
     size_t k = lzh_num_chunks(n, chunk_size);
     if (codec == LZH_CODEC_MEMCPY) return 256;
     size_t t = align_up(k * lzh_stage_stride(codec, chunk_size), 256) + 256;
+    if (codec == LZH_CODEC_LZ4 && chunk_size <= kLz4SplitMax)     // sequence records of the parse kernel
+        t += k * lzh_lz4_rec_stride(chunk_size) + align_up(k * 8, 256) + 256;
     if (codec == LZH_CODEC_ZSTD) {   // per-frame scratch of the two zstd kernels (zstdc_hip.hip), worst level
         size_t fs = 0;
         for (int lv : {1, 2, -1, -2}) fs = std::max(fs, lzh_zstd_scratch_stride(chunk_size, lv));
@@ -84,8 +90,8 @@ size_t lzh_decompress_temp_bytes(int codec, size_t n, size_t chunk_size) {
     return align_up((lzh_num_chunks(n, chunk_size) + 1) * sizeof(uint64_t), 256) + 256;
 }
 
-int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, size_t in_readable,
-                             size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream) {
+int lzh_compress_kernel_stage(int codec, int level, int stage_mask, const void* d_in, size_t n, size_t in_readable,
+                              size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream) {
     hipStream_t s = (hipStream_t)hip_stream;
     if (!chunk_size || !d_stage || !d_csizes || (n && !d_in)) return LZH_EARG;
     const size_t k = lzh_num_chunks(n, chunk_size);
@@ -93,20 +99,33 @@ int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, s
     const size_t stride = lzh_stage_stride(codec, chunk_size);
     Range range("lzh:compress_kernel");
     if (codec == LZH_CODEC_LZ4) {
-        LZH_CHECK(lzh_launch_lz4_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, level < 1 ? 1 : level,
-                                             (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
+        if (chunk_size <= kLz4SplitMax) {
+            uint8_t* recs = (uint8_t*)d_stage + align_up(k * stride, 256) + 256;
+            LZH_CHECK(lzh_launch_lz4_split((const uint8_t*)d_in, n, in_readable, chunk_size, level < 1 ? 1 : level,
+                                           (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, recs, stage_mask, s));
+        } else if (stage_mask & 1) {
+            LZH_CHECK(lzh_launch_lz4_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, level < 1 ? 1 : level,
+                                                 (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
+        }
     } else if (codec == LZH_CODEC_SNAPPY) {
-        LZH_CHECK(lzh_launch_snappy_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
-                                                stride, d_csizes, (uint32_t)k, s));
+        if (stage_mask & 1)
+            LZH_CHECK(lzh_launch_snappy_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
+                                                    stride, d_csizes, (uint32_t)k, s));
     } else if (codec == LZH_CODEC_ZSTD) {
         if (!lzh_zstd_level_ok(level, chunk_size)) return LZH_EARG;
         uint8_t* scratch = (uint8_t*)d_stage + align_up(k * stride, 256) + 256;
-        LZH_CHECK(lzh_launch_zstd_compress((const uint8_t*)d_in, n, in_readable, chunk_size, level, (uint8_t*)d_stage,
-                                           stride, d_csizes, (uint32_t)k, scratch, s));
+        if (stage_mask & 1)
+            LZH_CHECK(lzh_launch_zstd_compress((const uint8_t*)d_in, n, in_readable, chunk_size, level,
+                                               (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, scratch, s));
     } else {
         return LZH_EARG;
     }
     return LZH_OK;
+}
+
+int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, size_t in_readable,
+                             size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream) {
+    return lzh_compress_kernel_stage(codec, level, 3, d_in, n, in_readable, chunk_size, d_stage, d_csizes, hip_stream);
 }
 
 __global__ void lzh_fill_raw_sizes(uint32_t* cs, uint64_t k, uint64_t n, uint64_t chunk) {

@@ -229,6 +229,23 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     uint64_t rc_m = 0;                                                                             \
     int rc_tot = 0
 #define RECS_EMIT() op = emit_recs(in, R, out, O, op, rc_anc, rc_lit, rc_off, rc_mlx, rc_st, rc_m, rc_tot, lane)
+// kRec: the batch's sequences leave as records (literals | match length - 4 << 24 | offset << 48, one
+// u64 per sequence, chunk order) for lzh_lz4_emit_kernel instead of being assembled here
+#define RECS_OUT()                                                                                 \
+    do {                                                                                           \
+        if (kRec) {                                                                                \
+            if (rc_m) {                                                                            \
+                const int ri_ = nrec + __builtin_popcountll(rc_m & ((1ull << lane) - 1ull));       \
+                if (lane_on(rc_m)) {                                                               \
+                    st_b32(recs, 8 * ri_, rc_lit | (rc_mlx << 24));                                \
+                    st_b32(recs, 8 * ri_ + 4, (rc_mlx >> 8) | (rc_off << 16));                     \
+                }                                                                                  \
+                nrec += __builtin_popcountll(rc_m);                                                \
+            }                                                                                      \
+        } else {                                                                                   \
+            RECS_EMIT();                                                                           \
+        }                                                                                          \
+    } while (0)
 
 // Emit the records at op (returns the new op).  Common case (<= 256 bytes, literals in the
 // input ring): output byte t of the batch is lane t of pass t/64; its sequence is the last
@@ -507,33 +524,40 @@ __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t los
                 bk_ = lane == k_ ? b_ : bk_;                                                       \
             }                                                                                      \
             const int lit_ = p_ - bk_ - anc_, mlx_ = bk_ + pr_cn;                                  \
-            const int L_ = mem_ ? 3 + lit_ + ext_len_bytes(lit_) + ext_len_bytes(mlx_) : 0;        \
-            const int incl_ = wave_incl_scan(L_);                                                  \
             rc_anc = (uint32_t)anc_;                                                               \
             rc_lit = (uint32_t)lit_;                                                               \
             rc_off = (uint32_t)(p_ - (int)pr_ce);                                                  \
             rc_mlx = (uint32_t)mlx_;                                                               \
-            rc_st = (uint32_t)(incl_ - L_);                                                        \
             rc_m = pr_m;                                                                           \
-            rc_tot = rdlanei(incl_, 63);                                                           \
+            if (!kRec) {   /* output offsets: only the in-kernel emission needs them */            \
+                const int L_ = mem_ ? 3 + lit_ + ext_len_bytes(lit_) + ext_len_bytes(mlx_) : 0;    \
+                const int incl_ = wave_incl_scan(L_);                                              \
+                rc_st = (uint32_t)(incl_ - L_);                                                    \
+                rc_tot = rdlanei(incl_, 63);                                                       \
+            }                                                                                      \
             pr_m = 0;                                                                              \
         }                                                                                          \
     } while (0)
 
-template <bool kSmall, bool kStats>
+template <bool kSmall, bool kStats, bool kRec = false>
 __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab,
                                LDSA uint32_t* ringw, LDSA uint8_t* outb, uint32_t* out_size,
-                               unsigned long long* stats) {
+                               unsigned long long* stats, rsrc_t recs, uint32_t* rec_hdr) {
     const int lane = threadIdx.x;
     Table<kSmall> T{tab};
     uint64_t clk[kClk] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t ctr[kCtr] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t clk_last = kStats ? __builtin_amdgcn_s_memtime() : 0;
     if (n <= 0) {
+        if (kRec) {
+            if (lane == 0) { rec_hdr[0] = 0; rec_hdr[1] = 0; }
+            return;
+        }
         if (lane == 0) out.st8(0, 0);
         if (lane == 0) *out_size = 1;
         return;
     }
+    int nrec = 0;
     {
         LDSA uint32_t* t4 = (LDSA uint32_t*)tab;
 #pragma unroll
@@ -575,7 +599,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         for (int guard = 0; go && guard < 4 * n + 64; guard++) {
             runb = unii(runb) != 0; retest = unii(retest) != 0;
             base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
-            op = unii(op); anchor = unii(anchor); rc_tot = unii(rc_tot);
+            op = unii(op); anchor = unii(anchor); rc_tot = unii(rc_tot); nrec = unii(nrec);
             R.fill = unii(R.fill); R.ready = unii(R.ready); O.flushed = unii(O.flushed);
             LZ_STAT(0, 1);
             LZ_CLK(9);                                                 // (loop overhead / uncharged)
@@ -630,7 +654,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             // ---- deferred records + emission of the previous batch (under the loads above)
             pr_m = uni64(pr_m); pr_base = unii(pr_base); pr_anchor = unii(pr_anchor);
             RUN_RECORDS();
-            RECS_EMIT();
+            RECS_OUT();
             rc_m = 0;
             rc_tot = 0;
             LZ_CLK(2);                                                 // deferred emission
@@ -643,7 +667,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 const int target = min(front + in.sh + kAhead, endX + 256);
                 for (int r = 0; r < 4 && R.fill < target; r++) { R.refill(in.r, lane); LZ_STAT(12, 1); }
             }
-            if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
+            if (!kRec && op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
             int bkr, len;
             bool ok = eval_lane(ps, W, valid, bkr, len);
             if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
@@ -942,11 +966,15 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
     R.ready = R.fill;
     wave_lds_fence();
     RUN_RECORDS();
-    RECS_EMIT();
-    if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
-    op = emit_seq(in, R, out, O, op, anchor, n - anchor, false, 0, 0, lane);
-    O.flush(out, op, lane);
-    if (lane == 0) *out_size = (uint32_t)op;
+    RECS_OUT();
+    if (kRec) {
+        if (lane == 0) { rec_hdr[0] = (uint32_t)nrec; rec_hdr[1] = (uint32_t)anchor; }
+    } else {
+        if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
+        op = emit_seq(in, R, out, O, op, anchor, n - anchor, false, 0, 0, lane);
+        O.flush(out, op, lane);
+        if (lane == 0) *out_size = (uint32_t)op;
+    }
     if (kStats && lane == 0) {
         for (int i = 0; i < kCtr; i++) atomicAdd(&stats[i], (unsigned long long)ctr[i]);
         for (int i = 0; i < kClk; i++) atomicAdd(&stats[13 + i], (unsigned long long)clk[i]);
@@ -975,8 +1003,9 @@ lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_read
     LDSA uint32_t* tab = (LDSA uint32_t*)lds;
     LDSA uint32_t* ring = tab + 4096;
     LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
-    if (n < 65547) lz4v3::compress_chunk<true, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats);
-    else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats);
+    const rsrc_t nr = make_rsrc(nullptr, 0);
+    if (n < 65547) lz4v3::compress_chunk<true, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+    else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
 }
 
 // debug twin of the kernel above with event counters (tools/lz4_stats.py)
@@ -996,17 +1025,208 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
     LDSA uint32_t* tab = (LDSA uint32_t*)lds;
     LDSA uint32_t* ring = tab + 4096;
     LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
-    if (n < 65547) lz4v3::compress_chunk<true, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats);
-    else lz4v3::compress_chunk<false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats);
+    const rsrc_t nr = make_rsrc(nullptr, 0);
+    if (n < 65547) lz4v3::compress_chunk<true, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+    else lz4v3::compress_chunk<false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+}
+
+// ======================================================================= parse + emit split
+// The parse kernel (one wave per chunk, the compress_chunk loop above with kRec) leaves every
+// sequence as an 8-byte record; lzh_lz4_emit_kernel, which needs no hash table and runs at high
+// occupancy, lays the LZ4 block out (lz4.c:1022-1135 sequence format, :1204-1231 last literals):
+// for 64 records at a time a wave computes input anchors and output offsets by prefix sums,
+// every lane writes its sequence's bytes into an LDS ring, and the ring leaves for the staging
+// slot as aligned dwords.  Chunks up to 16 MiB (24-bit literal / match-length fields).
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
+                     uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4];
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t off = chunk * chunk_size;
+    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
+    const int n = (int)min(chunk_size, n_total - off);
+    const uint64_t readable = min<uint64_t>(in_readable - off, (uint64_t)n + 64);
+    Bytes rin, rout;
+    rin.init(in + off, readable);
+    rout.init(nullptr, 0);
+    LDSA uint32_t* tab = (LDSA uint32_t*)lds;
+    LDSA uint32_t* ring = tab + 4096;
+    const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
+    uint32_t* hdr = rec_hdr + 2 * chunk;
+    if (n < 65547) lz4v3::compress_chunk<true, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+    else lz4v3::compress_chunk<false, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+}
+
+namespace lz4e {
+
+constexpr int kRingB = 2048;            // LDS output ring (bytes)
+constexpr int kSpan = 2048;             // LDS copy of a record group's input span (bytes)
+// (4 KiB of LDS per wave: the emission kernel runs at the full 8 waves per SIMD)
+
+__device__ __forceinline__ int wave_max(int v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ int ext_len(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+__device__ __forceinline__ int wave_excl_scan(int x, int lane, int& total) {
+    int incl = lz4v3::wave_incl_scan(x);
+    total = __builtin_amdgcn_readlane(incl, 63);
+    return incl - x;
+}
+
+struct OutR {
+    LDSA uint8_t* b;
+    rsrc_t o;          // staging slot (256-aligned)
+    int flushed;       // bytes [0, flushed) are in global memory
+    __device__ __forceinline__ void put(int pos, uint32_t v) const { ((volatile LDSA uint8_t*)b)[pos & (kRingB - 1)] = (uint8_t)v; }
+    // global <- complete dwords of [flushed, upto) (all of it when fin: the partial last dword too)
+    __device__ __forceinline__ void flush(int upto, bool fin, int lane) {
+        wave_lds_fence();
+        const int d0 = flushed >> 2, d1 = fin ? (upto + 3) >> 2 : upto >> 2;
+        for (int d = d0 + lane; d < d1; d += 64)
+            st_b32(o, 4 * d, ((volatile LDSA uint32_t*)b)[d & (kRingB / 4 - 1)]);
+        flushed = 4 * d1;
+        if (flushed > upto) flushed = upto & ~3;   // (the partial dword is rewritten by the next flush)
+        wave_lds_fence();
+    }
+};
+
+// bytes of one sequence (or the last literals: ml < 0) written by the whole wave through the ring
+__device__ void put_seq_wave(OutR& R, const Bytes& in, int op, int anchor, int lit, int off, int mlx, int lane) {
+    const bool hm = mlx >= 0;
+    const int lx = ext_len(lit), mx = hm ? ext_len(mlx) : 0;
+    const uint32_t token = ((uint32_t)min(lit, 15) << 4) | (hm ? (uint32_t)min(mlx, 15) : 0u);
+    int pos = op;
+    if (lane == 0) R.put(pos, token);
+    pos++;
+    for (int b = 0; b < lx; b += 64) {
+        if (pos + b - R.flushed >= kRingB - 128) R.flush(pos + b, false, lane);
+        if (b + lane < lx) R.put(pos + b + lane, b + lane == lx - 1 ? (uint32_t)(lit - 15) % 255u : 255u);
+    }
+    pos += lx;
+    for (int b = 0; b < lit; b += 64) {
+        if (pos + b - R.flushed >= kRingB - 128) R.flush(pos + b, false, lane);
+        if (b + lane < lit) R.put(pos + b + lane, in.b(anchor + b + lane));
+    }
+    pos += lit;
+    if (hm) {
+        if (pos - R.flushed >= kRingB - 128) R.flush(pos, false, lane);
+        if (lane < 2) R.put(pos + lane, lane ? ((uint32_t)off >> 8) : ((uint32_t)off & 0xffu));
+        pos += 2;
+        for (int b = 0; b < mx; b += 64) {
+            if (pos + b - R.flushed >= kRingB - 128) R.flush(pos + b, false, lane);
+            if (b + lane < mx) R.put(pos + b + lane, b + lane == mx - 1 ? (uint32_t)(mlx - 15) % 255u : 255u);
+        }
+    }
+}
+
+}  // namespace lz4e
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                    const uint8_t* recs, uint64_t rec_stride, const uint32_t* rec_hdr, uint8_t* stage, uint64_t stride,
+                    uint32_t* csizes) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[lz4e::kRingB];
+    __shared__ __attribute__((aligned(16))) uint32_t ibuf[lz4e::kSpan / 4 + 4];   // input span of a group
+    const int lane = threadIdx.x;
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t off = chunk * chunk_size;
+    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
+    const int n = (int)min(chunk_size, n_total - off);
+    Bytes in_b;
+    in_b.init(in + off, min<uint64_t>(in_readable - off, (uint64_t)n + 64));
+    const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
+    const int nrec = (int)uni(rec_hdr[2 * chunk]);
+    lz4e::OutR R{(LDSA uint8_t*)ring, make_rsrc(stage + chunk * stride, (uint32_t)stride), 0};
+    int op = 0, ia = 0;
+    uint32_t nw0 = 0, nw1 = 0;                 // records of the next group (loaded one group ahead)
+    if (lane < nrec) { nw0 = ld_b32(rr, 8 * lane); nw1 = ld_b32(rr, 8 * lane + 4); }
+    for (int g = 0; g < nrec; g += 64) {
+        const int r = g + lane;
+        const bool v = r < nrec;
+        const uint32_t w0 = nw0, w1 = nw1;
+        if (r + 64 < nrec) { nw0 = ld_b32(rr, 8 * (r + 64)); nw1 = ld_b32(rr, 8 * (r + 64) + 4); }
+        const int lit = (int)(w0 & 0xFFFFFFu), mlx = (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8)), o = (int)(w1 >> 16);
+        const int S = v ? 3 + lit + lz4e::ext_len(lit) + lz4e::ext_len(mlx) : 0;
+        const int L = v ? lit + 4 + mlx : 0;
+        int T, Lt;
+        const int pos = op + lz4e::wave_excl_scan(S, lane, T);
+        const int anc = ia + lz4e::wave_excl_scan(L, lane, Lt);
+        const int Smax = (int)uni((uint32_t)lz4e::wave_max(S));
+        if (T <= lz4e::kRingB / 2 && Smax <= 64 && Lt + 8 <= lz4e::kSpan) {
+            // the group's input span [ia, ia + Lt) into LDS (literal bytes are read from there)
+            const int X0 = (ia + in_b.sh) & ~3;
+            const int nd = (ia + in_b.sh + Lt - X0 + 3) >> 2;
+            for (int d = lane; d < nd; d += 64) ibuf[d] = ld_b32(in_b.r, X0 + 4 * d);
+            wave_lds_fence();
+            const LDSA uint8_t* ib = (const LDSA uint8_t*)ibuf;
+            const int ioff = ia + in_b.sh - X0 - ia;   // input position p lives at ib[p + ioff]
+            // every lane writes its own sequence, byte t of it at pass t
+            if (op + T - R.flushed > lz4e::kRingB - 8) R.flush(op, false, lane);
+            const int lx = lz4e::ext_len(lit), mx = lz4e::ext_len(mlx);
+            const uint32_t token = ((uint32_t)min(lit, 15) << 4) | (uint32_t)min(mlx, 15);
+            const int lit0 = 1 + lx, lit1 = lit0 + lit;
+            for (int t = 0; t < Smax; t++) {
+                if (t < S) {
+                    uint32_t b = token;
+                    if (t >= 1 && t < lit0) b = t == lx ? (uint32_t)(lit - 15) % 255u : 255u;
+                    else if (t >= lit0 && t < lit1) b = ib[anc + t - lit0 + ioff];
+                    else if (t == lit1) b = (uint32_t)o & 0xffu;
+                    else if (t == lit1 + 1) b = (uint32_t)o >> 8;
+                    else if (t > lit1 + 1) b = (t - lit1 - 2 == mx - 1) ? (uint32_t)(mlx - 15) % 255u : 255u;
+                    R.put(pos + t, b);
+                }
+            }
+            op += T;
+            if (op - R.flushed >= lz4e::kRingB / 2) R.flush(op, false, lane);
+            wave_lds_fence();
+        } else {
+            for (int k = 0; k < 64 && g + k < nrec; k++) {
+                const int kl = rdlanei(lit, k), km = rdlanei(mlx, k), ko = rdlanei(o, k), ka = rdlanei(anc, k);
+                if (op + 256 - R.flushed > lz4e::kRingB) R.flush(op, false, lane);
+                lz4e::put_seq_wave(R, in_b, op, ka, kl, ko, km, lane);
+                op += 3 + kl + lz4e::ext_len(kl) + lz4e::ext_len(km);
+            }
+        }
+        ia += Lt;
+    }
+    // last literals (lz4.c:1204-1231): everything after the last match, the whole chunk if none
+    const int last = n - ia;
+    if (op + 256 - R.flushed > lz4e::kRingB) R.flush(op, false, lane);
+    lz4e::put_seq_wave(R, in_b, op, ia, last, 0, -1, lane);
+    op += 1 + last + lz4e::ext_len(last);
+    R.flush(op, true, lane);
+    if (lane == 0) csizes[chunk] = (uint32_t)op;
 }
 
 #include "launch.h"
+size_t lzh_lz4_rec_stride(uint64_t chunk_size) { return ((chunk_size / 4 + 4) * 8 + 255) / 256 * 256; }
+
 hipError_t lzh_launch_lz4_compress_v2(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                                       int acc, uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
                                       hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     hipLaunchKernelGGL(lzh_lz4_compress_v2_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable,
                        chunk_size, acc, stage, stride, csizes, 0u, (unsigned long long*)nullptr);
+    return hipGetLastError();
+}
+
+// parse kernel + emit kernel (records in `recs`: nchunks x rec_stride bytes, then 8 bytes per chunk);
+// stage_mask bit 0 = parse, bit 1 = emit (profiling runs one of them)
+hipError_t lzh_launch_lz4_split(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
+                                uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
+                                int stage_mask, hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    const uint64_t rs = lzh_lz4_rec_stride(chunk_size);
+    uint32_t* hdr = (uint32_t*)(recs + rs * nchunks);
+    if (stage_mask & 1)
+        hipLaunchKernelGGL(lzh_lz4_parse_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable, chunk_size,
+                           acc, recs, rs, hdr);
+    if (stage_mask & 2)
+        hipLaunchKernelGGL(lzh_lz4_emit_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable, chunk_size,
+                           (const uint8_t*)recs, rs, (const uint32_t*)hdr, stage, stride, csizes);
     return hipGetLastError();
 }
 
