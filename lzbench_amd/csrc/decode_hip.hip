@@ -383,7 +383,23 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
 // >= 64 = leaves the group, 255 = the lane itself is not taken), by binary lifting: jump tables
 // J_k = link^(2^k) through ds_bpermute, then every lane lifts from lane 0 to the furthest chain
 // lane <= itself.  No scalar walk (the decoder is scalar-issue bound).
+#ifndef LZH_DEC_WALK
+#define LZH_DEC_WALK 0
+#endif
 __device__ __forceinline__ uint64_t chain_members(int link, int lane) {
+    if (LZH_DEC_WALK) {
+        // scalar walk: one v_readlane per member (links strictly increase, so <= 64 steps)
+        uint64_t M = 0;
+        int sl = 0;
+        for (int it = 0; it < LZH_WAVE; it++) {
+            const int nx = rdlanei(link, sl);
+            if (nx == 255) break;
+            M |= 1ull << sl;
+            if (nx >= LZH_WAVE) break;
+            sl = nx;
+        }
+        return M;
+    }
     const int J0 = min(link, LZH_WAVE);
     const int J1 = J0 < LZH_WAVE ? (int)lane_gather((uint32_t)J0, J0) : LZH_WAVE;
     const int J2 = J1 < LZH_WAVE ? (int)lane_gather((uint32_t)J1, J1) : LZH_WAVE;

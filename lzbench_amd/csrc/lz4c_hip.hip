@@ -25,7 +25,12 @@ namespace lz4v3 {
 #define LZ_STAT(i, v) do { if (kStats) ctr[i] += (uint32_t)(v); } while (0)
 constexpr int kCtr = 13;
 // phase clocks (stats build only): time since the previous mark is charged to phase i
-#define LZ_CLK(i) do { if (!kStats) asm volatile("; LZMARK " #i ::: "memory"); if (kStats) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); clk[i] += t_ - clk_last; clk_last = t_; } } while (0)
+#ifdef LZH_ISA_MARKS   // phase markers in the ISA (tools: instruction counts per phase); off in builds
+#define LZ_MARK(i) asm volatile("; LZMARK " #i ::: "memory")
+#else
+#define LZ_MARK(i) ((void)0)
+#endif
+#define LZ_CLK(i) do { if (!kStats) LZ_MARK(i); if (kStats) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); clk[i] += t_ - clk_last; clk_last = t_; } } while (0)
 constexpr int kClk = 10;
 
 constexpr int kMinMatch = 4;
@@ -539,7 +544,12 @@ __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t los
         }                                                                                          \
     } while (0)
 
-template <bool kSmall, bool kStats, bool kRec = false>
+// kFast (acceleration > 1, lz4.c:958-967): run batches probe a data-independent pattern.  A search
+// from a segment origin e (a match end, re-tested, or position 0 at the chunk start) probes
+// e+1, e+2, then steps of acc for 64 probes: offsets {0, 1, 2, 2+acc, 2+2acc, ..} from e.  Run
+// batches cover the first 64 search probes of each segment (as with acc 1); later probes and the
+// chunk tail (where a probe's forwardIp could pass mflimit) go through stride batches.
+template <bool kSmall, bool kStats, bool kRec = false, bool kFast = false>
 __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab,
                                LDSA uint32_t* ringw, LDSA uint8_t* outb, uint32_t* out_size,
                                unsigned long long* stats, rsrc_t recs, uint32_t* rec_hdr) {
@@ -592,16 +602,43 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         // re-test at a match end, then 64 step-1 search probes, lz4.c:955-969 / :1148-1200);
         // pins = a pending ip-2 table fill (lz4.c:1145-1146) sitting at base.  Stride batches
         // (any other schedule): one sequence per batch, the search from s with k0 probes done.
-        bool runb = acc == 1, retest = false, go = true;
-        int base = 1, q = 1, qlim = 64, pins = -1;
+        bool runb = kFast || acc == 1, retest = false, go = true;
+        const int dlim = kFast ? 2 + 62 * acc : 64;      // last run-batch probe: segment origin + dlim
+        int base = 1, q = 1, qlim = dlim, pins = -1;
+        int so = 0;                              // segment origin (kFast pattern phase)
         int s = 1, k0 = 0;
+        // probe pattern from a segment origin (bits = offsets): PER = {0, acc, 2acc, ..}, PAT = {0, 1, 2 + PER}
+        uint64_t PER = ~0ull, PAT = ~0ull;
+        if (kFast) {
+            PER = 0;
+            for (int o = 0; o < LZH_WAVE; o += acc) PER |= 1ull << o;
+            PAT = 3ull | (PER << 2);
+        }
 
         for (int guard = 0; go && guard < 4 * n + 64; guard++) {
             runb = unii(runb) != 0; retest = unii(retest) != 0;
             base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
             op = unii(op); anchor = unii(anchor); rc_tot = unii(rc_tot); nrec = unii(nrec);
             R.fill = unii(R.fill); R.ready = unii(R.ready); O.flushed = unii(O.flushed);
+            so = unii(so);
             LZ_STAT(0, 1);
+            if (kFast && runb && base + LZH_WAVE - 1 + acc > mfl1) {
+                // near the chunk end a probe's forwardIp may pass mflimit: stride batches take over
+                // (the pending ip-2 insert first, then the re-test or the next search probe)
+                if (pins >= 0) {
+                    uint32_t w, bb = 0;
+                    if (R.has(pins - 4, pins + 12)) { w = R.u32(pins); if (!kSmall) bb = R.byte(pins + 4); }
+                    else { const uint64_t v = in.w40(pins); w = (uint32_t)v; bb = (uint32_t)(v >> 32); }
+                    const uint32_t hp = hash_of<kSmall>(w, bb);
+                    if (lane == 0) T.put(hp, (uint32_t)pins);
+                    wave_lds_fence();
+                }
+                const int d = q - so;
+                s = so + 1;
+                retest = d <= 0;
+                k0 = d <= 1 ? 0 : 1 + (d - 2 + acc - 1) / acc;
+                runb = false;
+            }
             LZ_CLK(9);                                                 // (loop overhead / uncharged)
 
             // ---- lanes -> positions
@@ -724,6 +761,19 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 const int fv = __builtin_popcountll(vmask);           // first lane past mflimit
                 const uint64_t I0 = pins >= 0 ? (1ull << (pins - base)) : 0ull;
                 const int lo = q - base, hi0 = min(qlim - base, LZH_WAVE - 1);
+                // probes of the batch's first segment (lanes lo..hi0; under kFast on the pattern)
+                uint64_t P0 = lane_bits(lo, hi0);
+                if (kFast) {
+                    const int off = so - base;
+                    uint64_t Mp;
+                    if (off >= 0) {
+                        Mp = PAT << off;
+                    } else {
+                        const int u = -off, t = ((2 - u) % acc + acc) % acc;
+                        Mp = (t < LZH_WAVE ? PER << t : 0ull) | (u == 1 ? 1ull : 0ull);
+                    }
+                    P0 &= Mp;
+                }
                 // Each lane's candidate: the latest earlier slot member that is inserted when the
                 // lane is probed (ak; -1 = the slot's old value).  Assume prev, resolve the batch,
                 // check the assumption against the resolved inserted set; repeat with corrected
@@ -742,14 +792,14 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     cn = min(le, mlimit - (p + kMinMatch));
                     const bool lng = oke && le == 20 && p + kMinMatch + 20 < mlimit;
                     e = lane + kMinMatch + cn;
-                    int f = ctz64v(e < LZH_WAVE ? (A & (~0ull << e)) : 0ull);
+                    int f = ctz64v(e < LZH_WAVE ? (A & (PAT << e)) : 0ull);
                     // chain walk (lz4.c:1142-1200: match end -> re-test -> search from ip+1)
                     Mm = 0;
                     endp = false;
                     uint64_t E;                                        // probed lanes
-                    const uint64_t r0 = A & lane_bits(lo, hi0);
+                    const uint64_t r0 = A & P0;
                     if (!r0) {
-                        E = lane_bits(lo, hi0);
+                        E = P0;
                         endp = hi0 >= fv;                              // ran past mflimit (lz4.c:969)
                     } else {
                         int sl = __builtin_ctzll(r0);
@@ -773,7 +823,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                                 es = sl + kMinMatch + c;
                                 cn = lane == sl ? c : cn;
                                 e = lane == sl ? es : e;
-                                fs = ctz64v(es < LZH_WAVE ? (A & (~0ull << es)) : 0ull);
+                                fs = ctz64v(es < LZH_WAVE ? (A & (PAT << es)) : 0ull);
                             } else {
                                 es = rdlanei(e, sl);
                             }
@@ -787,7 +837,11 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         const int j = mle ? 63 - __builtin_clzll(mle) : lane;
                         const int ej = (int)lane_gather((uint32_t)e, j);
                         const bool inside = mle && lane > j && lane < ej;
-                        E = ballot(lane >= lo && !inside && (!endip || lane < eL));
+                        bool probed = lane >= lo && !inside;
+                        if (kFast)   // before the first member: the first segment's pattern; after a
+                            probed = mle ? (lane == j || (lane >= ej && ((PAT >> ((lane - ej) & 63)) & 1ull)))
+                                         : lane_on(P0);        // member's end: its pattern
+                        E = ballot(probed && (!endip || lane < eL));
                         I = ballot(mle && lane == ej - 2);             // lz4.c:1146
                         endp = endip || (eL < LZH_WAVE && LZH_WAVE - 1 >= fv);   // or the search ran past mflimit
                     }
@@ -840,13 +894,14 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     if (Mm) {
                         const int ip = base + eL;
                         anchor = ip;
+                        so = ip;
                         if (eL < LZH_WAVE) {                           // searched to the batch end
                             q = base + LZH_WAVE;
-                            qlim = ip + LZH_WAVE;
+                            qlim = ip + dlim;
                             pins = -1;
                         } else {                                       // re-test in a later batch
                             q = ip;
-                            qlim = ip + LZH_WAVE;
+                            qlim = ip + dlim;
                             pins = eL - 2 >= LZH_WAVE ? ip - 2 : -1;
                         }
                     } else {
@@ -868,9 +923,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         if (wr) T.put(h, inI ? (uint32_t)p : old);
                     }
                     wave_lds_fence();
-                    if (!Mm && hi0 == qlim - base) {                   // step 1 exhausted: stride batches
+                    if (!Mm && hi0 == qlim - base) {                   // 64 probes done: stride batches
                         runb = false;
-                        s = qlim - 63;
+                        s = so + 1;
                         k0 = LZH_WAVE;
                         retest = false;
                     } else {
@@ -942,12 +997,13 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 anchor = ip;
                 if (ip >= mfl1) {
                     go = false;
-                } else if (acc == 1) {                                 // back to run batches
+                } else if (acc == 1 || kFast) {                        // back to run batches
                     runb = true;
                     pins = ip - 2;
                     base = ip - 2;
                     q = ip;
-                    qlim = ip + LZH_WAVE;
+                    so = ip;
+                    qlim = ip + dlim;
                 } else {   // fill table at ip-2 (lz4.c:1146), then re-test ip as lane 0
                     uint32_t w, bb = 0;
                     if (R.has(ip - 6, ip + 8)) { w = R.u32(ip - 2); if (!kSmall) bb = R.byte(ip + 2); }
@@ -1004,8 +1060,13 @@ lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_read
     LDSA uint32_t* ring = tab + 4096;
     LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
     const rsrc_t nr = make_rsrc(nullptr, 0);
-    if (n < 65547) lz4v3::compress_chunk<true, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
-    else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+    if (n < 65547) {
+        if (acc > 1) lz4v3::compress_chunk<true, false, false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+        else lz4v3::compress_chunk<true, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+    } else {
+        if (acc > 1) lz4v3::compress_chunk<false, false, false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+        else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+    }
 }
 
 // debug twin of the kernel above with event counters (tools/lz4_stats.py)
@@ -1026,8 +1087,13 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
     LDSA uint32_t* ring = tab + 4096;
     LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
     const rsrc_t nr = make_rsrc(nullptr, 0);
-    if (n < 65547) lz4v3::compress_chunk<true, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
-    else lz4v3::compress_chunk<false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+    if (n < 65547) {
+        if (acc > 1) lz4v3::compress_chunk<true, true, false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+        else lz4v3::compress_chunk<true, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+    } else {
+        if (acc > 1) lz4v3::compress_chunk<false, true, false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+        else lz4v3::compress_chunk<false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+    }
 }
 
 // ======================================================================= parse + emit split
@@ -1054,8 +1120,13 @@ lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, 
     LDSA uint32_t* ring = tab + 4096;
     const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
     uint32_t* hdr = rec_hdr + 2 * chunk;
-    if (n < 65547) lz4v3::compress_chunk<true, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
-    else lz4v3::compress_chunk<false, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+    if (n < 65547) {
+        if (acc > 1) lz4v3::compress_chunk<true, false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+        else lz4v3::compress_chunk<true, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+    } else {
+        if (acc > 1) lz4v3::compress_chunk<false, false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+        else lz4v3::compress_chunk<false, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+    }
 }
 
 namespace lz4e {

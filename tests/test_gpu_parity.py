@@ -175,13 +175,33 @@ def test_batched_rows_multi_file_chunk_list(torch_cuda):
         assert (out == data).all()
 
 
-@pytest.mark.parametrize("acc", [1, 2, 5, 17, 99])
+@pytest.mark.parametrize("acc", [1, 2, 3, 5, 17, 99])
 def test_lz4fast_levels(torch_cuda, acc):
     data = L.datagen("mixed", 8 << 20, seed=3)
     name = "lz4fast" if acc > 1 else "lz4"
     packed, cs = L.compress_chunks(data, name, 65536, level=acc)
     ep, ec = O.compress_chunks(data, name, 65536, acc)
     assert (cs == ec).all() and (packed == ep).all()
+
+
+def _runs(n, seed):
+    rng = np.random.default_rng(seed)
+    return np.repeat(rng.integers(0, 3, n // 4 + 16, dtype=np.uint8), rng.integers(1, 40, n // 4 + 16))[:n].copy()
+
+
+@pytest.mark.parametrize("acc", [2, 3, 4, 7, 64, 65, 200])
+@pytest.mark.parametrize("kind", ["text", "json", "binary", "random", "runs"])
+def test_lz4fast_pattern_batches(torch_cuda, acc, kind):
+    """Probe-pattern run batches (acc > 1) across corpora, byU16 and byU32 tables, ragged tails
+    and tiny chunks (where the tail switches to stride batches)."""
+    n = 3 << 20
+    data = _runs(n, 4) if kind == "runs" else L.datagen(kind, n, seed=11)
+    for chunk in (65536, 1 << 20, 4099, 65547):
+        packed, cs = L.compress_chunks(data, "lz4fast", chunk, level=acc)
+        ep, ec = O.compress_chunks(data, "lz4fast", chunk, acc)
+        assert (cs == ec).all() and (packed == ep).all(), (kind, acc, chunk)
+    out = L.decompress_chunks(packed, cs, len(data), "lz4", chunk)
+    assert (out == data).all()
 
 
 def test_unaligned_chunk_bases(torch_cuda):

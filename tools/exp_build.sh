@@ -8,12 +8,12 @@ out=$root/build/exp/$name
 mkdir -p $out
 cd $root/lzbench_amd/csrc
 objs=""
-for f in lz4c_hip snappyc_hip decode_hip pack_hip; do
+for f in lz4c_hip snappyc_hip decode_hip pack_hip zstdc_hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $flags -c $f.hip -o $out/$f.o &
   objs="$objs $out/$f.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $flags -x hip -c api.cpp -o $out/api.o &
 gcc -O2 -fPIC -c datagen.c -o $out/datagen.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/liblzbench_hip.so $objs $out/api.o $out/datagen.o -lm -pthread
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/liblzbench_hip.so $objs $out/api.o $out/datagen.o -lm -pthread -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
 echo built $out/liblzbench_hip.so

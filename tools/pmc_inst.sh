@@ -15,5 +15,5 @@ for v in "$@"; do
   ) > "$GRAFT_REPO_ROOT/$out/$v.p$i.log" 2>&1 || { echo "$v failed"; tail -5 "$GRAFT_REPO_ROOT/$out/$v.p$i.log"; exit 1; }
   i=$((i+1))
   done
-  echo "== $v"; python3 "$GRAFT_REPO_ROOT/tools/pmc_summary.py" "$GRAFT_REPO_ROOT/$out/$v" | grep -A16 "compress_v2\|decompress_v2"
+  echo "== $v"; python3 "$GRAFT_REPO_ROOT/tools/pmc_summary.py" "$GRAFT_REPO_ROOT/$out/$v" | grep -A16 "_kernel"
 done

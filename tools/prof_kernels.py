@@ -10,6 +10,7 @@ ap.add_argument("--chunk-kib", type=int, default=64)
 ap.add_argument("--corpus", default="text")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--decompress", action="store_true")
+ap.add_argument("--level", type=int, default=0)
 a = ap.parse_args()
 import torch
 import lzbench_amd as L
@@ -17,7 +18,7 @@ n = a.mib << 20
 host = L.datagen(a.corpus, n, seed=12345)
 d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda")
 d_in[:n].copy_(torch.from_numpy(host))
-dc = L.DeviceCodec(a.codec, n, a.chunk_kib << 10)
+dc = L.DeviceCodec(a.codec, n, a.chunk_kib << 10, level=a.level)
 dc.compress(d_in)
 torch.cuda.synchronize()
 t = time.time()
@@ -27,4 +28,4 @@ for _ in range(a.reps):
     else:
         dc.compress_kernel_only(d_in)
 torch.cuda.synchronize()
-print(f"{a.codec} {'dec' if a.decompress else 'comp'} {a.mib} MiB: {(time.time()-t)/a.reps*1e3:.2f} ms/rep, ratio {dc.packed_total()/n:.4f}", flush=True)
+print(f"{a.codec}{a.level or ''} {'dec' if a.decompress else 'comp'} {a.mib} MiB: {(time.time()-t)/a.reps*1e3:.2f} ms/rep, ratio {dc.packed_total()/n:.4f}", flush=True)
