@@ -81,7 +81,10 @@ struct Ring {
     int sh;
     int fill;
     int ready;
-    __device__ __forceinline__ bool has(int p0, int p1) const { return p0 + sh >= fill - kRing && p1 + sh <= ready; }
+    bool on = true;    // (false: no LDS ring, every read goes to memory)
+    __device__ __forceinline__ bool has(int p0, int p1) const {
+        return on && p0 + sh >= fill - kRing && p1 + sh <= ready;
+    }
     __device__ __forceinline__ uint32_t dword(int a) const {
         return ((volatile const LDSA uint32_t*)w)[(a >> 2) & (kRing / 4 - 1)];
     }
@@ -93,11 +96,16 @@ struct Ring {
         return ((volatile const LDSA uint8_t*)w)[(p + sh) & (kRing - 1)];
     }
     __device__ __forceinline__ void refill(rsrc_t r, int lane) {
+        if (!on) return;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(w + ((fill & (kRing - 1)) >> 2)), 4, fill + 4 * lane,
                                                  0, 0, 0);
         fill += 256;
     }
 };
+
+#ifndef LZH_PARSE_NORING
+#define LZH_PARSE_NORING 0   // parse kernel without the LDS input ring (16 KiB LDS: 10 waves per CU)
+#endif
 
 __device__ __forceinline__ int ext_len_bytes(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
 
@@ -573,7 +581,8 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
 #pragma unroll
         for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
     }
-    Ring R{ringw, in.sh, 0, 0};
+    constexpr bool kRingOn = !(kRec && LZH_PARSE_NORING);
+    Ring R{ringw, in.sh, 0, 0, kRingOn};
     OutRing O{outb, out.sh, 0};
     const int endX = n + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
@@ -593,7 +602,8 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         const int64_t a64 = (int64_t)acc << 6;
 
         {   // position 0 enters the table before the first search (lz4.c:922-923)
-            const uint32_t h0 = hash_of<kSmall>(R.u32(0), R.byte(4));
+            const uint64_t v0 = kRingOn ? ((uint64_t)R.u32(0) | ((uint64_t)R.byte(4) << 32)) : in.w40(0);
+            const uint32_t h0 = hash_of<kSmall>((uint32_t)v0, (uint32_t)(v0 >> 32));
             if (lane == 0) T.put(h0, 0);
             wave_lds_fence();
         }
@@ -695,6 +705,52 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             rc_m = 0;
             rc_tot = 0;
             LZ_CLK(2);                                                 // deferred emission
+            // run batch: the slot groups and the collider pre-evaluation need no candidate bytes,
+            // so they run under the candidate loads (a probe whose slot holds an earlier lane of
+            // the batch sees that lane's position if it was inserted, else the slot's old value)
+            uint64_t grp = 1ull << lane;
+            uint64_t coll = 0;
+            int prev = -1;
+            const uint64_t below = (1ull << lane) - 1ull;
+            bool okp = false;                                      // evaluation against lane prev
+            int bep = 0, lep = 0;
+            if (runb && losers) {
+                LZ_STAT(1, 1);
+                // slot groups without a loop: every lane of a slot read back the same claim
+                // winner W (whichever lane the hardware let win), so equal W <=> same slot;
+                // equality of the 6-bit W is bit-sliced over 6 ballots
+                const uint32_t W = back - (uint32_t)base;
+                uint64_t eq = vmask;
+#pragma unroll
+                for (int b = 0; b < 6; b++) {
+                    const bool wb = (W >> b) & 1u;
+                    const uint64_t bm = ballot(valid && wb);
+                    eq &= wb ? bm : ~bm;
+                }
+                grp = valid ? eq : (1ull << lane);
+                const uint64_t eb = grp & below;
+                prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
+                coll = ballot(prev >= 0);
+                // a collider's candidate is usually its closest earlier slot member: evaluate
+                // that pair once per batch (the per-step test below then only selects)
+                const int k = prev >= 0 ? prev : lane;
+                const uint32_t gm4 = lane_gather(ps.m4, k), gw = lane_gather(ps.w, k),
+                               g0 = lane_gather(ps.q0, k), g1 = lane_gather(ps.q1, k),
+                               g2 = lane_gather(ps.q2, k), g3 = lane_gather(ps.q3, k),
+                               g4 = lane_gather(ps.q4, k);
+                const uint32_t x0 = ps.q0 ^ g0, x1 = ps.q1 ^ g1, x2 = ps.q2 ^ g2, x3 = ps.q3 ^ g3,
+                               x4 = ps.q4 ^ g4;
+                int l = 20;
+                l = x4 ? 16 + (int)byte_ctz(x4) : l;
+                l = x3 ? 12 + (int)byte_ctz(x3) : l;
+                l = x2 ? 8 + (int)byte_ctz(x2) : l;
+                l = x1 ? 4 + (int)byte_ctz(x1) : l;
+                l = x0 ? (int)byte_ctz(x0) : l;
+                lep = l;
+                const uint32_t y = ps.m4 ^ gm4;
+                bep = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
+                okp = valid && gw == ps.w;
+            }
             wait_vm();
             R.ready = R.fill;
             wave_lds_fence();
@@ -711,52 +767,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
 
             if (runb) {
                 // ================= run batch: resolve every sequence that starts in the batch
-                // a probe whose slot holds an earlier lane of the batch sees that lane's position
-                // if it was inserted (probed or ip-2 filled), else the slot's old value: such
-                // "colliders" are re-evaluated per step against the in-batch candidate
-                uint64_t grp = 1ull << lane;
-                uint64_t coll = 0;
-                int prev = -1;
-                const uint64_t below = (1ull << lane) - 1ull;
-                bool okp = false;                                      // evaluation against lane prev
-                int bep = 0, lep = 0;
-                if (losers) {
-                    LZ_STAT(1, 1);
-                    // slot groups without a loop: every lane of a slot read back the same claim
-                    // winner W (whichever lane the hardware let win), so equal W <=> same slot;
-                    // equality of the 6-bit W is bit-sliced over 6 ballots
-                    const uint32_t W = back - (uint32_t)base;
-                    uint64_t eq = vmask;
-#pragma unroll
-                    for (int b = 0; b < 6; b++) {
-                        const bool wb = (W >> b) & 1u;
-                        const uint64_t bm = ballot(valid && wb);
-                        eq &= wb ? bm : ~bm;
-                    }
-                    grp = valid ? eq : (1ull << lane);
-                    const uint64_t eb = grp & below;
-                    prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
-                    coll = ballot(prev >= 0);
-                    // a collider's candidate is usually its closest earlier slot member: evaluate
-                    // that pair once per batch (the per-step test below then only selects)
-                    const int k = prev >= 0 ? prev : lane;
-                    const uint32_t gm4 = lane_gather(ps.m4, k), gw = lane_gather(ps.w, k),
-                                   g0 = lane_gather(ps.q0, k), g1 = lane_gather(ps.q1, k),
-                                   g2 = lane_gather(ps.q2, k), g3 = lane_gather(ps.q3, k),
-                                   g4 = lane_gather(ps.q4, k);
-                    const uint32_t x0 = ps.q0 ^ g0, x1 = ps.q1 ^ g1, x2 = ps.q2 ^ g2, x3 = ps.q3 ^ g3,
-                                   x4 = ps.q4 ^ g4;
-                    int l = 20;
-                    l = x4 ? 16 + (int)byte_ctz(x4) : l;
-                    l = x3 ? 12 + (int)byte_ctz(x3) : l;
-                    l = x2 ? 8 + (int)byte_ctz(x2) : l;
-                    l = x1 ? 4 + (int)byte_ctz(x1) : l;
-                    l = x0 ? (int)byte_ctz(x0) : l;
-                    lep = l;
-                    const uint32_t y = ps.m4 ^ gm4;
-                    bep = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
-                    okp = valid && gw == ps.w;
-                }
+                // ("colliders" are re-evaluated per step against the in-batch candidate)
                 LZ_CLK(4);                                             // eval + slot groups
                 const int fv = __builtin_popcountll(vmask);           // first lane past mflimit
                 const uint64_t I0 = pins >= 0 ? (1ull << (pins - base)) : 0ull;
@@ -1069,12 +1080,14 @@ lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_read
     }
 }
 
-// debug twin of the kernel above with event counters (tools/lz4_stats.py)
+// debug twin of the parse kernel with event counters and phase clocks (tools/lz4_stats.py)
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                               uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t chunk0,
                               unsigned long long* stats) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4];
+    // (the parse kernel's path: records dropped by a zero-size descriptor, header into LDS scratch)
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4];
+    __shared__ uint32_t hdr[2];
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t off = chunk * chunk_size;
     if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
@@ -1085,14 +1098,13 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
     rout.init(stage + chunk * stride, stride);
     LDSA uint32_t* tab = (LDSA uint32_t*)lds;
     LDSA uint32_t* ring = tab + 4096;
-    LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
     const rsrc_t nr = make_rsrc(nullptr, 0);
     if (n < 65547) {
-        if (acc > 1) lz4v3::compress_chunk<true, true, false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
-        else lz4v3::compress_chunk<true, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+        if (acc > 1) lz4v3::compress_chunk<true, true, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
+        else lz4v3::compress_chunk<true, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
     } else {
-        if (acc > 1) lz4v3::compress_chunk<false, true, false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
-        else lz4v3::compress_chunk<false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
+        if (acc > 1) lz4v3::compress_chunk<false, true, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
+        else lz4v3::compress_chunk<false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
     }
 }
 
@@ -1107,7 +1119,7 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                      uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + (LZH_PARSE_NORING ? 0 : lz4v3::kRing / 4)];
     const uint64_t chunk = blockIdx.x;
     const uint64_t off = chunk * chunk_size;
     if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
