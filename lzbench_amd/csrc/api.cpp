@@ -43,7 +43,7 @@ static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // LZ4 chunks up to this size compress in two kernels (parse -> 8-byte sequence records -> emit);
 // larger ones (24-bit record fields) in the single kernel that assembles the block itself
-static const size_t kLz4SplitMax = (size_t)16 << 20;
+static const size_t kLz4SplitMax = (size_t)16 << 20;   // LZ4 / snappy parse + emit split up to this chunk size
 
 extern "C" {
 
@@ -77,6 +77,8 @@ size_t lzh_compress_temp_bytes(int codec, size_t n, size_t chunk_size) {
     size_t t = align_up(k * lzh_stage_stride(codec, chunk_size), 256) + 256;
     if (codec == LZH_CODEC_LZ4 && chunk_size <= kLz4SplitMax)     // sequence records of the parse kernel
         t += k * lzh_lz4_rec_stride(chunk_size) + align_up(k * 8, 256) + 256;
+    if (codec == LZH_CODEC_SNAPPY && chunk_size <= kLz4SplitMax)
+        t += k * lzh_snappy_rec_stride(chunk_size) + align_up(k * 4, 256) + 256;
     if (codec == LZH_CODEC_ZSTD) {   // per-frame scratch of the two zstd kernels (zstdc_hip.hip), worst level
         size_t fs = 0;
         for (int lv : {1, 2, -1, -2}) fs = std::max(fs, lzh_zstd_scratch_stride(chunk_size, lv));
@@ -108,9 +110,14 @@ int lzh_compress_kernel_stage(int codec, int level, int stage_mask, const void* 
                                                  (uint8_t*)d_stage, stride, d_csizes, (uint32_t)k, s));
         }
     } else if (codec == LZH_CODEC_SNAPPY) {
-        if (stage_mask & 1)
+        if (chunk_size <= kLz4SplitMax) {
+            uint8_t* recs = (uint8_t*)d_stage + align_up(k * stride, 256) + 256;
+            LZH_CHECK(lzh_launch_snappy_split((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
+                                              stride, d_csizes, (uint32_t)k, recs, stage_mask, s));
+        } else if (stage_mask & 1) {
             LZH_CHECK(lzh_launch_snappy_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
                                                     stride, d_csizes, (uint32_t)k, s));
+        }
     } else if (codec == LZH_CODEC_ZSTD) {
         if (!lzh_zstd_level_ok(level, chunk_size)) return LZH_EARG;
         uint8_t* scratch = (uint8_t*)d_stage + align_up(k * stride, 256) + 256;

@@ -31,3 +31,7 @@ hipError_t lzh_launch_lz4_split(const uint8_t* in, uint64_t n_total, uint64_t in
                                 uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
                                 int stage_mask, hipStream_t s);
 size_t lzh_lz4_rec_stride(uint64_t chunk_size);
+hipError_t lzh_launch_snappy_split(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                                   uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
+                                   int stage_mask, hipStream_t s);
+size_t lzh_snappy_rec_stride(uint64_t chunk_size);

@@ -227,6 +227,23 @@ struct SnapSeq {
 // kept in scratch memory.)
 #define SREC_DECL uint32_t rc_anc = 0, rc_lit = 0, rc_off = 0, rc_ml = 0, rc_st = 0; uint64_t rc_m = 0; int rc_tot = 0
 #define SREC_EMIT() op = emit_recs(in, R, out, mark, op, rc_anc, rc_lit, rc_off, rc_ml, rc_st, rc_m, rc_tot, lane)
+// kRec: the sequences leave as 8-byte records (literal length | copy length << 17 | offset << 48, chunk
+// order; a literal-only record ends a fragment) for lzh_snappy_emit_kernel instead of being laid out here
+#define SREC_OUT()                                                                                 \
+    do {                                                                                           \
+        if (kRec) {                                                                                \
+            if (rc_m) {                                                                            \
+                const int ri_ = nrec + __builtin_popcountll(rc_m & ((1ull << lane) - 1ull));       \
+                if (lane_on(rc_m)) {                                                               \
+                    st_b32(recs, 8 * ri_, rc_lit | (rc_ml << 17));                                 \
+                    st_b32(recs, 8 * ri_ + 4, (rc_ml >> 15) | (rc_off << 16));                     \
+                }                                                                                  \
+                nrec += __builtin_popcountll(rc_m);                                                \
+            }                                                                                      \
+        } else {                                                                                   \
+            SREC_EMIT();                                                                           \
+        }                                                                                          \
+    } while (0)
 
 __device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const Bytes& out, LDSA uint8_t* mark, int op,
                                          uint32_t anc, uint32_t lit, uint32_t off, uint32_t ml, uint32_t st,
@@ -323,9 +340,11 @@ __device__ __forceinline__ int match_after4(const PS& a, uint32_t b1, uint32_t b
     return l;
 }
 
-// one fragment in[0, fn) appended at op
+// one fragment in[0, fn) appended at op (kRec: its records appended at nrec)
+template <bool kRec>
 __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int op, LDSA uint16_t* tab,
-                                 LDSA uint32_t* ringw, LDSA uint8_t* mark, unsigned long long* stats) {
+                                 LDSA uint32_t* ringw, LDSA uint8_t* mark, unsigned long long* stats, rsrc_t recs,
+                                 int& nrec) {
     const int lane = threadIdx.x;
     Table T{tab};
     const uint32_t tsize = table_size_for((uint32_t)fn);
@@ -401,7 +420,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
                     d6 = ld_b32(in.r, cA + 24);
                 }
-                SREC_EMIT();
+                SREC_OUT();
                 rc_m = 0;
                 rc_tot = 0;
                 wait_vm();
@@ -550,22 +569,24 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     const int anc = mb ? base + ep : next_emit;
                     const int lit = p - anc, mlen = 4 + cn;
                     const uint32_t offv = (uint32_t)(p - (int)ce);
-                    int L = 0;
-                    if (mem) { const SnapSeq Q(lit, offv, mlen); L = Q.total; }
-                    int incl = L;
-                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xf, 0xf, false);
-                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xf, 0xf, false);
-                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xf, 0xf, false);
-                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xf, 0xf, false);
-                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xa, 0xf, false);
-                    incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xc, 0xf, false);
                     rc_anc = (uint32_t)anc;
                     rc_lit = (uint32_t)lit;
                     rc_off = offv;
                     rc_ml = (uint32_t)mlen;
-                    rc_st = (uint32_t)(incl - L);
                     rc_m = Mm;
-                    rc_tot = rdlanei(incl, 63);
+                    if (!kRec) {   // output offsets: only the in-kernel emission needs them
+                        int L = 0;
+                        if (mem) { const SnapSeq Q(lit, offv, mlen); L = Q.total; }
+                        int incl = L;
+                        incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xf, 0xf, false);
+                        incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xf, 0xf, false);
+                        incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xf, 0xf, false);
+                        incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xf, 0xf, false);
+                        incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xa, 0xf, false);
+                        incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xc, 0xf, false);
+                        rc_st = (uint32_t)(incl - L);
+                        rc_tot = rdlanei(incl, 63);
+                    }
                     next_emit = base + eL;
                 }
                 if (endp) break;                                         // remainder from next_emit
@@ -644,7 +665,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
                 d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
             }
-            SREC_EMIT();
+            SREC_OUT();
             rc_m = 0;
             rc_tot = 0;
             {
@@ -775,14 +796,13 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
             len = min(len, fn - a);
             const int matched = 4 + len;
             {
-                const SnapSeq Q(P - next_emit, (uint32_t)(P - M), matched);
                 rc_anc = (uint32_t)next_emit;
                 rc_lit = (uint32_t)(P - next_emit);
                 rc_off = (uint32_t)(P - M);
                 rc_ml = (uint32_t)matched;
                 rc_st = 0;
                 rc_m = 1;
-                rc_tot = Q.total;
+                if (!kRec) rc_tot = SnapSeq(P - next_emit, (uint32_t)(P - M), matched).total;
             }
             const int ip = P + matched;
             next_emit = ip;
@@ -801,7 +821,14 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
             org = rt + 1;
         }
     }
-    SREC_EMIT();
+    SREC_OUT();
+    if (kRec) {   // the fragment's last literal run: a literal-only record
+        if (next_emit < fn) {
+            if (lane == 0) { st_b32(recs, 8 * nrec, (uint32_t)(fn - next_emit)); st_b32(recs, 8 * nrec + 4, 0u); }
+            nrec++;
+        }
+        return op;
+    }
     if (next_emit < fn) op = emit_seq(in, R, out, op, next_emit, fn - next_emit, 0, 0, lane);
     wave_lds_fence();
     return op;
@@ -834,13 +861,187 @@ lzh_snappy_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
         const uint64_t readable = min<uint64_t>(in_readable - off - fpos, (uint64_t)fn + 64);
         Bytes rin;
         rin.init(in + off + fpos, readable);
-        op = snv2::compress_fragment(rin, fn, rout, op, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13),
-                                     (LDSA uint8_t*)((LDSA uint32_t*)lds + (1 << 13) + 256), stats);
+        int nrec = 0;
+        op = snv2::compress_fragment<false>(rin, fn, rout, op, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13),
+                                            (LDSA uint8_t*)((LDSA uint32_t*)lds + (1 << 13) + 256), stats,
+                                            make_rsrc(nullptr, 0), nrec);
     }
     if (lane == 0) csizes[chunk] = (uint32_t)op;
 }
 
+// ======================================================================= parse + emit split
+// As for LZ4 (lz4c_hip.hip): the parse kernel (the loop above with kRec, no output marks) leaves
+// 8-byte records; lzh_snappy_emit_kernel (no hash table: high occupancy) writes the varint header
+// (snappy.cc:1047-1050) and lays out EmitLiteral / EmitCopy (:342-443) for 64 records at a time.
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                        uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + 256];   // table | ring
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t off = chunk * chunk_size;
+    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
+    const uint32_t n = (uint32_t)min(chunk_size, n_total - off);
+    const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
+    Bytes rout;
+    rout.init(nullptr, 0);
+    int nrec = 0;
+    for (uint32_t fpos = 0; fpos < n; fpos += 65536u) {
+        const int fn = (int)min(65536u, n - fpos);
+        const uint64_t readable = min<uint64_t>(in_readable - off - fpos, (uint64_t)fn + 64);
+        Bytes rin;
+        rin.init(in + off + fpos, readable);
+        snv2::compress_fragment<true>(rin, fn, rout, 0, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13), nullptr,
+                                      nullptr, rr, nrec);
+    }
+    if (threadIdx.x == 0) rec_hdr[chunk] = (uint32_t)nrec;
+}
+
+namespace sne {
+
+constexpr int kRingB = 2048;            // LDS output ring (bytes)
+constexpr int kSpan = 2048;             // LDS copy of a record group's input span (bytes)
+
+__device__ __forceinline__ int wave_max(int v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_excl_scan(int x, int& total) {
+    int incl = x;
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xf, 0xf, false);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xf, 0xf, false);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xf, 0xf, false);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xf, 0xf, false);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xa, 0xf, false);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xc, 0xf, false);
+    total = __builtin_amdgcn_readlane(incl, 63);
+    return incl - x;
+}
+
+struct OutR {
+    LDSA uint8_t* b;
+    rsrc_t o;          // staging slot (256-aligned)
+    int flushed;       // bytes [0, flushed) are in global memory
+    __device__ __forceinline__ void put(int pos, uint32_t v) const { ((volatile LDSA uint8_t*)b)[pos & (kRingB - 1)] = (uint8_t)v; }
+    // global <- complete dwords of [flushed, upto) (all of it when fin: the partial last dword too)
+    __device__ __forceinline__ void flush(int upto, bool fin, int lane) {
+        wave_lds_fence();
+        const int d0 = flushed >> 2, d1 = fin ? (upto + 3) >> 2 : upto >> 2;
+        for (int d = d0 + lane; d < d1; d += 64)
+            st_b32(o, 4 * d, ((volatile LDSA uint32_t*)b)[d & (kRingB / 4 - 1)]);
+        flushed = 4 * d1;
+        if (flushed > upto) flushed = upto & ~3;   // (the partial dword is rewritten by the next flush)
+        wave_lds_fence();
+    }
+};
+
+}  // namespace sne
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                       const uint8_t* recs, uint64_t rec_stride, const uint32_t* rec_hdr, uint8_t* stage,
+                       uint64_t stride, uint32_t* csizes) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[sne::kRingB];
+    __shared__ __attribute__((aligned(16))) uint32_t ibuf[sne::kSpan / 4 + 4];   // input span of a group
+    const int lane = threadIdx.x;
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t off = chunk * chunk_size;
+    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
+    const uint32_t n = (uint32_t)min(chunk_size, n_total - off);
+    Bytes in_b;
+    in_b.init(in + off, min<uint64_t>(in_readable - off, (uint64_t)n + 64));
+    const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
+    const int nrec = (int)uni(rec_hdr[chunk]);
+    sne::OutR R{(LDSA uint8_t*)ring, make_rsrc(stage + chunk * stride, (uint32_t)stride), 0};
+    int op = 0;
+    {   // varint32 uncompressed length (snappy.cc:1047-1050)
+        uint32_t v = n;
+        int nb = 1;
+        while (v >= 128) { v >>= 7; nb++; }
+        if (lane < nb) R.put(lane, ((n >> (7 * lane)) & 0x7fu) | (lane + 1 < nb ? 0x80u : 0u));
+        op = nb;
+    }
+    int ia = 0;
+    uint32_t nw0 = 0, nw1 = 0;                 // records of the next group (loaded one group ahead)
+    if (lane < nrec) { nw0 = ld_b32(rr, 8 * lane); nw1 = ld_b32(rr, 8 * lane + 4); }
+    for (int g = 0; g < nrec; g += 64) {
+        const int r = g + lane;
+        const bool v = r < nrec;
+        const uint32_t w0 = nw0, w1 = nw1;
+        if (r + 64 < nrec) { nw0 = ld_b32(rr, 8 * (r + 64)); nw1 = ld_b32(rr, 8 * (r + 64) + 4); }
+        const int lit = v ? (int)(w0 & 0x1FFFFu) : 0;
+        const int ml = v ? (int)((w0 >> 17) | ((w1 & 0xFFFFu) << 15)) : 0;
+        const uint32_t o = w1 >> 16;
+        const snv2::SnapSeq Q(lit, o, ml);
+        const int S = v ? Q.total : 0;
+        const int L = lit + ml;
+        int T, Lt;
+        const int pos = op + sne::wave_excl_scan(S, T);
+        const int anc = ia + sne::wave_excl_scan(L, Lt);
+        const int Smax = (int)uni((uint32_t)sne::wave_max(S));
+        if (T <= sne::kRingB / 2 && Smax <= 64 && Lt + 8 <= sne::kSpan) {
+            // the group's input span [ia, ia + Lt) into LDS (literal bytes are read from there)
+            const int X0 = (ia + in_b.sh) & ~3;
+            const int nd = (ia + in_b.sh + Lt - X0 + 3) >> 2;
+            for (int d = lane; d < nd; d += 64) ibuf[d] = ld_b32(in_b.r, X0 + 4 * d);
+            wave_lds_fence();
+            const LDSA uint8_t* ib = (const LDSA uint8_t*)ibuf;
+            const int ioff = in_b.sh - X0;            // input position p lives at ib[p + ioff]
+            if (op + T - R.flushed > sne::kRingB - 8) R.flush(op, false, lane);
+            // every lane writes its own (literal, copy) pair, byte t of it at pass t
+            for (int t = 0; t < Smax; t++) {
+                if (t < S) {
+                    const int li = t - Q.lit0;
+                    const uint32_t lb = (li >= 0 && li < lit) ? (uint32_t)ib[anc + li + ioff] : 0u;
+                    R.put(pos + t, Q.byte(t, lb));
+                }
+            }
+            op += T;
+            if (op - R.flushed >= sne::kRingB / 2) R.flush(op, false, lane);
+            wave_lds_fence();
+        } else {
+            for (int k = 0; k < 64 && g + k < nrec; k++) {
+                const int kl = rdlanei(lit, k), km = rdlanei(ml, k), ka = rdlanei(anc, k);
+                const uint32_t ko = rdlane(o, k);
+                const snv2::SnapSeq K(kl, ko, km);
+                for (int b = 0; b < K.total; b += 64) {
+                    if (op + b + 64 - R.flushed > sne::kRingB) R.flush(op + b, false, lane);
+                    const int t = b + lane;
+                    const int li = t - K.lit0;
+                    const uint32_t lb = (li >= 0 && li < kl) ? in_b.b(ka + li) : 0u;
+                    if (t < K.total) R.put(op + t, K.byte(t, lb));
+                }
+                op += K.total;
+            }
+        }
+        ia += Lt;
+    }
+    R.flush(op, true, lane);
+    if (lane == 0) csizes[chunk] = (uint32_t)op;
+}
+
 #include "launch.h"
+size_t lzh_snappy_rec_stride(uint64_t chunk_size) {
+    return ((chunk_size / 4 + chunk_size / 65536 + 8) * 8 + 255) / 256 * 256;
+}
+
+// parse kernel + emit kernel (records: nchunks x rec_stride bytes, then a u32 count per chunk);
+// stage_mask bit 0 = parse, bit 1 = emit
+hipError_t lzh_launch_snappy_split(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                                   uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
+                                   int stage_mask, hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    const uint64_t rs = lzh_snappy_rec_stride(chunk_size);
+    uint32_t* hdr = (uint32_t*)(recs + rs * nchunks);
+    if (stage_mask & 1)
+        hipLaunchKernelGGL(lzh_snappy_parse_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable,
+                           chunk_size, recs, rs, hdr);
+    if (stage_mask & 2)
+        hipLaunchKernelGGL(lzh_snappy_emit_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable,
+                           chunk_size, (const uint8_t*)recs, rs, (const uint32_t*)hdr, stage, stride, csizes);
+    return hipGetLastError();
+}
+
 hipError_t lzh_launch_snappy_compress_v2(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                                          uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
                                          hipStream_t s) {
