@@ -27,6 +27,9 @@ namespace snv2 {
 #define SN_STAT(i, v) do { if (stats && lane == 0) atomicAdd(&stats[i], (unsigned long long)(v)); } while (0)
 
 constexpr int kRing = 1024;
+#ifndef LZH_SN_PARSE_NORING
+#define LZH_SN_PARSE_NORING 0   // parse kernel without the LDS input ring (32 KiB LDS: 5 waves per CU)
+#endif
 constexpr int kAhead = 704;
 constexpr int kRT = 16;
 constexpr uint64_t kPat0 = 0x55555555ffffffffull;   // probe offsets 0..63 of a search (0..32, 34, .., 62)
@@ -45,7 +48,10 @@ struct Ring {
     int sh;
     int fill;
     int ready;    // fill level known to have landed (refills are issued after a batch's load wait)
-    __device__ __forceinline__ bool has(int p0, int p1) const { return p0 + sh >= fill - kRing && p1 + sh <= ready; }
+    bool on = true;    // (false: no LDS ring, every read goes to memory)
+    __device__ __forceinline__ bool has(int p0, int p1) const {
+        return on && p0 + sh >= fill - kRing && p1 + sh <= ready;
+    }
     __device__ __forceinline__ uint32_t dword(int a) const {
         return ((volatile const LDSA uint32_t*)w)[(a >> 2) & (kRing / 4 - 1)];
     }
@@ -57,6 +63,7 @@ struct Ring {
         return ((volatile const LDSA uint8_t*)w)[(p + sh) & (kRing - 1)];
     }
     __device__ __forceinline__ void refill(rsrc_t r, int lane) {
+        if (!on) return;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(w + ((fill & (kRing - 1)) >> 2)), 4, fill + 4 * lane,
                                                  0, 0, 0);
         fill += 256;
@@ -354,7 +361,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
         const int nvec = (int)(tsize * 2 / 16);
         for (int i = lane; i < nvec; i += LZH_WAVE) lds_zero16(t4 + 4 * i);
     }
-    Ring R{ringw, in.sh, 0, 0};
+    Ring R{ringw, in.sh, 0, 0, !(kRec && LZH_SN_PARSE_NORING)};
     const int endX = fn + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
     wait_vm();
@@ -423,20 +430,8 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 SREC_OUT();
                 rc_m = 0;
                 rc_tot = 0;
-                wait_vm();
-                R.ready = R.fill;
-                wave_lds_fence();
-                {
-                    const int target = min(base + in.sh + kAhead, endX + 256);
-                    for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
-                }
-                const uint32_t cs = (uint32_t)(cand + in.sh) & 3u;
-                const bool ok = __builtin_amdgcn_alignbyte(d1, d0, cs) == ps.w;
-                const int len = match_after4(ps, __builtin_amdgcn_alignbyte(d2, d1, cs),
-                                             __builtin_amdgcn_alignbyte(d3, d2, cs),
-                                             __builtin_amdgcn_alignbyte(d4, d3, cs),
-                                             __builtin_amdgcn_alignbyte(d5, d4, cs),
-                                             __builtin_amdgcn_alignbyte(d6, d5, cs));
+                // (the slot groups and the collider pre-evaluation need no candidate bytes: they
+                // run under the candidate loads)
                 // slot groups: every lane of a slot read back the same claim winner
                 const uint64_t below = (1ull << lane) - 1ull;
                 uint64_t grp = 1ull << lane, coll = 0;
@@ -463,6 +458,20 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                                        lane_gather(ps.q4, k), lane_gather(ps.q5, k));
                     okp = gw == ps.w;
                 }
+                wait_vm();
+                R.ready = R.fill;
+                wave_lds_fence();
+                {
+                    const int target = min(base + in.sh + kAhead, endX + 256);
+                    for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
+                }
+                const uint32_t cs = (uint32_t)(cand + in.sh) & 3u;
+                const bool ok = __builtin_amdgcn_alignbyte(d1, d0, cs) == ps.w;
+                const int len = match_after4(ps, __builtin_amdgcn_alignbyte(d2, d1, cs),
+                                             __builtin_amdgcn_alignbyte(d3, d2, cs),
+                                             __builtin_amdgcn_alignbyte(d4, d3, cs),
+                                             __builtin_amdgcn_alignbyte(d5, d4, cs),
+                                             __builtin_amdgcn_alignbyte(d6, d5, cs));
                 // resolve (as the LZ4 kernel): assume each collider's candidate is its closest
                 // earlier slot member, walk, verify against the inserted set, repeat if needed
                 int ak = prev;
@@ -877,7 +886,7 @@ lzh_snappy_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 extern "C" __global__ void __launch_bounds__(64)
 lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                         uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + 256];   // table | ring
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + (LZH_SN_PARSE_NORING ? 0 : 256)];   // table | ring
     const uint64_t chunk = blockIdx.x;
     const uint64_t off = chunk * chunk_size;
     if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
