@@ -42,7 +42,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BASELINE_METRIC = "comp+decomp MB/s, lz4 -b64 on 1 GiB; ratio + bit-exact vs CPU ref"
 COMPRESS_KERNEL = {"lz4": "lzh_lz4_parse_kernel", "lz4fast": "lzh_lz4_parse_kernel",
-                   "snappy": "lzh_snappy_compress_v2_kernel",
+                   "snappy": "lzh_snappy_parse_kernel",
                    "zstd": "lzh_zstd_match_kernel+lzh_zstd_entropy_kernel"}
 DECOMPRESS_KERNEL = {"zstd": "lzh_zstd_decompress_kernel"}
 
@@ -297,7 +297,7 @@ def main():
         e[0].record(stream)
         codec.compress_stage(d_in, 1)            # parse kernel: the dominant kernel (roofline)
         e[1].record(stream)
-        codec.compress_stage(d_in, 2)            # LZ4 block emission from the parse records
+        codec.compress_stage(d_in, 2)            # block emission (LZ4 / snappy) from the parse records
         e[4].record(stream)
         codec.compress_finish(d_in)              # size scan + packing (raw-store rule)
         e[2].record(stream)

@@ -105,8 +105,9 @@ int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, s
                              size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream);
 
 /* One stage of lzh_compress_kernel_only (profiling, roofline of one kernel): stage_mask bit 0 =
- * the parse kernel (LZ4: sequence records; snappy / zstd: the whole codec), bit 1 = the LZ4
- * block-emission kernel (records -> staging slots and sizes).  Both bits = lzh_compress_kernel_only. */
+ * the parse kernel (LZ4 / snappy: sequence records, chunks up to 16 MiB; zstd: the whole codec),
+ * bit 1 = the LZ4 / snappy block-emission kernel (records -> staging slots and sizes).  Both
+ * bits = lzh_compress_kernel_only. */
 int lzh_compress_kernel_stage(int codec, int level, int stage_mask, const void* d_in, size_t n, size_t in_readable,
                               size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream);
 
