@@ -528,8 +528,8 @@ __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t los
             const int ep_ = (int)lane_gather((uint32_t)pr_e, jp_);                                 \
             const int anc_ = mb_ ? pr_base + ep_ : pr_anchor;                                      \
             const int maxb_ = min(p_ - anc_, (int)pr_ce);                                          \
-            int bk_ = min(pr_be, maxb_);                                                           \
-            const bool scu_ = mem_ && pr_be == 4 && maxb_ > 4;                                     \
+            int bk_ = kRec ? 0 : min(pr_be, maxb_);   /* kRec: catch-up in the emission kernel */  \
+            const bool scu_ = !kRec && mem_ && pr_be == 4 && maxb_ > 4;                            \
             for (uint64_t sm_ = ballot(scu_); sm_; sm_ &= sm_ - 1) {                               \
                 LZ_STAT(5, 1);                                                                     \
                 const int k_ = __builtin_ctzll(sm_);                                               \
@@ -992,8 +992,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 const int P = rdlanei(p, fh);
                 const int M = rdlanei((int)cand, fh);
                 int cnt;
-                const int bk = finish_match<kStats>(in, P, M, rdlanei(bkr, fh), rdlanei(len, fh), anchor, mlimit, cnt,
-                                                    lane, ctr);
+                int bk = finish_match<kStats>(in, P, M, kRec ? 0 : rdlanei(bkr, fh), rdlanei(len, fh), anchor, mlimit,
+                                              cnt, lane, ctr);
+                if (kRec) bk = 0;   // (catch-up in the emission kernel)
                 {
                     const int lit = P - bk - anchor, mlx = bk + cnt;
                     rc_anc = (uint32_t)anchor;
@@ -1153,6 +1154,12 @@ __device__ __forceinline__ int wave_max(int v) {
 }
 
 __device__ __forceinline__ int ext_len(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+
+// bytes [p-4, p) as a dword, byte p-1 the most significant; bytes before 0 read as 0
+__device__ __forceinline__ uint32_t u32_before(const Bytes& in, int p) {
+    if (p >= 4) return in.w32(p - 4);
+    return p <= 0 ? 0u : in.w32(0) << (8 * (4 - p));
+}
 __device__ __forceinline__ int wave_excl_scan(int x, int lane, int& total) {
     int incl = lz4v3::wave_incl_scan(x);
     total = __builtin_amdgcn_readlane(incl, 63);
@@ -1231,12 +1238,29 @@ lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, u
         const bool v = r < nrec;
         const uint32_t w0 = nw0, w1 = nw1;
         if (r + 64 < nrec) { nw0 = ld_b32(rr, 8 * (r + 64)); nw1 = ld_b32(rr, 8 * (r + 64) + 4); }
-        const int lit = (int)(w0 & 0xFFFFFFu), mlx = (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8)), o = (int)(w1 >> 16);
-        const int S = v ? 3 + lit + lz4e::ext_len(lit) + lz4e::ext_len(mlx) : 0;
+        // records carry the sequence before catch-up (the parse kernel defers it): literals up to
+        // the match start P found by the search, match length past P+4
+        int lit = (int)(w0 & 0xFFFFFFu), mlx = (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8));
+        const int o = (int)(w1 >> 16);
         const int L = v ? lit + 4 + mlx : 0;
         int T, Lt;
-        const int pos = op + lz4e::wave_excl_scan(S, lane, T);
         const int anc = ia + lz4e::wave_excl_scan(L, lane, Lt);
+        {   // catch-up (lz4.c:1017-1020): extend the match backwards while ip > anchor, match > start
+            const int P = anc + lit, M = P - o;
+            const int maxb = min(lit, M);
+            if (v && maxb > 0) {
+                const uint32_t x = lz4e::u32_before(in_b, P) ^ lz4e::u32_before(in_b, M);
+                int bk = x ? (int)((uint32_t)__builtin_clz(x) >> 3) : 4;
+                bk = min(bk, maxb);
+                if (bk == 4) {                                   // (rare) past the first 4 bytes
+                    while (bk < maxb && in_b.b(P - 1 - bk) == in_b.b(M - 1 - bk)) bk++;
+                }
+                lit -= bk;
+                mlx += bk;
+            }
+        }
+        const int S = v ? 3 + lit + lz4e::ext_len(lit) + lz4e::ext_len(mlx) : 0;
+        const int pos = op + lz4e::wave_excl_scan(S, lane, T);
         const int Smax = (int)uni((uint32_t)lz4e::wave_max(S));
         if (T <= lz4e::kRingB / 2 && Smax <= 64 && Lt + 8 <= lz4e::kSpan) {
             // the group's input span [ia, ia + Lt) into LDS (literal bytes are read from there)
