@@ -242,8 +242,9 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     uint64_t rc_m = 0;                                                                             \
     int rc_tot = 0
 #define RECS_EMIT() op = emit_recs(in, R, out, O, op, rc_anc, rc_lit, rc_off, rc_mlx, rc_st, rc_m, rc_tot, lane)
-// kRec: the batch's sequences leave as records (literals | match length - 4 << 24 | offset << 48, one
-// u64 per sequence, chunk order) for lzh_lz4_emit_kernel instead of being assembled here
+// kRec: the batch's sequences leave as records (match start P | match length - 4 << 24 | offset << 48,
+// one u64 per sequence, chunk order, before catch-up) for lzh_lz4_emit_kernel instead of being
+// assembled here; the literal run of a record starts at the previous record's match end
 #define RECS_OUT()                                                                                 \
     do {                                                                                           \
         if (kRec) {                                                                                \
@@ -538,7 +539,7 @@ __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t los
             }                                                                                      \
             const int lit_ = p_ - bk_ - anc_, mlx_ = bk_ + pr_cn;                                  \
             rc_anc = (uint32_t)anc_;                                                               \
-            rc_lit = (uint32_t)lit_;                                                               \
+            rc_lit = kRec ? (uint32_t)p_ : (uint32_t)lit_;   /* kRec: the match start P */        \
             rc_off = (uint32_t)(p_ - (int)pr_ce);                                                  \
             rc_mlx = (uint32_t)mlx_;                                                               \
             rc_m = pr_m;                                                                           \
@@ -998,7 +999,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 {
                     const int lit = P - bk - anchor, mlx = bk + cnt;
                     rc_anc = (uint32_t)anchor;
-                    rc_lit = (uint32_t)lit;
+                    rc_lit = kRec ? (uint32_t)P : (uint32_t)lit;   // kRec: the match start P
                     rc_off = (uint32_t)(P - M);
                     rc_mlx = (uint32_t)mlx;
                     rc_st = 0;
@@ -1238,13 +1239,18 @@ lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, u
         const bool v = r < nrec;
         const uint32_t w0 = nw0, w1 = nw1;
         if (r + 64 < nrec) { nw0 = ld_b32(rr, 8 * (r + 64)); nw1 = ld_b32(rr, 8 * (r + 64) + 4); }
-        // records carry the sequence before catch-up (the parse kernel defers it): literals up to
-        // the match start P found by the search, match length past P+4
-        int lit = (int)(w0 & 0xFFFFFFu), mlx = (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8));
+        // records carry the sequence before catch-up (the parse kernel defers it): the match start
+        // P found by the search and the match length past P+4; the literals run from the previous
+        // record's match end (lane-1 by a wave shift; the previous group's end for lane 0)
+        const int Pm = (int)(w0 & 0xFFFFFFu);
+        int mlx = (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8));
         const int o = (int)(w1 >> 16);
-        const int L = v ? lit + 4 + mlx : 0;
-        int T, Lt;
-        const int anc = ia + lz4e::wave_excl_scan(L, lane, Lt);
+        const int end = Pm + 4 + mlx;
+        const int anc = __builtin_amdgcn_update_dpp(ia, end, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        int lit = Pm - anc;
+        const int nv = min(64, nrec - g);
+        const int Lt = rdlanei(end, nv - 1) - ia;
+        int T;
         {   // catch-up (lz4.c:1017-1020): extend the match backwards while ip > anchor, match > start
             const int P = anc + lit, M = P - o;
             const int maxb = min(lit, M);
