@@ -690,14 +690,14 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             const uint32_t h = hash_of<kSmall>(ps.w, b4);
             LZ_CLK(0);                                                 // lanes -> positions, P side, hash
             const uint32_t old = T.get(h);
+            uint32_t cand = old;
+            MWin W;
+            W.load(in, cand, valid);                                   // (issued before the claim round trip)
             if (LZH_BRFREE && vmask == ~0ull) T.put(h, (uint32_t)p);   // (no exec-mask juggling)
             else if (valid) T.put(h, (uint32_t)p);
             wave_lds_fence();
             const uint32_t back = T.get(h);
             const uint64_t losers = ballot(valid && back != (uint32_t)p);
-            uint32_t cand = old;
-            MWin W;
-            W.load(in, cand, valid);
             LZ_CLK(1);                                                 // table read/claim/read back, loads issued
             // ---- deferred records + emission of the previous batch (under the loads above)
             pr_m = uni64(pr_m); pr_base = unii(pr_base); pr_anchor = unii(pr_anchor);
