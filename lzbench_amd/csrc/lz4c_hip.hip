@@ -1251,29 +1251,33 @@ lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, u
         const int nv = min(64, nrec - g);
         const int Lt = rdlanei(end, nv - 1) - ia;
         int T;
-        {   // catch-up (lz4.c:1017-1020): extend the match backwards while ip > anchor, match > start
-            const int P = anc + lit, M = P - o;
-            const int maxb = min(lit, M);
-            if (v && maxb > 0) {
-                const uint32_t x = lz4e::u32_before(in_b, P) ^ lz4e::u32_before(in_b, M);
-                int bk = x ? (int)((uint32_t)__builtin_clz(x) >> 3) : 4;
-                bk = min(bk, maxb);
-                if (bk == 4) {                                   // (rare) past the first 4 bytes
-                    while (bk < maxb && in_b.b(P - 1 - bk) == in_b.b(M - 1 - bk)) bk++;
-                }
-                lit -= bk;
-                mlx += bk;
+        // the catch-up operands and the group's input span [ia, ia + Lt) (literal bytes are read
+        // from LDS) are loaded together: one memory wait per group
+        const int M = Pm - o;
+        const int maxb = min(lit, M);
+        uint32_t xp = 0, xm = 0;
+        if (v && maxb > 0) { xp = lz4e::u32_before(in_b, Pm); xm = lz4e::u32_before(in_b, M); }
+        const bool span = Lt + 8 <= lz4e::kSpan;
+        const int X0 = (ia + in_b.sh) & ~3;
+        if (span) {
+            const int nd = (ia + in_b.sh + Lt - X0 + 3) >> 2;
+            for (int d = lane; d < nd; d += 64) ibuf[d] = ld_b32(in_b.r, X0 + 4 * d);
+            wave_lds_fence();
+        }
+        if (v && maxb > 0) {   // catch-up (lz4.c:1017-1020): extend the match backwards while ip > anchor, match > start
+            const uint32_t x = xp ^ xm;
+            int bk = x ? (int)((uint32_t)__builtin_clz(x) >> 3) : 4;
+            bk = min(bk, maxb);
+            if (bk == 4) {                                   // (rare) past the first 4 bytes
+                while (bk < maxb && in_b.b(Pm - 1 - bk) == in_b.b(M - 1 - bk)) bk++;
             }
+            lit -= bk;
+            mlx += bk;
         }
         const int S = v ? 3 + lit + lz4e::ext_len(lit) + lz4e::ext_len(mlx) : 0;
         const int pos = op + lz4e::wave_excl_scan(S, lane, T);
         const int Smax = (int)uni((uint32_t)lz4e::wave_max(S));
-        if (T <= lz4e::kRingB / 2 && Smax <= 64 && Lt + 8 <= lz4e::kSpan) {
-            // the group's input span [ia, ia + Lt) into LDS (literal bytes are read from there)
-            const int X0 = (ia + in_b.sh) & ~3;
-            const int nd = (ia + in_b.sh + Lt - X0 + 3) >> 2;
-            for (int d = lane; d < nd; d += 64) ibuf[d] = ld_b32(in_b.r, X0 + 4 * d);
-            wave_lds_fence();
+        if (T <= lz4e::kRingB / 2 && Smax <= 64 && span) {
             const LDSA uint8_t* ib = (const LDSA uint8_t*)ibuf;
             const int ioff = ia + in_b.sh - X0 - ia;   // input position p lives at ib[p + ioff]
             // every lane writes its own sequence, byte t of it at pass t
