@@ -400,14 +400,14 @@ __device__ __forceinline__ uint64_t chain_members(int link, int lane) {
         }
         return M;
     }
+    // (every member takes >= 2 stream bytes -- a snappy literal tag + 1 byte or a COPY_1, LZ4 >= 3 --
+    // so a chain from lane 0 has at most 32 members: jumps of 1..16 reach every one of them)
     const int J0 = min(link, LZH_WAVE);
     const int J1 = J0 < LZH_WAVE ? (int)lane_gather((uint32_t)J0, J0) : LZH_WAVE;
     const int J2 = J1 < LZH_WAVE ? (int)lane_gather((uint32_t)J1, J1) : LZH_WAVE;
     const int J3 = J2 < LZH_WAVE ? (int)lane_gather((uint32_t)J2, J2) : LZH_WAVE;
     const int J4 = J3 < LZH_WAVE ? (int)lane_gather((uint32_t)J3, J3) : LZH_WAVE;
-    const int J5 = J4 < LZH_WAVE ? (int)lane_gather((uint32_t)J4, J4) : LZH_WAVE;
     int x = 0, y;
-    y = (int)lane_gather((uint32_t)J5, x); x = y <= lane ? y : x;
     y = (int)lane_gather((uint32_t)J4, x); x = y <= lane ? y : x;
     y = (int)lane_gather((uint32_t)J3, x); x = y <= lane ? y : x;
     y = (int)lane_gather((uint32_t)J2, x); x = y <= lane ? y : x;
