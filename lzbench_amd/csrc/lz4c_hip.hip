@@ -82,6 +82,7 @@ struct Ring {
     int fill;
     int ready;
     bool on = true;    // (false: no LDS ring, every read goes to memory)
+    bool mirror = false;   // the ring's first 32 bytes are mirrored past its end (reads never wrap)
     __device__ __forceinline__ bool has(int p0, int p1) const {
         return on && p0 + sh >= fill - kRing && p1 + sh <= ready;
     }
@@ -99,6 +100,8 @@ struct Ring {
         if (!on) return;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(w + ((fill & (kRing - 1)) >> 2)), 4, fill + 4 * lane,
                                                  0, 0, 0);
+        if (mirror && (fill & (kRing - 1)) == 0 && lane < 8)   // the same 32 bytes into the mirror
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(w + kRing / 4), 4, fill + 4 * lane, 0, 0, 0);
         fill += 256;
     }
 };
@@ -334,6 +337,25 @@ __device__ __forceinline__ PSide p_side_ring(const Ring& R, int p) {
     const uint32_t s = (uint32_t)X & 3u;
     const uint32_t a0 = R.dword(A), a1 = R.dword(A + 4), a2 = R.dword(A + 8), a3 = R.dword(A + 12),
                    a4 = R.dword(A + 16), a5 = R.dword(A + 20), a6 = R.dword(A + 24), a7 = R.dword(A + 28);
+    PSide v;
+    v.m4 = __builtin_amdgcn_alignbyte(a1, a0, s);
+    v.w = __builtin_amdgcn_alignbyte(a2, a1, s);
+    v.q0 = __builtin_amdgcn_alignbyte(a3, a2, s);
+    v.q1 = __builtin_amdgcn_alignbyte(a4, a3, s);
+    v.q2 = __builtin_amdgcn_alignbyte(a5, a4, s);
+    v.q3 = __builtin_amdgcn_alignbyte(a6, a5, s);
+    v.q4 = __builtin_amdgcn_alignbyte(a7, a6, s);
+    return v;
+}
+
+// the same from a mirrored ring: one base address, immediate offsets, no wrap (kM4: the word at
+// p-4, needed only for an in-kernel catch-up)
+template <bool kM4>
+__device__ __forceinline__ PSide p_side_ring_m(const Ring& R, int p) {
+    const int X = p - 4 + R.sh;
+    const uint32_t s = (uint32_t)X & 3u;
+    const volatile LDSA uint32_t* q = (const volatile LDSA uint32_t*)R.w + ((X & (kRing - 1)) >> 2);
+    const uint32_t a0 = kM4 ? q[0] : 0u, a1 = q[1], a2 = q[2], a3 = q[3], a4 = q[4], a5 = q[5], a6 = q[6], a7 = q[7];
     PSide v;
     v.m4 = __builtin_amdgcn_alignbyte(a1, a0, s);
     v.w = __builtin_amdgcn_alignbyte(a2, a1, s);
@@ -583,7 +605,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
     }
     constexpr bool kRingOn = !(kRec && LZH_PARSE_NORING);
-    Ring R{ringw, in.sh, 0, 0, kRingOn};
+    Ring R{ringw, in.sh, 0, 0, kRingOn, kRec};   // (the parse kernel's ring carries a 32-byte mirror)
     OutRing O{outb, out.sh, 0};
     const int endX = n + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
@@ -681,7 +703,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             PSide ps;
             uint32_t b4 = 0;
             if (R.has(front - 4, pmax + 28)) {
-                ps = p_side_ring(R, p);
+                ps = kRec ? p_side_ring_m<false>(R, p) : p_side_ring(R, p);
             } else {
                 LZ_STAT(9, 1);
                 ps = p_side_global(in, p);
@@ -1088,7 +1110,7 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
                               uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t chunk0,
                               unsigned long long* stats) {
     // (the parse kernel's path: records dropped by a zero-size descriptor, header into LDS scratch)
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + 8];
     __shared__ uint32_t hdr[2];
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t off = chunk * chunk_size;
@@ -1121,7 +1143,7 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                      uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + (LZH_PARSE_NORING ? 0 : lz4v3::kRing / 4)];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + (LZH_PARSE_NORING ? 0 : lz4v3::kRing / 4 + 8)];   // table | ring + mirror
     const uint64_t chunk = blockIdx.x;
     const uint64_t off = chunk * chunk_size;
     if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
