@@ -409,6 +409,22 @@ struct MWin {
 
 __device__ __forceinline__ uint32_t byte_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x) >> 3; }
 
+// v_ffbl_b32: index of the lowest set bit, ~0 for 0 (the hardware result, no zero select)
+__device__ __forceinline__ uint32_t ffbl_hw(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// index of the first differing byte of two 20-byte windows given their word XORs (20 if none):
+// a zero word's v_ffbl is ~0, so the min over "4k + first set byte of word k" picks the first
+// nonzero word without a select chain
+__device__ __forceinline__ int first_diff20(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t x4) {
+    const uint32_t f0 = ffbl_hw(x0) >> 3, f1 = (ffbl_hw(x1) >> 3) + 4, f2 = (ffbl_hw(x2) >> 3) + 8,
+                   f3 = (ffbl_hw(x3) >> 3) + 12, f4 = (ffbl_hw(x4) >> 3) + 16;
+    return (int)min(min(min(f0, f1), min(f2, f3)), min(f4, 20u));
+}
+
 // returns ok; sets bkr (0..4) and len (0..20)
 __device__ __forceinline__ bool eval_lane(const PSide& P, const MWin& W, bool valid, int& bkr, int& len) {
     const uint32_t s = (uint32_t)W.sm;
@@ -419,12 +435,7 @@ __device__ __forceinline__ bool eval_lane(const PSide& P, const MWin& W, bool va
     const uint32_t x2 = P.q2 ^ __builtin_amdgcn_alignbyte(W.d5, W.d4, s);
     const uint32_t x3 = P.q3 ^ __builtin_amdgcn_alignbyte(W.d6, W.d5, s);
     const uint32_t x4 = P.q4 ^ __builtin_amdgcn_alignbyte(W.d7, W.d6, s);
-    int l = 20;
-    l = x4 ? 16 + (int)byte_ctz(x4) : l;
-    l = x3 ? 12 + (int)byte_ctz(x3) : l;
-    l = x2 ? 8 + (int)byte_ctz(x2) : l;
-    l = x1 ? 4 + (int)byte_ctz(x1) : l;
-    l = x0 ? (int)byte_ctz(x0) : l;
+    const int l = first_diff20(x0, x1, x2, x3, x4);
     len = l;
     const uint32_t y = P.m4 ^ mm4;
     bkr = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
@@ -743,14 +754,16 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 // winner W (whichever lane the hardware let win), so equal W <=> same slot;
                 // equality of the 6-bit W is bit-sliced over 6 ballots
                 const uint32_t W = back - (uint32_t)base;
-                uint64_t eq = vmask;
+                uint32_t ne0 = 0, ne1 = 0;                         // lanes whose winner differs in a bit
 #pragma unroll
                 for (int b = 0; b < 6; b++) {
-                    const bool wb = (W >> b) & 1u;
-                    const uint64_t bm = ballot(valid && wb);
-                    eq &= wb ? bm : ~bm;
+                    const uint64_t bm = ballot((W >> b) & 1u);
+                    const uint32_t mine = (uint32_t)__builtin_amdgcn_sbfe((int)W, b, 1);   // 0 / ~0
+                    ne0 |= (uint32_t)bm ^ mine;
+                    ne1 |= (uint32_t)(bm >> 32) ^ mine;
                 }
-                grp = valid ? eq : (1ull << lane);
+                const uint64_t ne = ((uint64_t)ne1 << 32) | ne0;
+                grp = valid ? (~ne & vmask) : (1ull << lane);
                 const uint64_t eb = grp & below;
                 prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
                 coll = ballot(prev >= 0);
@@ -763,12 +776,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                                g4 = lane_gather(ps.q4, k);
                 const uint32_t x0 = ps.q0 ^ g0, x1 = ps.q1 ^ g1, x2 = ps.q2 ^ g2, x3 = ps.q3 ^ g3,
                                x4 = ps.q4 ^ g4;
-                int l = 20;
-                l = x4 ? 16 + (int)byte_ctz(x4) : l;
-                l = x3 ? 12 + (int)byte_ctz(x3) : l;
-                l = x2 ? 8 + (int)byte_ctz(x2) : l;
-                l = x1 ? 4 + (int)byte_ctz(x1) : l;
-                l = x0 ? (int)byte_ctz(x0) : l;
+                const int l = first_diff20(x0, x1, x2, x3, x4);
                 lep = l;
                 const uint32_t y = ps.m4 ^ gm4;
                 bep = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
@@ -903,12 +911,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         if (far) {
                             const uint32_t x0 = ps.q0 ^ g0, x1 = ps.q1 ^ g1, x2 = ps.q2 ^ g2, x3 = ps.q3 ^ g3,
                                            x4 = ps.q4 ^ g4;
-                            int l = 20;
-                            l = x4 ? 16 + (int)byte_ctz(x4) : l;
-                            l = x3 ? 12 + (int)byte_ctz(x3) : l;
-                            l = x2 ? 8 + (int)byte_ctz(x2) : l;
-                            l = x1 ? 4 + (int)byte_ctz(x1) : l;
-                            l = x0 ? (int)byte_ctz(x0) : l;
+                            const int l = first_diff20(x0, x1, x2, x3, x4);
                             le = l;
                             const uint32_t y = ps.m4 ^ gm4;
                             be = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
