@@ -1301,26 +1301,31 @@ lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, u
         }
         const int S = v ? 3 + lit + lz4e::ext_len(lit) + lz4e::ext_len(mlx) : 0;
         const int pos = op + lz4e::wave_excl_scan(S, lane, T);
-        const int Smax = (int)uni((uint32_t)lz4e::wave_max(S));
-        if (T <= lz4e::kRingB / 2 && Smax <= 64 && span) {
+        const int litv = v ? lit : 0;
+        const int litmax = (int)uni((uint32_t)lz4e::wave_max(litv));
+        if (T <= lz4e::kRingB / 2 && litmax <= 64 && span) {
             const LDSA uint8_t* ib = (const LDSA uint8_t*)ibuf;
             const int ioff = ia + in_b.sh - X0 - ia;   // input position p lives at ib[p + ioff]
-            // every lane writes its own sequence, byte t of it at pass t
+            // every lane writes its own sequence (lz4.c:1022-1135): token, one literal-length byte
+            // when lit >= 15 (lit <= 64 here), the literals (a lane-parallel copy as long as the
+            // group's longest run), offset, match-length bytes
             if (op + T - R.flushed > lz4e::kRingB - 8) R.flush(op, false, lane);
             const int lx = lz4e::ext_len(lit), mx = lz4e::ext_len(mlx);
             const uint32_t token = ((uint32_t)min(lit, 15) << 4) | (uint32_t)min(mlx, 15);
-            const int lit0 = 1 + lx, lit1 = lit0 + lit;
-            for (int t = 0; t < Smax; t++) {
-                if (t < S) {
-                    uint32_t b = token;
-                    if (t >= 1 && t < lit0) b = t == lx ? (uint32_t)(lit - 15) % 255u : 255u;
-                    else if (t >= lit0 && t < lit1) b = ib[anc + t - lit0 + ioff];
-                    else if (t == lit1) b = (uint32_t)o & 0xffu;
-                    else if (t == lit1 + 1) b = (uint32_t)o >> 8;
-                    else if (t > lit1 + 1) b = (t - lit1 - 2 == mx - 1) ? (uint32_t)(mlx - 15) % 255u : 255u;
-                    R.put(pos + t, b);
-                }
+            const int lp = pos + 1 + lx;
+            if (v) {
+                R.put(pos, token);
+                if (lx) R.put(pos + 1, (uint32_t)(lit - 15));
             }
+            for (int t = 0; t < litmax; t++)
+                if (t < litv) R.put(lp + t, ib[anc + t + ioff]);
+            const int mp = lp + lit;
+            if (v) {
+                R.put(mp, (uint32_t)o & 0xffu);
+                R.put(mp + 1, (uint32_t)o >> 8);
+            }
+            for (int t = 0; ballot(v && t < mx); t++)
+                if (v && t < mx) R.put(mp + 2 + t, t == mx - 1 ? (uint32_t)(mlx - 15) % 255u : 255u);
             op += T;
             if (op - R.flushed >= lz4e::kRingB / 2) R.flush(op, false, lane);
             wave_lds_fence();
