@@ -304,9 +304,9 @@ __device__ __forceinline__ int wave_incl_max(int x) {
 // (byte-by-byte semantics); a literal-only member has mlk = 0, a copy-only member litk = 0.
 // One output byte per lane per pass; the owner is the last start mark at or before the byte.
 template <class W, class SinkType>
-__device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t* mark, int ip, int op,
-                                           int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
-                                           int off, int lane) {
+__device__ __forceinline__ void emit_group1(const W& w, SinkType& O, LDSA uint8_t* mark, int ip, int op,
+                                            int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
+                                            int off, int lane) {
     const bool kmem = lane_on(keep);
     int carry = 63 - __builtin_clzll(keep);                      // (pass 0 always has a start at 0)
     const uint32_t xl = ((uint32_t)excl << 10) | lrel;           // (lrel < 1024, excl < 2^22)
@@ -376,6 +376,113 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
             dm |= ballot(ready);
         }
         O.maybe_flush(min(pbase + LZH_WAVE, op + total), lane);
+    }
+}
+
+
+#ifndef LZH_DEC_PAIR
+#define LZH_DEC_PAIR 1
+#endif
+// Output byte ob of a group from its owner's fields (literal from the stream window, match byte
+// from the LDS window / flushed output); done = final now (not an unresolved in-pass source).
+template <class W, class SinkType>
+__device__ __forceinline__ uint32_t owned_byte(const W& w, const SinkType& O, int ip, int op, int pbase, int pass_bytes,
+                                               int ob, int total, uint32_t a, uint32_t xk, int offk, int& src,
+                                               bool& done, bool& far) {
+    const uint32_t b = xk & 1023u;
+    const int ek = (int)(xk >> 10);
+    const int litk = (int)(a & 0xffffu);
+    const bool act = ob < total;
+    const int u = ob - ek;
+    const bool is_lit = u < litk;
+    const uint32_t lb = w.lane_byte(ip + (int)b + (is_lit ? u : 0));
+    const int mu = u - litk;
+    const int mstart = op + ek + litk;
+    src = mstart - offk + mu;
+    if (ballot(act && !is_lit && mu >= offk)) {                    // overlapping copy: period offk
+        const int md = (int)((uint32_t)mu % (uint32_t)max(offk, 1));
+        src = (!is_lit && mu >= offk) ? mstart - offk + md : src;
+    }
+    const bool near = !is_lit && src >= O.ringlo && src >= pbase + pass_bytes - SinkType::kWin;
+    const bool inpass = !is_lit && src >= pbase;
+    const uint32_t g = O.get(src);
+    done = is_lit || (near && !inpass);
+    far = act && !is_lit && !near;
+    return is_lit ? lb : g;
+}
+
+// Two output bytes per lane per pass (128-byte passes): a byte pair has at most two owners (the
+// member owning its first byte, and one starting at its second), so each pass gathers two sets of
+// member fields instead of one per 64 bytes.  Marks: 128 bytes + 64 bytes of scratch.
+template <class W, class SinkType>
+__device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t* mark, int ip, int op,
+                                           int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
+                                           int off, int lane) {
+    if (!LZH_DEC_PAIR) {
+        emit_group1(w, O, mark, ip, op, total, keep, excl, pA, lrel, off, lane);
+        return;
+    }
+    constexpr int kP = 2 * LZH_WAVE;
+    const bool kmem = lane_on(keep);
+    int carry = 63 - __builtin_clzll(keep);                      // (pass 0 always has a start at 0)
+    const uint32_t xl = ((uint32_t)excl << 10) | lrel;           // (lrel < 1024, excl < 2^22)
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int pb = 0; pb < total; pb += kP) {
+        ((volatile LDSA uint16_t*)mark)[lane] = 0xffffu;
+        wave_lds_fence();
+        const bool mine = kmem && excl >= pb && excl < pb + kP;
+        mark[mine ? excl - pb : kP + lane] = (uint8_t)lane;
+        wave_lds_fence();
+        const uint32_t mm = ((volatile LDSA uint16_t*)mark)[lane];
+        const uint32_t m0 = mm & 0xffu, m1 = mm >> 8;
+        // owner of the lane's first byte: its own mark, else the last mark of an earlier lane
+        const uint64_t lt = ballot(mm != 0xffffu) & below;
+        const int js = lt ? 63 - __builtin_clzll(lt) : lane;
+        const uint32_t mj = lane_gather(mm, js);
+        const int prevk = lt ? (int)((mj >> 8) != 0xffu ? (mj >> 8) : (mj & 0xffu)) : carry;
+        const int k0 = m0 != 0xffu ? (int)m0 : prevk;
+        const int k1 = m1 != 0xffu ? (int)m1 : k0;
+        carry = rdlanei(k1, 63);
+        const uint32_t a0 = lane_gather(pA, k0), x0 = lane_gather(xl, k0);
+        const int f0 = (int)lane_gather((uint32_t)off, k0);
+        uint32_t a1 = a0, x1 = x0;
+        int f1 = f0;
+        if (ballot(k1 != k0)) {
+            a1 = lane_gather(pA, k1);
+            x1 = lane_gather(xl, k1);
+            f1 = (int)lane_gather((uint32_t)off, k1);
+        }
+        const int pbase = op + pb;
+        const int ob0 = pb + 2 * lane, ob1 = ob0 + 1;
+        int src0, src1;
+        bool done0, done1, far0, far1;
+        uint32_t v0 = owned_byte(w, O, ip, op, pbase, kP, ob0, total, a0, x0, f0, src0, done0, far0);
+        uint32_t v1 = owned_byte(w, O, ip, op, pbase, kP, ob1, total, a1, x1, f1, src1, done1, far1);
+        if (ballot(far0 || far1)) {   // far sources were flushed long ago: their stores must be done
+            wait_vm();
+            const uint32_t g0 = O.out.b_sc1(far0 ? src0 : 0), g1 = O.out.b_sc1(far1 ? src1 : 0);
+            v0 = far0 ? g0 : v0;
+            v1 = far1 ? g1 : v1;
+            done0 = done0 || far0;
+            done1 = done1 || far1;
+        }
+        O.put(op + ob0, v0);
+        O.put(op + ob1, v1);
+        // in-pass sources: rounds until every byte read a finished source
+        uint64_t dm0 = ballot(done0 || ob0 >= total), dm1 = ballot(done1 || ob1 >= total);
+        for (int r = 0; r < kP && (~dm0 | ~dm1); r++) {
+            const int s0 = src0 - pbase, s1 = src1 - pbase;
+            const bool rd0 = !lane_on(dm0) && (((s0 & 1 ? dm1 : dm0) >> ((s0 >> 1) & 63)) & 1ull);
+            const bool rd1 = !lane_on(dm1) && (((s1 & 1 ? dm1 : dm0) >> ((s1 >> 1) & 63)) & 1ull);
+            const uint32_t g0 = O.get(src0), g1 = O.get(src1);
+            v0 = rd0 ? g0 : v0;
+            v1 = rd1 ? g1 : v1;
+            O.put(op + ob0, v0);
+            O.put(op + ob1, v1);
+            dm0 |= ballot(rd0);
+            dm1 |= ballot(rd1);
+        }
+        O.maybe_flush(min(pbase + kP, op + total), lane);
     }
 }
 
@@ -598,7 +705,7 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
                          const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                          int32_t* status, uint32_t chunk0) {
     // output window | start marks | input ring
-    __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + 2 * LZH_WAVE + kRingBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + 3 * LZH_WAVE + kRingBytes];
     const int lane = threadIdx.x;
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t ooff = chunk * chunk_size;
@@ -617,7 +724,7 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
     } else {
         owin::Sink O{(LDSA uint8_t*)win, rout, 0, 0};
         LDSA uint8_t* mark = (LDSA uint8_t*)win + owin::kW;
-        LDSA uint8_t* ring = mark + 2 * LZH_WAVE;
+        LDSA uint8_t* ring = mark + 3 * LZH_WAVE;
         r = codec == 0 ? groups::lz4_decode(rin, cs, O, mark, ring, part, lane)
                        : groups::snappy_decode(rin, cs, O, mark, ring, part, lane);
         if (r > 0) O.flush(r, lane);
@@ -693,7 +800,7 @@ __device__ __forceinline__ uint32_t c_sym(Cell c) { return c >> 18; }
 
 // per-wave LDS
 struct Lds {
-    uint8_t win[kZW + 2 * LZH_WAVE];     // output window | start marks (groups::emit_group)
+    uint8_t win[kZW + 3 * LZH_WAVE];     // output window | start marks + scratch (groups::emit_group)
     uint16_t huf[1 << kHufLogMax];      // Huffman decoding table: symbol | nbBits << 8
     Cell ll[512], ml[512], of[256];     // sequence FSE tables (ZSTD_seqSymbol's fields, packed)
     Cell wt[64];                       // FSE table of the Huffman weights (accuracy <= 6)
