@@ -381,29 +381,26 @@ __device__ __forceinline__ void emit_group1(const W& w, SinkType& O, LDSA uint8_
 
 
 #ifndef LZH_DEC_PAIR
-#define LZH_DEC_PAIR 1
+#define LZH_DEC_PAIR 1   // 0: one byte per lane per pass (emit_group1)
 #endif
-// Output byte ob of a group from its owner's fields (literal from the stream window, match byte
-// from the LDS window / flushed output); done = final now (not an unresolved in-pass source).
+// Output byte ob (group-relative) from its owner's fields, precomputed per member so that a byte
+// costs adds and compares only: lend = the owner's literal end (group-relative), lsb = stream
+// position of its literal byte at ob = lsb + ob, msrc = absolute output position of its match
+// source at ob = msrc + ob (byte-by-byte semantics; overlapping copies take the period form).
+// done = final now (not an unresolved in-pass source); far = source only in global memory.
 template <class W, class SinkType>
-__device__ __forceinline__ uint32_t owned_byte(const W& w, const SinkType& O, int ip, int op, int pbase, int pass_bytes,
-                                               int ob, int total, uint32_t a, uint32_t xk, int offk, int& src,
-                                               bool& done, bool& far) {
-    const uint32_t b = xk & 1023u;
-    const int ek = (int)(xk >> 10);
-    const int litk = (int)(a & 0xffffu);
+__device__ __forceinline__ uint32_t owned_byte(const W& w, const SinkType& O, int op, int pbase, int thr, int ob,
+                                               int total, int lend, int lsb, int msrc, int offk, int& src, bool& done,
+                                               bool& far) {
     const bool act = ob < total;
-    const int u = ob - ek;
-    const bool is_lit = u < litk;
-    const uint32_t lb = w.lane_byte(ip + (int)b + (is_lit ? u : 0));
-    const int mu = u - litk;
-    const int mstart = op + ek + litk;
-    src = mstart - offk + mu;
-    if (ballot(act && !is_lit && mu >= offk)) {                    // overlapping copy: period offk
-        const int md = (int)((uint32_t)mu % (uint32_t)max(offk, 1));
-        src = (!is_lit && mu >= offk) ? mstart - offk + md : src;
+    const bool is_lit = ob < lend;
+    const uint32_t lb = w.lane_byte(lsb + (is_lit ? ob : lend - 1));
+    src = msrc + ob;
+    if (ballot(act && !is_lit && ob >= lend + offk)) {             // overlapping copy: period offk
+        const int md = (int)((uint32_t)(ob - lend) % (uint32_t)max(offk, 1));
+        src = (!is_lit && ob >= lend + offk) ? op + lend - offk + md : src;
     }
-    const bool near = !is_lit && src >= O.ringlo && src >= pbase + pass_bytes - SinkType::kWin;
+    const bool near = !is_lit && src >= O.ringlo && src >= thr;
     const bool inpass = !is_lit && src >= pbase;
     const uint32_t g = O.get(src);
     done = is_lit || (near && !inpass);
@@ -425,7 +422,10 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
     constexpr int kP = 2 * LZH_WAVE;
     const bool kmem = lane_on(keep);
     int carry = 63 - __builtin_clzll(keep);                      // (pass 0 always has a start at 0)
-    const uint32_t xl = ((uint32_t)excl << 10) | lrel;           // (lrel < 1024, excl < 2^22)
+    // per member: literal end, literal stream base, match source base (see owned_byte)
+    const int m_lend = excl + (int)(pA & 0xffffu);
+    const int m_lsb = ip + (int)lrel - excl;
+    const int m_msrc = op - off;
     const uint64_t below = (1ull << lane) - 1ull;
     for (int pb = 0; pb < total; pb += kP) {
         ((volatile LDSA uint16_t*)mark)[lane] = 0xffffu;
@@ -443,21 +443,22 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
         const int k0 = m0 != 0xffu ? (int)m0 : prevk;
         const int k1 = m1 != 0xffu ? (int)m1 : k0;
         carry = rdlanei(k1, 63);
-        const uint32_t a0 = lane_gather(pA, k0), x0 = lane_gather(xl, k0);
-        const int f0 = (int)lane_gather((uint32_t)off, k0);
-        uint32_t a1 = a0, x1 = x0;
-        int f1 = f0;
+        const int le0 = (int)lane_gather((uint32_t)m_lend, k0), ls0 = (int)lane_gather((uint32_t)m_lsb, k0),
+                  ms0 = (int)lane_gather((uint32_t)m_msrc, k0), of0 = (int)lane_gather((uint32_t)off, k0);
+        int le1 = le0, ls1 = ls0, ms1 = ms0, of1 = of0;
         if (ballot(k1 != k0)) {
-            a1 = lane_gather(pA, k1);
-            x1 = lane_gather(xl, k1);
-            f1 = (int)lane_gather((uint32_t)off, k1);
+            le1 = (int)lane_gather((uint32_t)m_lend, k1);
+            ls1 = (int)lane_gather((uint32_t)m_lsb, k1);
+            ms1 = (int)lane_gather((uint32_t)m_msrc, k1);
+            of1 = (int)lane_gather((uint32_t)off, k1);
         }
         const int pbase = op + pb;
+        const int thr = pbase + kP - SinkType::kWin;               // sources below: overwritten in the window
         const int ob0 = pb + 2 * lane, ob1 = ob0 + 1;
         int src0, src1;
         bool done0, done1, far0, far1;
-        uint32_t v0 = owned_byte(w, O, ip, op, pbase, kP, ob0, total, a0, x0, f0, src0, done0, far0);
-        uint32_t v1 = owned_byte(w, O, ip, op, pbase, kP, ob1, total, a1, x1, f1, src1, done1, far1);
+        uint32_t v0 = owned_byte(w, O, op, pbase, thr, ob0, total, le0, ls0, ms0, of0, src0, done0, far0);
+        uint32_t v1 = owned_byte(w, O, op, pbase, thr, ob1, total, le1, ls1, ms1, of1, src1, done1, far1);
         if (ballot(far0 || far1)) {   // far sources were flushed long ago: their stores must be done
             wait_vm();
             const uint32_t g0 = O.out.b_sc1(far0 ? src0 : 0), g1 = O.out.b_sc1(far1 ? src1 : 0);
