@@ -30,6 +30,11 @@ __device__ __forceinline__ uint32_t ld_b32(rsrc_t r, int off) { return __builtin
 __device__ __forceinline__ uint32_t ld_u8(rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0); }
 __device__ __forceinline__ void st_u8(rsrc_t r, int off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0); }
 __device__ __forceinline__ void st_b32(rsrc_t r, int off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0); }
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_b64(rsrc_t r, int off, uint32_t lo, uint32_t hi) {
+    const u32x2 v = {lo, hi};
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 0);
+}
 
 // unaligned little-endian 32-bit read at byte position pos (>= 0) from two aligned dwords
 __device__ __forceinline__ uint32_t ld_u32(rsrc_t r, int pos) {
@@ -47,7 +52,7 @@ __device__ __forceinline__ uint64_t ld_u40(rsrc_t r, int pos) {
     return (uint64_t)v | ((uint64_t)b4 << 32);
 }
 
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }   // (the lane mask itself: no v_cndmask / v_cmp round trip through a VGPR)
 // this lane's bit of a wave-uniform lane mask (the inverse of ballot: one v_cndmask on the SGPR
 // pair instead of a 64-bit shift, mask and compare per lane)
 __device__ __forceinline__ bool lane_on(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }

@@ -171,7 +171,8 @@ struct SinkT {
     // out[op + t] = out[op - off + t] for t < len (byte by byte semantics), 0 < off <= op
     __device__ __forceinline__ void match(int op, int off, int len, int lane) {
         const int src0 = op - off;
-        if (src0 >= ringlo && off <= KW - LZH_WAVE) {
+        // (reach kWin - 128: the group emitter may have written up to 127 bytes past its end)
+        if (src0 >= ringlo && off <= KW - 2 * LZH_WAVE) {
             for (int base = 0; base < len; base += LZH_WAVE) {
                 const int t = base + lane;
                 const int s = off >= LZH_WAVE ? src0 + t : src0 + (int)((uint32_t)t % (uint32_t)off);
@@ -467,6 +468,8 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
             done0 = done0 || far0;
             done1 = done1 || far1;
         }
+        // (bytes past the group's end land in window slots at most 127 bytes past it, which no
+        // later reader takes as near: the next group's threshold, SinkT::match's kWin - 128 reach)
         O.put(op + ob0, v0);
         O.put(op + ob1, v1);
         // in-pass sources: rounds until every byte read a finished source

@@ -251,13 +251,13 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 #define RECS_OUT()                                                                                 \
     do {                                                                                           \
         if (kRec) {                                                                                \
-            if (rc_m) {                                                                            \
-                const int ri_ = nrec + __builtin_popcountll(rc_m & ((1ull << lane) - 1ull));       \
-                if (lane_on(rc_m)) {                                                               \
-                    st_b32(recs, 8 * ri_, rc_lit | (rc_mlx << 24));                                \
-                    st_b32(recs, 8 * ri_ + 4, (rc_mlx >> 8) | (rc_off << 16));                     \
-                }                                                                                  \
-                nrec += __builtin_popcountll(rc_m);                                                \
+            const uint64_t rm_ = uni64(rc_m);   /* (wave-uniform: keep it in SGPRs) */             \
+            if (rm_) {                                                                             \
+                const int ri_ = nrec + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(rm_ >> 32),       \
+                                           __builtin_amdgcn_mbcnt_lo((uint32_t)rm_, 0u));          \
+                if (lane_on(rm_))                                                                  \
+                    st_b64(recs, 8 * ri_, rc_lit | (rc_mlx << 24), (rc_mlx >> 8) | (rc_off << 16));  \
+                nrec = unii(nrec + __builtin_popcountll(rm_));                                     \
             }                                                                                      \
         } else {                                                                                   \
             RECS_EMIT();                                                                           \

@@ -241,10 +241,8 @@ struct SnapSeq {
         if (kRec) {                                                                                \
             if (rc_m) {                                                                            \
                 const int ri_ = nrec + __builtin_popcountll(rc_m & ((1ull << lane) - 1ull));       \
-                if (lane_on(rc_m)) {                                                               \
-                    st_b32(recs, 8 * ri_, rc_lit | (rc_ml << 17));                                 \
-                    st_b32(recs, 8 * ri_ + 4, (rc_ml >> 15) | (rc_off << 16));                     \
-                }                                                                                  \
+                if (lane_on(rc_m))                                                                 \
+                    st_b64(recs, 8 * ri_, rc_lit | (rc_ml << 17), (rc_ml >> 15) | (rc_off << 16));   \
                 nrec += __builtin_popcountll(rc_m);                                                \
             }                                                                                      \
         } else {                                                                                   \
