@@ -52,6 +52,22 @@ __device__ __forceinline__ uint64_t ld_u40(rsrc_t r, int pos) {
     return (uint64_t)v | ((uint64_t)b4 << 32);
 }
 
+// v_ffbl_b32: index of the lowest set bit, ~0 for 0 (the hardware result, no zero select)
+__device__ __forceinline__ uint32_t ffbl_hw(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// index of the first differing byte of two 20-byte windows given their word XORs (20 if none):
+// a zero word's v_ffbl is ~0, so the min over "4k + first set byte of word k" picks the first
+// nonzero word without a select chain
+__device__ __forceinline__ int first_diff20(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t x4) {
+    const uint32_t f0 = ffbl_hw(x0) >> 3, f1 = (ffbl_hw(x1) >> 3) + 4, f2 = (ffbl_hw(x2) >> 3) + 8,
+                   f3 = (ffbl_hw(x3) >> 3) + 12, f4 = (ffbl_hw(x4) >> 3) + 16;
+    return (int)min(min(min(f0, f1), min(f2, f3)), min(f4, 20u));
+}
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }   // (the lane mask itself: no v_cndmask / v_cmp round trip through a VGPR)
 // this lane's bit of a wave-uniform lane mask (the inverse of ballot: one v_cndmask on the SGPR
 // pair instead of a 64-bit shift, mask and compare per lane)

@@ -49,6 +49,7 @@ struct Ring {
     int fill;
     int ready;    // fill level known to have landed (refills are issued after a batch's load wait)
     bool on = true;    // (false: no LDS ring, every read goes to memory)
+    bool mirror = false;   // the ring's first 32 bytes are mirrored past its end (reads never wrap)
     __device__ __forceinline__ bool has(int p0, int p1) const {
         return on && p0 + sh >= fill - kRing && p1 + sh <= ready;
     }
@@ -66,6 +67,8 @@ struct Ring {
         if (!on) return;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(w + ((fill & (kRing - 1)) >> 2)), 4, fill + 4 * lane,
                                                  0, 0, 0);
+        if (mirror && (fill & (kRing - 1)) == 0 && lane < 8)   // the same 32 bytes into the mirror
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(w + kRing / 4), 4, fill + 4 * lane, 0, 0, 0);
         fill += 256;
     }
 };
@@ -239,11 +242,13 @@ struct SnapSeq {
 #define SREC_OUT()                                                                                 \
     do {                                                                                           \
         if (kRec) {                                                                                \
-            if (rc_m) {                                                                            \
-                const int ri_ = nrec + __builtin_popcountll(rc_m & ((1ull << lane) - 1ull));       \
-                if (lane_on(rc_m))                                                                 \
+            const uint64_t rm_ = uni64(rc_m);   /* (wave-uniform: keep it in SGPRs) */             \
+            if (rm_) {                                                                             \
+                const int ri_ = nrec + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(rm_ >> 32),       \
+                                           __builtin_amdgcn_mbcnt_lo((uint32_t)rm_, 0u));          \
+                if (lane_on(rm_))                                                                  \
                     st_b64(recs, 8 * ri_, rc_lit | (rc_ml << 17), (rc_ml >> 15) | (rc_off << 16));   \
-                nrec += __builtin_popcountll(rc_m);                                                \
+                nrec = unii(nrec + __builtin_popcountll(rm_));                                     \
             }                                                                                      \
         } else {                                                                                   \
             SREC_EMIT();                                                                           \
@@ -316,7 +321,10 @@ __device__ __forceinline__ PS p_side(const Ring& R, const Bytes& in, bool ring, 
     const int X = (ring ? p + R.sh : p + in.sh), A = X & ~3;
     const uint32_t s = (uint32_t)X & 3u;
     uint32_t a0, a1, a2, a3, a4, a5, a6;
-    if (ring) {
+    if (ring && R.mirror) {   // one base address, immediate offsets (the mirror absorbs the wrap)
+        const volatile LDSA uint32_t* q = (const volatile LDSA uint32_t*)R.w + ((A & (kRing - 1)) >> 2);
+        a0 = q[0]; a1 = q[1]; a2 = q[2]; a3 = q[3]; a4 = q[4]; a5 = q[5]; a6 = q[6];
+    } else if (ring) {
         a0 = R.dword(A); a1 = R.dword(A + 4); a2 = R.dword(A + 8); a3 = R.dword(A + 12);
         a4 = R.dword(A + 16); a5 = R.dword(A + 20); a6 = R.dword(A + 24);
     } else {
@@ -335,14 +343,7 @@ __device__ __forceinline__ PS p_side(const Ring& R, const Bytes& in, bool ring, 
 // bytes matched after the first 4 (0..20) between two 24-byte windows
 __device__ __forceinline__ int match_after4(const PS& a, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t b4,
                                             uint32_t b5) {
-    const uint32_t x1 = a.q1 ^ b1, x2 = a.q2 ^ b2, x3 = a.q3 ^ b3, x4 = a.q4 ^ b4, x5 = a.q5 ^ b5;
-    int l = 20;
-    l = x5 ? 16 + (int)byte_ctz(x5) : l;
-    l = x4 ? 12 + (int)byte_ctz(x4) : l;
-    l = x3 ? 8 + (int)byte_ctz(x3) : l;
-    l = x2 ? 4 + (int)byte_ctz(x2) : l;
-    l = x1 ? (int)byte_ctz(x1) : l;
-    return l;
+    return first_diff20(a.q1 ^ b1, a.q2 ^ b2, a.q3 ^ b3, a.q4 ^ b4, a.q5 ^ b5);
 }
 
 // one fragment in[0, fn) appended at op (kRec: its records appended at nrec)
@@ -359,7 +360,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
         const int nvec = (int)(tsize * 2 / 16);
         for (int i = lane; i < nvec; i += LZH_WAVE) lds_zero16(t4 + 4 * i);
     }
-    Ring R{ringw, in.sh, 0, 0, !(kRec && LZH_SN_PARSE_NORING)};
+    Ring R{ringw, in.sh, 0, 0, !(kRec && LZH_SN_PARSE_NORING), kRec};   // (parse kernel: mirrored ring)
     const int endX = fn + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
     wait_vm();
@@ -413,18 +414,18 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 const PS ps = p_side(R, in, ring, p);
                 const uint32_t h = (ps.w * 0x1e35a7bdu) >> shift;
                 const uint32_t old = T.get(h);
-                T.put(h, (uint32_t)p);
-                wave_lds_fence();
-                const uint32_t back = T.get(h);
-                const uint64_t losers = ballot(back != (uint32_t)p);
                 const uint32_t cand = old;
                 uint32_t d0, d1, d2, d3, d4, d5, d6;
-                {
+                {   // (the candidate window loads are issued before the claim round trip)
                     const int cX = (int)cand + in.sh, cA = cX & ~3;
                     d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
                     d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
                     d6 = ld_b32(in.r, cA + 24);
                 }
+                T.put(h, (uint32_t)p);
+                wave_lds_fence();
+                const uint32_t back = T.get(h);
+                const uint64_t losers = ballot(back != (uint32_t)p);
                 SREC_OUT();
                 rc_m = 0;
                 rc_tot = 0;
@@ -439,14 +440,15 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 if (losers) {
                     SN_STAT(1, 1);
                     const uint32_t W = back - (uint32_t)base;
-                    uint64_t eq = ~0ull;
+                    uint32_t ne0 = 0, ne1 = 0;                     // lanes whose winner differs in a bit
 #pragma unroll
                     for (int b = 0; b < 6; b++) {
-                        const bool wb = (W >> b) & 1u;
-                        const uint64_t bm = ballot(wb);
-                        eq &= wb ? bm : ~bm;
+                        const uint64_t bm = ballot((W >> b) & 1u);
+                        const uint32_t mine = (uint32_t)__builtin_amdgcn_sbfe((int)W, b, 1);   // 0 / ~0
+                        ne0 |= (uint32_t)bm ^ mine;
+                        ne1 |= (uint32_t)(bm >> 32) ^ mine;
                     }
-                    grp = eq;
+                    grp = ~(((uint64_t)ne1 << 32) | ne0);
                     const uint64_t eb = grp & below;
                     prev = eb ? 63 - __builtin_clzll(eb) : -1;
                     coll = ballot(prev >= 0);
@@ -884,7 +886,7 @@ lzh_snappy_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 extern "C" __global__ void __launch_bounds__(64)
 lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                         uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + (LZH_SN_PARSE_NORING ? 0 : 256)];   // table | ring
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + (LZH_SN_PARSE_NORING ? 0 : 256 + 8)];   // table | ring + mirror
     const uint64_t chunk = blockIdx.x;
     const uint64_t off = chunk * chunk_size;
     if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
