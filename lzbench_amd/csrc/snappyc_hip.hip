@@ -237,8 +237,10 @@ struct SnapSeq {
 // kept in scratch memory.)
 #define SREC_DECL uint32_t rc_anc = 0, rc_lit = 0, rc_off = 0, rc_ml = 0, rc_st = 0; uint64_t rc_m = 0; int rc_tot = 0
 #define SREC_EMIT() op = emit_recs(in, R, out, mark, op, rc_anc, rc_lit, rc_off, rc_ml, rc_st, rc_m, rc_tot, lane)
-// kRec: the sequences leave as 8-byte records (literal length | copy length << 17 | offset << 48, chunk
-// order; a literal-only record ends a fragment) for lzh_snappy_emit_kernel instead of being laid out here
+// kRec: the sequences leave as 8-byte records (copy start P in the chunk | copy length << 24 | offset << 48,
+// chunk order; a literal-only record, copy length 0 at P = its end, ends a fragment) for
+// lzh_snappy_emit_kernel instead of being laid out here; a record's literal run starts at the previous
+// record's end
 #define SREC_OUT()                                                                                 \
     do {                                                                                           \
         if (kRec) {                                                                                \
@@ -247,7 +249,7 @@ struct SnapSeq {
                 const int ri_ = nrec + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(rm_ >> 32),       \
                                            __builtin_amdgcn_mbcnt_lo((uint32_t)rm_, 0u));          \
                 if (lane_on(rm_))                                                                  \
-                    st_b64(recs, 8 * ri_, rc_lit | (rc_ml << 17), (rc_ml >> 15) | (rc_off << 16));   \
+                    st_b64(recs, 8 * ri_, rc_lit | (rc_ml << 24), (rc_ml >> 8) | (rc_off << 16));    \
                 nrec = unii(nrec + __builtin_popcountll(rm_));                                     \
             }                                                                                      \
         } else {                                                                                   \
@@ -350,7 +352,7 @@ __device__ __forceinline__ int match_after4(const PS& a, uint32_t b1, uint32_t b
 template <bool kRec>
 __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int op, LDSA uint16_t* tab,
                                  LDSA uint32_t* ringw, LDSA uint8_t* mark, unsigned long long* stats, rsrc_t recs,
-                                 int& nrec) {
+                                 int& nrec, int fbase) {
     const int lane = threadIdx.x;
     Table T{tab};
     const uint32_t tsize = table_size_for((uint32_t)fn);
@@ -579,7 +581,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     const int lit = p - anc, mlen = 4 + cn;
                     const uint32_t offv = (uint32_t)(p - (int)ce);
                     rc_anc = (uint32_t)anc;
-                    rc_lit = (uint32_t)lit;
+                    rc_lit = kRec ? (uint32_t)(fbase + p) : (uint32_t)lit;   // kRec: the copy start P
                     rc_off = offv;
                     rc_ml = (uint32_t)mlen;
                     rc_m = Mm;
@@ -806,7 +808,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
             const int matched = 4 + len;
             {
                 rc_anc = (uint32_t)next_emit;
-                rc_lit = (uint32_t)(P - next_emit);
+                rc_lit = kRec ? (uint32_t)(fbase + P) : (uint32_t)(P - next_emit);
                 rc_off = (uint32_t)(P - M);
                 rc_ml = (uint32_t)matched;
                 rc_st = 0;
@@ -833,7 +835,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
     SREC_OUT();
     if (kRec) {   // the fragment's last literal run: a literal-only record
         if (next_emit < fn) {
-            if (lane == 0) { st_b32(recs, 8 * nrec, (uint32_t)(fn - next_emit)); st_b32(recs, 8 * nrec + 4, 0u); }
+            if (lane == 0) st_b64(recs, 8 * nrec, (uint32_t)(fbase + fn), 0u);
             nrec++;
         }
         return op;
@@ -873,7 +875,7 @@ lzh_snappy_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
         int nrec = 0;
         op = snv2::compress_fragment<false>(rin, fn, rout, op, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13),
                                             (LDSA uint8_t*)((LDSA uint32_t*)lds + (1 << 13) + 256), stats,
-                                            make_rsrc(nullptr, 0), nrec);
+                                            make_rsrc(nullptr, 0), nrec, 0);
     }
     if (lane == 0) csizes[chunk] = (uint32_t)op;
 }
@@ -901,7 +903,7 @@ lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readabl
         Bytes rin;
         rin.init(in + off + fpos, readable);
         snv2::compress_fragment<true>(rin, fn, rout, 0, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13), nullptr,
-                                      nullptr, rr, nrec);
+                                      nullptr, rr, nrec, (int)fpos);
     }
     if (threadIdx.x == 0) rec_hdr[chunk] = (uint32_t)nrec;
 }
@@ -978,15 +980,19 @@ lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable
         const bool v = r < nrec;
         const uint32_t w0 = nw0, w1 = nw1;
         if (r + 64 < nrec) { nw0 = ld_b32(rr, 8 * (r + 64)); nw1 = ld_b32(rr, 8 * (r + 64) + 4); }
-        const int lit = v ? (int)(w0 & 0x1FFFFu) : 0;
-        const int ml = v ? (int)((w0 >> 17) | ((w1 & 0xFFFFu) << 15)) : 0;
+        // the literal run of a record starts at the previous record's end (lane-1 by a wave shift;
+        // the previous group's end for lane 0)
+        const int Pc = (int)(w0 & 0xFFFFFFu);
+        const int ml = v ? (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8)) : 0;
         const uint32_t o = w1 >> 16;
+        const int end = Pc + ml;
+        const int anc = __builtin_amdgcn_update_dpp(ia, end, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        const int lit = v ? Pc - anc : 0;
         const snv2::SnapSeq Q(lit, o, ml);
         const int S = v ? Q.total : 0;
-        const int L = lit + ml;
-        int T, Lt;
+        const int Lt = rdlanei(end, min(64, nrec - g) - 1) - ia;
+        int T;
         const int pos = op + sne::wave_excl_scan(S, T);
-        const int anc = ia + sne::wave_excl_scan(L, Lt);
         const int Smax = (int)uni((uint32_t)sne::wave_max(S));
         if (T <= sne::kRingB / 2 && Smax <= 64 && Lt + 8 <= sne::kSpan) {
             // the group's input span [ia, ia + Lt) into LDS (literal bytes are read from there)
