@@ -128,3 +128,22 @@ __device__ __forceinline__ void copy_span(const Bytes& src, int s0, const Bytes&
 // flat_load/flat_store (vector-memory pipe, vmcnt waits) instead of ds_read/ds_write.
 #define LDSA __attribute__((address_space(3)))
 __device__ __forceinline__ void lds_zero16(LDSA uint32_t* p) { p[0] = 0; p[1] = 0; p[2] = 0; p[3] = 0; }
+
+// Emission rings (structs with b / o / flushed / put / flush over a kRing-byte LDS ring, see the
+// LZ4 and snappy emission kernels): out[pos, pos+len) = in[src, src+len) for a long literal run.
+// The ring is flushed up to pos (its last bytes before pos as byte stores, so no store overlaps
+// another), the body goes out as dword stores straight to the staging slot, and the ring takes the
+// run's last partial dword so that its next dword flush rewrites those bytes unchanged.
+template <int kRing, class OutRing>
+__device__ __forceinline__ void bulk_literals(OutRing& R, const Bytes& in, int src, int pos, int len, int lane) {
+    R.flush(pos, false, lane);                         // complete dwords before pos
+    Bytes ob;
+    ob.r = R.o;
+    ob.sh = 0;
+    const int f = R.flushed;
+    if (lane < pos - f) ob.st8(f + lane, ((volatile LDSA uint8_t*)R.b)[(f + lane) & (kRing - 1)]);
+    copy_span(in, src, ob, pos, len, lane, LZH_WAVE);
+    const int e = pos + len, e4 = e & ~3;
+    if (lane < e - e4) R.put(e4 + lane, in.b(src + (e4 - pos) + lane));
+    R.flushed = e4;
+}

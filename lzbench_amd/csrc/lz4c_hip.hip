@@ -1208,9 +1208,13 @@ __device__ void put_seq_wave(OutR& R, const Bytes& in, int op, int anchor, int l
         if (b + lane < lx) R.put(pos + b + lane, b + lane == lx - 1 ? (uint32_t)(lit - 15) % 255u : 255u);
     }
     pos += lx;
-    for (int b = 0; b < lit; b += 64) {
-        if (pos + b - R.flushed >= kRingB - 128) R.flush(pos + b, false, lane);
-        if (b + lane < lit) R.put(pos + b + lane, in.b(anchor + b + lane));
+    if (lit >= 256) {   // long literal run (incompressible data, last literals): straight to HBM
+        bulk_literals<kRingB>(R, in, anchor, pos, lit, lane);
+    } else {
+        for (int b = 0; b < lit; b += 64) {
+            if (pos + b - R.flushed >= kRingB - 128) R.flush(pos + b, false, lane);
+            if (b + lane < lit) R.put(pos + b + lane, in.b(anchor + b + lane));
+        }
     }
     pos += lit;
     if (hm) {

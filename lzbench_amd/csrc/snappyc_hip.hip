@@ -946,6 +946,8 @@ struct OutR {
     }
 };
 
+constexpr int kBulk = 256;   // literal runs at least this long go straight to HBM (bulk_literals)
+
 }  // namespace sne
 
 extern "C" __global__ void __launch_bounds__(64)
@@ -1019,7 +1021,14 @@ lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable
                 const int kl = rdlanei(lit, k), km = rdlanei(ml, k), ka = rdlanei(anc, k);
                 const uint32_t ko = rdlane(o, k);
                 const snv2::SnapSeq K(kl, ko, km);
-                for (int b = 0; b < K.total; b += 64) {
+                int t0 = 0;
+                if (kl >= sne::kBulk) {   // long literal run: header through the ring, body straight to HBM
+                    if (op + 64 - R.flushed > sne::kRingB) R.flush(op, false, lane);
+                    if (lane < K.lit0) R.put(op + lane, K.byte(lane, 0u));
+                    bulk_literals<sne::kRingB>(R, in_b, ka, op + K.lit0, kl, lane);
+                    t0 = K.lit1;
+                }
+                for (int b = t0; b < K.total; b += 64) {
                     if (op + b + 64 - R.flushed > sne::kRingB) R.flush(op + b, false, lane);
                     const int t = b + lane;
                     const int li = t - K.lit0;
