@@ -85,6 +85,7 @@ __device__ __forceinline__ uint32_t lane_gather(uint32_t v, int src) {
 __device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_vm_but1() { asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); }   // all but the last issued
 
 // Byte-addressed view of a global span through a 4-aligned buffer descriptor: position p
 // lives at descriptor offset p + sh (sh = base address mod 4), so chunk bases of any

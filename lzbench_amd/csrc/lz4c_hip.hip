@@ -252,6 +252,7 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     do {                                                                                           \
         if (kRec) {                                                                                \
             const uint64_t rm_ = uni64(rc_m);   /* (wave-uniform: keep it in SGPRs) */             \
+            recs_st = rm_ != 0;                                                                    \
             if (rm_) {                                                                             \
                 const int ri_ = nrec + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(rm_ >> 32),       \
                                            __builtin_amdgcn_mbcnt_lo((uint32_t)rm_, 0u));          \
@@ -596,6 +597,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         return;
     }
     int nrec = 0;
+    bool recs_st = false;     // a record store was issued after this batch's candidate loads
     {
         LDSA uint32_t* t4 = (LDSA uint32_t*)tab;
 #pragma unroll
@@ -768,7 +770,11 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 bep = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
                 okp = valid && gw == ps.w;
             }
-            wait_vm();
+            // the candidate loads; a record store issued after them need not be acknowledged
+            // (vector memory operations complete in issue order)
+            if (kRec && recs_st) wait_vm_but1();
+            else wait_vm();
+            recs_st = false;
             R.ready = R.fill;
             wave_lds_fence();
             LZ_CLK(3);                                                 // exposed load wait
