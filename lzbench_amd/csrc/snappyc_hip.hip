@@ -995,8 +995,8 @@ lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable
         const int Lt = rdlanei(end, min(64, nrec - g) - 1) - ia;
         int T;
         const int pos = op + sne::wave_excl_scan(S, T);
-        const int Smax = (int)uni((uint32_t)sne::wave_max(S));
-        if (T <= sne::kRingB / 2 && Smax <= 64 && Lt + 8 <= sne::kSpan) {
+        const int litmax = (int)uni((uint32_t)sne::wave_max(lit));
+        if (T <= sne::kRingB / 2 && litmax <= 64 && Lt + 8 <= sne::kSpan) {
             // the group's input span [ia, ia + Lt) into LDS (literal bytes are read from there)
             const int X0 = (ia + in_b.sh) & ~3;
             const int nd = (ia + in_b.sh + Lt - X0 + 3) >> 2;
@@ -1005,12 +1005,34 @@ lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable
             const LDSA uint8_t* ib = (const LDSA uint8_t*)ibuf;
             const int ioff = in_b.sh - X0;            // input position p lives at ib[p + ioff]
             if (op + T - R.flushed > sne::kRingB - 8) R.flush(op, false, lane);
-            // every lane writes its own (literal, copy) pair, byte t of it at pass t
-            for (int t = 0; t < Smax; t++) {
-                if (t < S) {
-                    const int li = t - Q.lit0;
-                    const uint32_t lb = (li >= 0 && li < lit) ? (uint32_t)ib[anc + li + ioff] : 0u;
-                    R.put(pos + t, Q.byte(t, lb));
+            // every lane writes its own (literal, copy) pair phase by phase (snappy.cc:342-443):
+            // tag and (lit <= 64 here) at most one length byte, the literal run (a lane-parallel
+            // copy as long as the group's longest), the 64 / 60-byte COPY_2 pieces of a long copy,
+            // the final COPY_1 or COPY_2
+            if (v && lit > 0) {
+                R.put(pos, Q.tag);
+                if (Q.hl > 1) R.put(pos + 1, Q.nm1 & 0xffu);
+            }
+            for (int t = 0; t < litmax; t++)
+                if (t < lit) R.put(pos + Q.lit0 + t, ib[anc + t + ioff]);
+            const int cp = pos + Q.lit1;
+            const int np = v && ml > 0 ? Q.k + Q.has60 : 0;
+            for (int i = 0; ballot(i < np); i++) {
+                if (i < np) {
+                    R.put(cp + 3 * i, i < Q.k ? (2u | (63u << 2)) : (2u | (59u << 2)));
+                    R.put(cp + 3 * i + 1, Q.lo);
+                    R.put(cp + 3 * i + 2, Q.hi);
+                }
+            }
+            if (v && ml > 0) {
+                const int fp = cp + Q.pre;
+                if (Q.c1) {
+                    R.put(fp, 1u | ((uint32_t)(Q.rem - 4) << 2) | ((Q.offv >> 8) << 5));
+                    R.put(fp + 1, Q.lo);
+                } else {
+                    R.put(fp, 2u | ((uint32_t)(Q.rem - 1) << 2));
+                    R.put(fp + 1, Q.lo);
+                    R.put(fp + 2, Q.hi);
                 }
             }
             op += T;
