@@ -78,7 +78,7 @@ size_t lzh_compress_temp_bytes(int codec, size_t n, size_t chunk_size) {
     if (codec == LZH_CODEC_LZ4 && chunk_size <= kLz4SplitMax)     // sequence records of the parse kernel
         t += k * lzh_lz4_rec_stride(chunk_size) + align_up(k * 8, 256) + 256;
     if (codec == LZH_CODEC_SNAPPY && chunk_size <= kLz4SplitMax)
-        t += k * lzh_snappy_rec_stride(chunk_size) + align_up(k * 4, 256) + 256;
+        t += k * lzh_snappy_rec_stride(chunk_size) + align_up(k * 4 * lzh_snappy_frags(chunk_size), 256) + 256;
     if (codec == LZH_CODEC_ZSTD) {   // per-frame scratch of the two zstd kernels (zstdc_hip.hip), worst level
         size_t fs = 0;
         for (int lv : {1, 2, -1, -2}) fs = std::max(fs, lzh_zstd_scratch_stride(chunk_size, lv));

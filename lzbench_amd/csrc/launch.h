@@ -35,3 +35,4 @@ hipError_t lzh_launch_snappy_split(const uint8_t* in, uint64_t n_total, uint64_t
                                    uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
                                    int stage_mask, hipStream_t s);
 size_t lzh_snappy_rec_stride(uint64_t chunk_size);
+uint32_t lzh_snappy_frags(uint64_t chunk_size);

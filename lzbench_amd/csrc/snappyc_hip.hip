@@ -887,7 +887,7 @@ lzh_snappy_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 
 extern "C" __global__ void __launch_bounds__(64)
 lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
-                        uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr) {
+                        uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint32_t frags) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + (LZH_SN_PARSE_NORING ? 0 : 256 + 8)];   // table | ring + mirror
     const uint64_t chunk = blockIdx.x;
     const uint64_t off = chunk * chunk_size;
@@ -897,15 +897,19 @@ lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readabl
     Bytes rout;
     rout.init(nullptr, 0);
     int nrec = 0;
-    for (uint32_t fpos = 0; fpos < n; fpos += 65536u) {
+    uint32_t* hdr = rec_hdr + chunk * frags;       // cumulative record count after each fragment
+    uint32_t f = 0;
+    for (uint32_t fpos = 0; fpos < n; fpos += 65536u, f++) {
         const int fn = (int)min(65536u, n - fpos);
         const uint64_t readable = min<uint64_t>(in_readable - off - fpos, (uint64_t)fn + 64);
         Bytes rin;
         rin.init(in + off + fpos, readable);
         snv2::compress_fragment<true>(rin, fn, rout, 0, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13), nullptr,
                                       nullptr, rr, nrec, (int)fpos);
+        if (threadIdx.x == 0) hdr[f] = (uint32_t)nrec;
     }
-    if (threadIdx.x == 0) rec_hdr[chunk] = (uint32_t)nrec;
+    for (; f < frags; f++)
+        if (threadIdx.x == 0) hdr[f] = (uint32_t)nrec;
 }
 
 namespace sne {
@@ -929,19 +933,42 @@ __device__ __forceinline__ int wave_excl_scan(int x, int& total) {
     return incl - x;
 }
 
+// Output ring of one wave writing the byte range [start, end) of a staging slot.  kEdge: other
+// waves share the slot (one 64 KiB fragment each) -- dword stores inside the range, byte stores for
+// the partial dwords at its edges, so no store touches another wave's bytes; otherwise the range
+// starts at 0 and the last partial dword is stored whole.
+template <bool kEdge>
 struct OutR {
     LDSA uint8_t* b;
     rsrc_t o;          // staging slot (256-aligned)
-    int flushed;       // bytes [0, flushed) are in global memory
+    int flushed;       // bytes [start, flushed) are in global memory
     __device__ __forceinline__ void put(int pos, uint32_t v) const { ((volatile LDSA uint8_t*)b)[pos & (kRingB - 1)] = (uint8_t)v; }
-    // global <- complete dwords of [flushed, upto) (all of it when fin: the partial last dword too)
+    __device__ __forceinline__ uint32_t rbyte(int pos) const { return ((volatile LDSA uint8_t*)b)[pos & (kRingB - 1)]; }
+    // global <- [flushed, upto): bytes up to the first dword boundary, whole dwords, and (fin) the
+    // bytes of the last partial dword; without fin the partial last dword waits for more bytes
     __device__ __forceinline__ void flush(int upto, bool fin, int lane) {
         wave_lds_fence();
-        const int d0 = flushed >> 2, d1 = fin ? (upto + 3) >> 2 : upto >> 2;
-        for (int d = d0 + lane; d < d1; d += 64)
+        if (!kEdge) {
+            const int d0 = flushed >> 2, d1 = fin ? (upto + 3) >> 2 : upto >> 2;
+            for (int d = d0 + lane; d < d1; d += 64)
+                st_b32(o, 4 * d, ((volatile LDSA uint32_t*)b)[d & (kRingB / 4 - 1)]);
+            flushed = 4 * d1;
+            if (flushed > upto) flushed = upto & ~3;   // (the partial dword is rewritten by the next flush)
+            wave_lds_fence();
+            return;
+        }
+        const int a = flushed, a4 = (a + 3) & ~3, b4 = upto & ~3;
+        const int h1 = min(a4, upto);
+        if (lane < h1 - a) st_u8(o, a + lane, rbyte(a + lane));
+        for (int d = (a4 >> 2) + lane; d < (b4 >> 2); d += 64)
             st_b32(o, 4 * d, ((volatile LDSA uint32_t*)b)[d & (kRingB / 4 - 1)]);
-        flushed = 4 * d1;
-        if (flushed > upto) flushed = upto & ~3;   // (the partial dword is rewritten by the next flush)
+        if (fin) {
+            const int t0 = max(a4, b4);
+            if (lane < upto - t0) st_u8(o, t0 + lane, rbyte(t0 + lane));
+            flushed = upto;
+        } else {
+            flushed = max(h1, b4);
+        }
         wave_lds_fence();
     }
 };
@@ -950,38 +977,41 @@ constexpr int kBulk = 256;   // literal runs at least this long go straight to H
 
 }  // namespace sne
 
-extern "C" __global__ void __launch_bounds__(64)
-lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
-                       const uint8_t* recs, uint64_t rec_stride, const uint32_t* rec_hdr, uint8_t* stage,
-                       uint64_t stride, uint32_t* csizes) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[sne::kRingB];
-    __shared__ __attribute__((aligned(16))) uint32_t ibuf[sne::kSpan / 4 + 4];   // input span of a group
-    const int lane = threadIdx.x;
-    const uint64_t chunk = blockIdx.x;
-    const uint64_t off = chunk * chunk_size;
-    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
-    const uint32_t n = (uint32_t)min(chunk_size, n_total - off);
-    Bytes in_b;
-    in_b.init(in + off, min<uint64_t>(in_readable - off, (uint64_t)n + 64));
-    const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
-    const int nrec = (int)uni(rec_hdr[chunk]);
-    sne::OutR R{(LDSA uint8_t*)ring, make_rsrc(stage + chunk * stride, (uint32_t)stride), 0};
-    int op = 0;
-    {   // varint32 uncompressed length (snappy.cc:1047-1050)
-        uint32_t v = n;
-        int nb = 1;
-        while (v >= 128) { v >>= 7; nb++; }
-        if (lane < nb) R.put(lane, ((n >> (7 * lane)) & 0x7fu) | (lane + 1 < nb ? 0x80u : 0u));
-        op = nb;
-    }
-    int ia = 0;
-    uint32_t nw0 = 0, nw1 = 0;                 // records of the next group (loaded one group ahead)
-    if (lane < nrec) { nw0 = ld_b32(rr, 8 * lane); nw1 = ld_b32(rr, 8 * lane + 4); }
-    for (int g = 0; g < nrec; g += 64) {
+namespace sne {
+
+// output bytes of the records [r0, r1) (the first literal run starts at ia)
+__device__ int frag_bytes(rsrc_t rr, int r0, int r1, int ia, int lane) {
+    int total = 0;
+    for (int g = r0; g < r1; g += 64) {
         const int r = g + lane;
-        const bool v = r < nrec;
+        const bool v = r < r1;
+        uint32_t w0 = 0, w1 = 0;
+        if (v) { w0 = ld_b32(rr, 8 * r); w1 = ld_b32(rr, 8 * r + 4); }
+        const int Pc = (int)(w0 & 0xFFFFFFu);
+        const int ml = v ? (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8)) : 0;
+        const int end = Pc + ml;
+        const int anc = __builtin_amdgcn_update_dpp(ia, end, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        const int lit = v ? Pc - anc : 0;
+        const snv2::SnapSeq Q(lit, w1 >> 16, ml);
+        int T;
+        wave_excl_scan(v ? Q.total : 0, T);
+        total += T;
+        ia = rdlanei(end, min(64, r1 - g) - 1);
+    }
+    return total;
+}
+
+// lay out the records [r0, r1) at op (the first literal run starts at ia); returns the end
+template <class OutR>
+__device__ __forceinline__ int emit_records(OutR& R, const Bytes& in_b, rsrc_t rr, int r0, int r1, int ia, int op,
+                            LDSA uint32_t* ibuf, int lane) {
+    uint32_t nw0 = 0, nw1 = 0;                 // records of the next group (loaded one group ahead)
+    if (r0 + lane < r1) { nw0 = ld_b32(rr, 8 * (r0 + lane)); nw1 = ld_b32(rr, 8 * (r0 + lane) + 4); }
+    for (int g = r0; g < r1; g += 64) {
+        const int r = g + lane;
+        const bool v = r < r1;
         const uint32_t w0 = nw0, w1 = nw1;
-        if (r + 64 < nrec) { nw0 = ld_b32(rr, 8 * (r + 64)); nw1 = ld_b32(rr, 8 * (r + 64) + 4); }
+        if (r + 64 < r1) { nw0 = ld_b32(rr, 8 * (r + 64)); nw1 = ld_b32(rr, 8 * (r + 64) + 4); }
         // the literal run of a record starts at the previous record's end (lane-1 by a wave shift;
         // the previous group's end for lane 0)
         const int Pc = (int)(w0 & 0xFFFFFFu);
@@ -992,7 +1022,7 @@ lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable
         const int lit = v ? Pc - anc : 0;
         const snv2::SnapSeq Q(lit, o, ml);
         const int S = v ? Q.total : 0;
-        const int Lt = rdlanei(end, min(64, nrec - g) - 1) - ia;
+        const int Lt = rdlanei(end, min(64, r1 - g) - 1) - ia;
         int T;
         const int pos = op + sne::wave_excl_scan(S, T);
         const int litmax = (int)uni((uint32_t)sne::wave_max(lit));
@@ -1039,7 +1069,7 @@ lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable
             if (op - R.flushed >= sne::kRingB / 2) R.flush(op, false, lane);
             wave_lds_fence();
         } else {
-            for (int k = 0; k < 64 && g + k < nrec; k++) {
+            for (int k = 0; k < 64 && g + k < r1; k++) {
                 const int kl = rdlanei(lit, k), km = rdlanei(ml, k), ka = rdlanei(anc, k);
                 const uint32_t ko = rdlane(o, k);
                 const snv2::SnapSeq K(kl, ko, km);
@@ -1062,11 +1092,106 @@ lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable
         }
         ia += Lt;
     }
-    R.flush(op, true, lane);
-    if (lane == 0) csizes[chunk] = (uint32_t)op;
+    return op;
+}
+
+}  // namespace sne
+
+// One workgroup per chunk, one wave per 64 KiB fragment (W waves, looping when a chunk has more
+// fragments): each wave sums its fragment's output bytes from the records, the fragments' offsets
+// follow by a prefix over them, and each wave lays its fragment out at its offset.  (-b64: one
+// wave per chunk; -b256: four, where one wave per chunk left half the wave slots idle.)
+namespace sne {
+constexpr int kSpanDw = kSpan / 4 + 4;   // LDS dwords of a wave's input span
+constexpr int kMaxFrags = 256;           // 16 MiB chunks (the split path's limit)
+
+// (the rings, spans and sizes are separate __shared__ arrays: through one shared base the compiler
+// cannot tell the span reads from the ring writes apart and serialises the literal copy)
+template <bool kMulti>
+__device__ __forceinline__ void emit_chunk(LDSA uint8_t* rings, LDSA uint32_t* ibufs, LDSA uint32_t* fsz,
+                                           const uint8_t* in, uint64_t n_total, uint64_t in_readable,
+                                           uint64_t chunk_size, const uint8_t* recs, uint64_t rec_stride,
+                                           const uint32_t* rec_hdr, uint8_t* stage, uint64_t stride, uint32_t* csizes,
+                                           uint32_t frags) {
+    const int lane = threadIdx.x & 63, wave = kMulti ? threadIdx.x >> 6 : 0, W = kMulti ? blockDim.x >> 6 : 1;
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t off = chunk * chunk_size;
+    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
+    const uint32_t n = (uint32_t)min(chunk_size, n_total - off);
+    LDSA uint8_t* ring = rings + wave * kRingB;
+    LDSA uint32_t* ibuf = ibufs + wave * kSpanDw;
+    Bytes in_b;
+    in_b.init(in + off, min<uint64_t>(in_readable - off, (uint64_t)n + 64));
+    const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
+    const uint32_t* hdr = rec_hdr + chunk * frags;
+    const int nf = (int)((n + 65535u) >> 16);
+    const rsrc_t so = make_rsrc(stage + chunk * stride, (uint32_t)stride);
+    int nb = 1;                                    // varint32 uncompressed length (snappy.cc:1047-1050)
+    for (uint32_t v = n; v >= 128; v >>= 7) nb++;
+    if constexpr (!kMulti) {   // one fragment (chunks of at most 64 KiB)
+        OutR<false> R{ring, so, 0};
+        if (lane < nb) R.put(lane, ((n >> (7 * lane)) & 0x7fu) | (lane + 1 < nb ? 0x80u : 0u));
+        const int e = emit_records(R, in_b, rr, 0, (int)uni(hdr[0]), 0, nb, ibuf, lane);
+        R.flush(e, true, lane);
+        if (lane == 0) csizes[chunk] = (uint32_t)e;
+    } else {
+    // sizes of all fragments but the last (the last one's end is the chunk's compressed size)
+    for (int f = wave; f < nf - 1; f += W) {
+        const int r0 = f == 0 ? 0 : (int)uni(hdr[f - 1]), r1 = (int)uni(hdr[f]);
+        const int bytes = frag_bytes(rr, r0, r1, f << 16, lane);
+        if (lane == 0) fsz[f] = (uint32_t)bytes;
+    }
+    if (kMulti) __syncthreads();
+    // the varint goes through fragment 0's ring (an empty chunk: a store of its own)
+    const uint32_t vb = ((n >> (7 * lane)) & 0x7fu) | (lane + 1 < nb ? 0x80u : 0u);
+    if (nf == 0 && wave == 0) {
+        if (lane < nb) st_u8(so, lane, vb);
+        if (lane == 0) csizes[chunk] = (uint32_t)nb;
+    }
+    int base = nb;
+    for (int f = 0; f < nf; f++) {
+        if ((f % W) == wave) {
+            const int r0 = f == 0 ? 0 : (int)uni(hdr[f - 1]), r1 = (int)uni(hdr[f]);
+            OutR<kMulti> R{ring, so, f == 0 ? 0 : base};
+            if (f == 0 && lane < nb) R.put(lane, vb);
+            const int e = emit_records(R, in_b, rr, r0, r1, f << 16, base, ibuf, lane);
+            R.flush(e, true, lane);
+            if (f == nf - 1 && lane == 0) csizes[chunk] = (uint32_t)e;
+        }
+        if (f < nf - 1) base += (int)uni(((volatile LDSA uint32_t*)fsz)[f]);
+    }
+    }
+}
+
+}  // namespace sne
+
+// -b64 and smaller chunks: a single fragment, one wave
+extern "C" __global__ void __launch_bounds__(64)
+lzh_snappy_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                       const uint8_t* recs, uint64_t rec_stride, const uint32_t* rec_hdr, uint8_t* stage,
+                       uint64_t stride, uint32_t* csizes, uint32_t frags) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[sne::kRingB];
+    __shared__ __attribute__((aligned(16))) uint32_t ibuf[sne::kSpanDw];
+    sne::emit_chunk<false>((LDSA uint8_t*)ring, (LDSA uint32_t*)ibuf, nullptr, in, n_total, in_readable, chunk_size,
+                           recs, rec_stride, rec_hdr, stage, stride, csizes, frags);
+}
+
+// larger chunks: kW >= min(fragments, 8) waves (the block has exactly that many), each with its
+// ring and span, and the fragment sizes
+template <int kW>
+__global__ void __launch_bounds__(64 * kW)
+lzh_snappy_emit_frag_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
+                            const uint8_t* recs, uint64_t rec_stride, const uint32_t* rec_hdr, uint8_t* stage,
+                            uint64_t stride, uint32_t* csizes, uint32_t frags) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kW * sne::kRingB];
+    __shared__ __attribute__((aligned(16))) uint32_t ibuf[kW * sne::kSpanDw];
+    __shared__ uint32_t fsz[sne::kMaxFrags];
+    sne::emit_chunk<true>((LDSA uint8_t*)ring, (LDSA uint32_t*)ibuf, (LDSA uint32_t*)fsz, in, n_total, in_readable,
+                          chunk_size, recs, rec_stride, rec_hdr, stage, stride, csizes, frags);
 }
 
 #include "launch.h"
+uint32_t lzh_snappy_frags(uint64_t chunk_size) { return (uint32_t)((chunk_size + 65535) >> 16); }
 size_t lzh_snappy_rec_stride(uint64_t chunk_size) {
     return ((chunk_size / 4 + chunk_size / 65536 + 8) * 8 + 255) / 256 * 256;
 }
@@ -1079,12 +1204,24 @@ hipError_t lzh_launch_snappy_split(const uint8_t* in, uint64_t n_total, uint64_t
     if (nchunks == 0) return hipSuccess;
     const uint64_t rs = lzh_snappy_rec_stride(chunk_size);
     uint32_t* hdr = (uint32_t*)(recs + rs * nchunks);
+    const uint32_t frags = lzh_snappy_frags(chunk_size);
     if (stage_mask & 1)
         hipLaunchKernelGGL(lzh_snappy_parse_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable,
-                           chunk_size, recs, rs, hdr);
-    if (stage_mask & 2)
-        hipLaunchKernelGGL(lzh_snappy_emit_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable,
-                           chunk_size, (const uint8_t*)recs, rs, (const uint32_t*)hdr, stage, stride, csizes);
+                           chunk_size, recs, rs, hdr, frags);
+    if (stage_mask & 2) {
+        if (frags > (uint32_t)sne::kMaxFrags) return hipErrorInvalidValue;
+        const uint32_t W = frags < 8 ? frags : 8;
+#define LZH_SNE_ARGS in, n_total, in_readable, chunk_size, (const uint8_t*)recs, rs, (const uint32_t*)hdr, stage, stride, csizes, frags
+        if (W <= 1)
+            hipLaunchKernelGGL(lzh_snappy_emit_kernel, dim3(nchunks), dim3(64), 0, s, LZH_SNE_ARGS);
+        else if (W == 2)
+            hipLaunchKernelGGL(lzh_snappy_emit_frag_kernel<2>, dim3(nchunks), dim3(128), 0, s, LZH_SNE_ARGS);
+        else if (W <= 4)
+            hipLaunchKernelGGL(lzh_snappy_emit_frag_kernel<4>, dim3(nchunks), dim3(64 * W), 0, s, LZH_SNE_ARGS);
+        else
+            hipLaunchKernelGGL(lzh_snappy_emit_frag_kernel<8>, dim3(nchunks), dim3(64 * W), 0, s, LZH_SNE_ARGS);
+#undef LZH_SNE_ARGS
+    }
     return hipGetLastError();
 }
 
