@@ -14,6 +14,21 @@
 // input; on valid streams both produce identical bytes.)
 #include "common.h"
 
+// Debug counters (-DLZH_DEC_STATS=1 builds only, read by tools/dec_stats.py): per-wave sums in LDS,
+// added to a device array when the chunk ends.
+#ifndef LZH_DEC_STATS
+#define LZH_DEC_STATS 0
+#endif
+#if LZH_DEC_STATS
+__shared__ unsigned long long g_dst[16];
+__device__ unsigned long long lzh_dec_stats_buf[16];
+#define DST(i, v) do { if (threadIdx.x == 0) g_dst[i] += (unsigned long long)(v); } while (0)
+#define DCLK(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#else
+#define DST(i, v) do {} while (0)
+#define DCLK(t) do {} while (0)
+#endif
+
 namespace {
 
 #ifndef LZH_DEC_RING
@@ -447,7 +462,9 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
         const int le0 = (int)lane_gather((uint32_t)m_lend, k0), ls0 = (int)lane_gather((uint32_t)m_lsb, k0),
                   ms0 = (int)lane_gather((uint32_t)m_msrc, k0), of0 = (int)lane_gather((uint32_t)off, k0);
         int le1 = le0, ls1 = ls0, ms1 = ms0, of1 = of0;
+        DST(2, 1);
         if (ballot(k1 != k0)) {
+            DST(3, 1);
             le1 = (int)lane_gather((uint32_t)m_lend, k1);
             ls1 = (int)lane_gather((uint32_t)m_lsb, k1);
             ms1 = (int)lane_gather((uint32_t)m_msrc, k1);
@@ -461,6 +478,7 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
         uint32_t v0 = owned_byte(w, O, op, pbase, thr, ob0, total, le0, ls0, ms0, of0, src0, done0, far0);
         uint32_t v1 = owned_byte(w, O, op, pbase, thr, ob1, total, le1, ls1, ms1, of1, src1, done1, far1);
         if (ballot(far0 || far1)) {   // far sources were flushed long ago: their stores must be done
+            DST(5, 1);
             wait_vm();
             const uint32_t g0 = O.out.b_sc1(far0 ? src0 : 0), g1 = O.out.b_sc1(far1 ? src1 : 0);
             v0 = far0 ? g0 : v0;
@@ -475,6 +493,7 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
         // in-pass sources: rounds until every byte read a finished source
         uint64_t dm0 = ballot(done0 || ob0 >= total), dm1 = ballot(done1 || ob1 >= total);
         for (int r = 0; r < kP && (~dm0 | ~dm1); r++) {
+            DST(4, 1);
             const int s0 = src0 - pbase, s1 = src1 - pbase;
             const bool rd0 = !lane_on(dm0) && (((s0 & 1 ? dm1 : dm0) >> ((s0 >> 1) & 63)) & 1ull);
             const bool rd1 = !lane_on(dm1) && (((s1 & 1 ? dm1 : dm0) >> ((s1 >> 1) & 63)) & 1ull);
@@ -536,6 +555,7 @@ __device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* 
     w.load(0, lane);
     int ip = 0, op = 0;
     for (int guard = 0; guard <= cs; guard++) {
+        DCLK(t0);
         ip = unii(ip); op = unii(op);
         O.flushed = unii(O.flushed); O.ringlo = unii(O.ringlo);
         if (!w.covers(ip, ip + 2 * LZH_WAVE)) w.load(ip, lane);
@@ -567,6 +587,10 @@ __device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* 
         const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
         if (!keep) {
             const int r = checked::lz4_one(in, cs, O, w, cap, ip, op, lane);
+            DST(6, 1);
+#if LZH_DEC_STATS
+            DST(10, __builtin_amdgcn_s_memtime() - t0);
+#endif
             if (r < 0) return r;
             if (r == 1) break;
             continue;
@@ -574,9 +598,18 @@ __device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* 
         const int lastk = 63 - __builtin_clzll(keep);
         const int total = rdlanei(incl, lastk);
         const int ip_next = ip + rdlanei(pe - ip, lastk);
+        DCLK(t1);
 #ifndef LZH_ABL_NOEMIT
         emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)ml << 16), (uint32_t)(p1 - ip),
                    off, lane);
+#endif
+#if LZH_DEC_STATS
+        DCLK(t2);
+        DST(0, 1);
+        DST(1, __builtin_popcountll(keep));
+        DST(7, total);
+        DST(8, t1 - t0);
+        DST(9, t2 - t1);
 #endif
         op += total;
         ip = ip_next;
@@ -714,6 +747,10 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t ooff = chunk * chunk_size;
     if (ooff >= n_total) return;
+#if LZH_DEC_STATS
+    if (lane < 16) g_dst[lane] = 0;
+    DCLK(tk0);
+#endif
     const int part = (int)min(chunk_size, n_total - ooff);
     const uint64_t ioff = offsets[chunk];
     const int cs = (int)csizes[chunk];
@@ -734,7 +771,22 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
         if (r > 0) O.flush(r, lane);
     }
     if (lane == 0) status[chunk] = r;
+#if LZH_DEC_STATS
+    DST(11, 1);
+    DST(12, __builtin_amdgcn_s_memtime() - tk0);
+    if (lane < 16) atomicAdd(&lzh_dec_stats_buf[lane], g_dst[lane]);
+#endif
 }
+
+#if LZH_DEC_STATS
+extern "C" int lzh_debug_dec_stats(unsigned long long* host, int reset) {
+    if (reset) {
+        unsigned long long z[16] = {};
+        return hipMemcpyToSymbol(HIP_SYMBOL(lzh_dec_stats_buf), z, sizeof(z)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(lzh_dec_stats_buf), 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ---------------------------------------------------------------------------------------
 // zstd frames (RFC 8878), the decode side of lzbench's zstd rows (compressors.cpp:1767-1773:
