@@ -45,7 +45,20 @@ extern "C" {
  * (ZSTD_getParams(level, chunk, 0) + content size, no dictionary, no checksum).  Compression:
  * the fast-strategy levels (zstd 1, 2 where fast, zstd_fast -1..-5), bit-exact with the reference;
  * other levels return LZH_EARG.  Decoding: any frame of that shape. */
-enum { LZH_CODEC_LZ4 = 0, LZH_CODEC_SNAPPY = 1, LZH_CODEC_MEMCPY = 2, LZH_CODEC_ZSTD = 3 };
+/* LZH_CODEC_LZ4F: one LZ4 frame per chunk as LZ4F_compressFrame writes it (lz4/lz4frame.c:429-470)
+ * with independent blocks; level = LZH_LZ4F_PARAMS(blockSizeID 0|4..7, flags, acceleration).
+ * Decoding: frames with independent blocks (or one block), every block but the last full, no
+ * dictionary id; other frames report -2.
+ * LZH_CODEC_NVLZ4: one nvcomp LZ4 container per chunk (the format of the reference's nvcomp_lz4
+ * row, nvcomp/LZ4Metadata.h), LZ4 blocks of 1 << (15 + level) bytes, level 0..5 (compressors.cpp:1863).
+ * Both: lzh_compress_async / lzh_decompress_async and the rows below; not lzh_compress_kernel_only /
+ * lzh_compress_finish_async. */
+enum { LZH_CODEC_LZ4 = 0, LZH_CODEC_SNAPPY = 1, LZH_CODEC_MEMCPY = 2, LZH_CODEC_ZSTD = 3, LZH_CODEC_LZ4F = 4,
+       LZH_CODEC_NVLZ4 = 5 };
+#define LZH_LZ4F_BLOCK_CHECKSUM   0x10   /* LZ4F_blockChecksumEnabled */
+#define LZH_LZ4F_CONTENT_CHECKSUM 0x20   /* LZ4F_contentChecksumEnabled */
+#define LZH_LZ4F_CONTENT_SIZE     0x40   /* frameInfo.contentSize = chunk size */
+#define LZH_LZ4F_PARAMS(bsid, flags, acc) ((bsid) | (flags) | ((acc) << 8))
 enum { LZH_OK = 0, LZH_EARG = -1, LZH_EHIP = -2, LZH_ESPACE = -3, LZH_ECORRUPT = -4 };
 
 /* ---- 1. lzbench rows (per-chunk ABI) ------------------------------------------------ */
@@ -53,6 +66,8 @@ char*   lzbench_hip_lz4_init(size_t chunk_size, size_t level, size_t ngpus);
 char*   lzbench_hip_snappy_init(size_t chunk_size, size_t level, size_t ngpus);
 char*   lzbench_hip_memcpy_init(size_t chunk_size, size_t level, size_t ngpus);
 char*   lzbench_hip_zstd_init(size_t chunk_size, size_t level, size_t ngpus);
+char*   lzbench_hip_lz4frame_init(size_t chunk_size, size_t level, size_t ngpus);
+char*   lzbench_hip_nvcomp_lz4_init(size_t chunk_size, size_t level, size_t ngpus);
 void    lzbench_hip_deinit(char* workmem);
 /* lz4: LZ4_compress_default semantics; lz4fast: level = acceleration (LZ4_compress_fast) */
 int64_t lzbench_hip_lz4_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
@@ -64,6 +79,14 @@ int64_t lzbench_hip_snappy_decompress(char* in, size_t insize, char* out, size_t
  * zstd / zstd_fast rows pass it (size_t of a possibly negative int) */
 int64_t lzbench_hip_zstd_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
 int64_t lzbench_hip_zstd_decompress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+/* LZ4 frame per chunk: level = LZH_LZ4F_PARAMS(...): 4..7 = blockSizeID 64 KiB .. 4 MiB without flags,
+ * e.g. 0x74 = 64 KiB blocks + block / content checksums + content size */
+int64_t lzbench_hip_lz4frame_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+int64_t lzbench_hip_lz4frame_decompress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+/* nvcomp LZ4 container per chunk: replaces lzbench_nvcomp_compress / _decompress (compressors.cpp:1916-2014),
+ * level 0..5 = chunks of 32 KiB << level */
+int64_t lzbench_hip_nvcomp_lz4_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
+int64_t lzbench_hip_nvcomp_lz4_decompress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
 /* hipMemcpy plumbing row: host -> HBM -> host round trip of the chunk */
 int64_t lzbench_hip_memcpy(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t p2, char* workmem);
 

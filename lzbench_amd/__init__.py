@@ -23,7 +23,8 @@ import numpy as np
 __all__ = [
     "ExtensionMissing", "lib", "CODECS", "COMP_DESC", "CompressorDesc", "find_compressor",
     "compress_chunks", "decompress_chunks", "chunk_sizes_for", "datagen", "DeviceCodec",
-    "LZH_CODEC_LZ4", "LZH_CODEC_SNAPPY", "LZH_CODEC_MEMCPY", "LZH_CODEC_ZSTD", "PAD_SIZE", "get_compress_bound",
+    "LZH_CODEC_LZ4", "LZH_CODEC_SNAPPY", "LZH_CODEC_MEMCPY", "LZH_CODEC_ZSTD", "LZH_CODEC_LZ4F", "LZH_CODEC_NVLZ4",
+    "LZ4F_BLOCK_CHECKSUM", "LZ4F_CONTENT_CHECKSUM", "LZ4F_CONTENT_SIZE", "PAD_SIZE", "get_compress_bound",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -31,9 +32,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LZH_LIB") or os.path.join(_HERE, "liblzbench_hip.so")
 DATAGEN_PATH = os.path.join(_HERE, "libdatagen.so")
 
-LZH_CODEC_LZ4, LZH_CODEC_SNAPPY, LZH_CODEC_MEMCPY, LZH_CODEC_ZSTD = 0, 1, 2, 3
+LZH_CODEC_LZ4, LZH_CODEC_SNAPPY, LZH_CODEC_MEMCPY, LZH_CODEC_ZSTD, LZH_CODEC_LZ4F, LZH_CODEC_NVLZ4 = 0, 1, 2, 3, 4, 5
 CODECS = {"lz4": LZH_CODEC_LZ4, "lz4fast": LZH_CODEC_LZ4, "snappy": LZH_CODEC_SNAPPY, "memcpy": LZH_CODEC_MEMCPY,
-          "zstd": LZH_CODEC_ZSTD, "zstd_fast": LZH_CODEC_ZSTD}
+          "zstd": LZH_CODEC_ZSTD, "zstd_fast": LZH_CODEC_ZSTD, "lz4frame": LZH_CODEC_LZ4F,
+          "nvcomp_lz4": LZH_CODEC_NVLZ4}
+# LZ4 frame parameters (include/lzbench_hip.h LZH_LZ4F_*): level = bsid | flags | acceleration << 8
+LZ4F_BLOCK_CHECKSUM, LZ4F_CONTENT_CHECKSUM, LZ4F_CONTENT_SIZE = 0x10, 0x20, 0x40
+# codecs whose level is passed through as is (the others: 1 for lz4 = LZ4_compress_default, 0)
+_LEVELED = ("lz4fast", "zstd", "zstd_fast", "lz4frame", "nvcomp_lz4")
 PAD_SIZE = 16 * 1024          # lzbench.h:14
 
 
@@ -60,6 +66,12 @@ SIGNATURES = {
     "lzbench_hip_snappy_init": (_P, [_SZ, _SZ, _SZ]),
     "lzbench_hip_memcpy_init": (_P, [_SZ, _SZ, _SZ]),
     "lzbench_hip_zstd_init": (_P, [_SZ, _SZ, _SZ]),
+    "lzbench_hip_lz4frame_init": (_P, [_SZ, _SZ, _SZ]),
+    "lzbench_hip_nvcomp_lz4_init": (_P, [_SZ, _SZ, _SZ]),
+    "lzbench_hip_lz4frame_compress": _COMPRESS_FUNC,
+    "lzbench_hip_lz4frame_decompress": _COMPRESS_FUNC,
+    "lzbench_hip_nvcomp_lz4_compress": _COMPRESS_FUNC,
+    "lzbench_hip_nvcomp_lz4_decompress": _COMPRESS_FUNC,
     "lzbench_hip_zstd_compress": _COMPRESS_FUNC,
     "lzbench_hip_zstd_decompress": _COMPRESS_FUNC,
     "lzbench_hip_deinit": (None, [_P]),
@@ -158,6 +170,14 @@ COMP_DESC = (
     CompressorDesc("hip_zstd_fast", "1.5.2", -5, -1, 1, 0, "lzbench_hip_zstd_compress", "lzbench_hip_zstd_decompress",
                    "lzbench_hip_zstd_init", "lzbench_hip_deinit",
                    "lzbench_hip_compress_batch", "lzbench_hip_decompress_batch"),
+    # framed formats: an LZ4 frame per chunk (level = LZH_LZ4F_PARAMS), the nvcomp_lz4 row's container
+    # (lzbench.h:218, levels 0..5 = chunks of 32 KiB << level)
+    CompressorDesc("hip_lz4frame", "1.9.3", 4, 7, 1, 0, "lzbench_hip_lz4frame_compress",
+                   "lzbench_hip_lz4frame_decompress", "lzbench_hip_lz4frame_init", "lzbench_hip_deinit",
+                   "lzbench_hip_compress_batch", "lzbench_hip_decompress_batch"),
+    CompressorDesc("hip_nvcomp_lz4", "1.2.2", 0, 5, 1, 0, "lzbench_hip_nvcomp_lz4_compress",
+                   "lzbench_hip_nvcomp_lz4_decompress", "lzbench_hip_nvcomp_lz4_init", "lzbench_hip_deinit",
+                   "lzbench_hip_compress_batch", "lzbench_hip_decompress_batch"),
 )
 
 
@@ -191,7 +211,8 @@ class _Row:
 
     def __init__(self, codec: str, chunk_size: int, level: int = 0, ngpus: int = 1):
         L = lib()
-        base = {"memcpy": "memcpy", "snappy": "snappy", "zstd": "zstd", "zstd_fast": "zstd"}.get(codec, "lz4")
+        base = {"memcpy": "memcpy", "snappy": "snappy", "zstd": "zstd", "zstd_fast": "zstd", "lz4frame": "lz4frame",
+                "nvcomp_lz4": "nvcomp_lz4"}.get(codec, "lz4")
         self.desc = find_compressor("hipMemcpy" if codec == "memcpy" else codec)
         self.wm = getattr(L, f"lzbench_hip_{base}_init")(chunk_size, level, ngpus)
         if not self.wm:
@@ -213,7 +234,7 @@ class _Row:
 def _row_level(codec: str, level: int) -> int:
     """The level argument lzbench passes for the row: lz4fast acceleration, zstd level (zstd_fast
     rows are negative), 1 for lz4 (LZ4_compress_default), 0 for snappy; size_t on the wire."""
-    if codec in ("lz4fast", "zstd", "zstd_fast"):
+    if codec in _LEVELED:
         return level & 0xFFFFFFFFFFFFFFFF
     return 1 if codec == "lz4" else 0
 
@@ -262,7 +283,7 @@ class DeviceCodec:
         import torch
         self.torch = torch
         self.codec = CODECS[codec]
-        self.level = level if codec in ("lz4fast", "zstd", "zstd_fast") else (1 if codec == "lz4" else 0)
+        self.level = level if codec in _LEVELED else (1 if codec == "lz4" else 0)
         self.n, self.chunk_size = n, chunk_size
         L = lib()
         self.k = L.lzh_num_chunks(n, chunk_size)

@@ -56,7 +56,13 @@ size_t lzh_num_chunks(size_t n, size_t chunk_size) {
     return n == 0 ? 1 : (n + chunk_size - 1) / chunk_size;
 }
 
+static bool is_frame(int codec) { return codec == LZH_CODEC_LZ4F || codec == LZH_CODEC_NVLZ4; }
+
 static size_t codec_bound(int codec, size_t part) {
+    if (codec == LZH_CODEC_LZ4F)    // raw blocks at worst, 64 KiB blocks the smallest: header, block words, end
+        return part + 8 * ((part + 65535) / 65536) + 32;
+    if (codec == LZH_CODEC_NVLZ4)   // LZ4 blocks of 32 KiB at the least, 8-byte fields
+        return part + part / 255 + 24 * ((part + 32767) / 32768) + 48;
     if (codec == LZH_CODEC_LZ4) return part + part / 255 + 16;     // LZ4_compressBound, lz4.h:171
     if (codec == LZH_CODEC_SNAPPY) return 32 + part + part / 6;    // MaxCompressedLength, snappy.cc:99-121
     if (codec == LZH_CODEC_ZSTD)                                    // ZSTD_COMPRESSBOUND, zstd.h:~210
@@ -71,9 +77,70 @@ size_t lzh_max_packed_bytes(int codec, size_t n, size_t chunk_size) {
     return n + k * (codec_bound(codec, chunk_size) - chunk_size + 8) + 64;
 }
 
+// Framed layouts: frames of F bytes (the chunks) cut into blocks of bs = min(F, B) bytes
+struct FrameGeo {
+    size_t F, bs, nframes, nblocks;
+    uint32_t bpf;
+};
+
+static size_t frame_block_bytes(int codec, int level) {
+    if (codec == LZH_CODEC_LZ4F) { const int id = level & 7; return (size_t)1 << (8 + 2 * (id ? id : 4)); }
+    return (size_t)32768 << level;
+}
+
+static bool frame_level_ok(int codec, int level) {
+    if (codec == LZH_CODEC_LZ4F) { const int id = level & 7; return level >= 0 && level < (1 << 16) && (id == 0 || id >= 4) && !(level & 0x88); }
+    return level >= 0 && level <= 5;
+}
+
+static FrameGeo frame_geo(size_t B, size_t n, size_t F) {
+    FrameGeo g;
+    g.F = F;
+    g.bs = std::min(F, B);
+    g.bpf = (uint32_t)((F + g.bs - 1) / g.bs);
+    g.nframes = lzh_num_chunks(n, F);
+    if (n == 0) {
+        g.nblocks = 0;
+    } else {
+        const size_t last = n - (g.nframes - 1) * F;
+        g.nblocks = (g.nframes - 1) * g.bpf + (last + g.bs - 1) / g.bs;
+    }
+    return g;
+}
+
+// temp of a framed compression: staging slots | LZ4 sequence records (+ 8 B per block) | block
+// sizes | block offsets inside their frame
+struct FrameTemp { size_t stride, stage, recs, bcs, rel, total; };
+static FrameTemp frame_temp(const FrameGeo& g) {
+    FrameTemp t;
+    t.stride = lzh_stage_stride(LZH_CODEC_LZ4, g.bs);
+    t.stage = 0;
+    t.recs = align_up(g.nblocks * t.stride, 256) + 256;
+    t.bcs = t.recs + g.nblocks * lzh_lz4_rec_stride(g.bs) + align_up(g.nblocks * 8, 256) + 256;
+    t.rel = t.bcs + align_up(g.nblocks * 4, 256) + 256;
+    t.total = t.rel + align_up(g.nblocks * 4, 256) + 256;
+    return t;
+}
+
+static size_t frame_temp_worst(int codec, size_t n, size_t F) {
+    size_t t = 0;
+    for (int l = 0; l < 6; l++) {
+        const size_t B = codec == LZH_CODEC_LZ4F ? ((size_t)65536 << (2 * std::min(l, 3))) : ((size_t)32768 << l);
+        t = std::max(t, frame_temp(frame_geo(B, n, F)).total);
+    }
+    return t;
+}
+
+// decode side: maxbpf descriptor slots per frame (blocks of 64 KiB / 32 KiB at the least)
+static uint32_t frame_maxbpf(int codec, size_t F) {
+    const size_t bmin = codec == LZH_CODEC_LZ4F ? 65536 : 32768;
+    return (uint32_t)std::max<size_t>(1, (F + bmin - 1) / bmin);
+}
+
 size_t lzh_compress_temp_bytes(int codec, size_t n, size_t chunk_size) {
     size_t k = lzh_num_chunks(n, chunk_size);
     if (codec == LZH_CODEC_MEMCPY) return 256;
+    if (is_frame(codec)) return frame_temp_worst(codec, n, chunk_size) + 256;
     size_t t = align_up(k * lzh_stage_stride(codec, chunk_size), 256) + 256;
     if (codec == LZH_CODEC_LZ4 && chunk_size <= kLz4SplitMax)     // sequence records of the parse kernel
         t += k * lzh_lz4_rec_stride(chunk_size) + align_up(k * 8, 256) + 256;
@@ -88,8 +155,13 @@ size_t lzh_compress_temp_bytes(int codec, size_t n, size_t chunk_size) {
 }
 
 size_t lzh_decompress_temp_bytes(int codec, size_t n, size_t chunk_size) {
-    (void)codec;
-    return align_up((lzh_num_chunks(n, chunk_size) + 1) * sizeof(uint64_t), 256) + 256;
+    const size_t k = lzh_num_chunks(n, chunk_size);
+    size_t t = align_up((k + 1) * sizeof(uint64_t), 256) + 256;
+    if (is_frame(codec)) {   // block descriptors, block statuses, frame statuses
+        const size_t nd = k * frame_maxbpf(codec, chunk_size);
+        t += align_up(nd * 32, 256) + align_up(nd * 4, 256) + align_up(k * 4, 256) + 256;
+    }
+    return t;
 }
 
 int lzh_compress_kernel_stage(int codec, int level, int stage_mask, const void* d_in, size_t n, size_t in_readable,
@@ -118,6 +190,19 @@ int lzh_compress_kernel_stage(int codec, int level, int stage_mask, const void* 
             LZH_CHECK(lzh_launch_snappy_compress_v2((const uint8_t*)d_in, n, in_readable, chunk_size, (uint8_t*)d_stage,
                                                     stride, d_csizes, (uint32_t)k, s));
         }
+    } else if (is_frame(codec)) {
+        // (d_stage = the whole compression temp of a framed layout; d_csizes = frame sizes)
+        if (!frame_level_ok(codec, level)) return LZH_EARG;
+        const FrameGeo g = frame_geo(frame_block_bytes(codec, level), n, chunk_size);
+        const FrameTemp t = frame_temp(g);
+        uint8_t* base = (uint8_t*)d_stage;
+        uint32_t* bcs = (uint32_t*)(base + t.bcs);
+        const int acc = codec == LZH_CODEC_LZ4F ? std::max(1, (level >> 8) & 0xff) : 1;
+        LZH_CHECK(lzh_launch_lz4_split((const uint8_t*)d_in, n, in_readable, g.bs, acc, base + t.stage, t.stride, bcs,
+                                       (uint32_t)g.nblocks, base + t.recs, stage_mask, s, g.F, g.bpf));
+        if (stage_mask & 2)
+            LZH_CHECK(lzh_launch_frame_sizes(codec, level, n, g.F, g.bs, g.bpf, bcs, (uint32_t*)(base + t.rel), d_csizes,
+                                             (uint32_t)g.nframes, s));
     } else if (codec == LZH_CODEC_ZSTD) {
         if (!lzh_zstd_level_ok(level, chunk_size)) return LZH_EARG;
         uint8_t* scratch = (uint8_t*)d_stage + align_up(k * stride, 256) + 256;
@@ -132,6 +217,7 @@ int lzh_compress_kernel_stage(int codec, int level, int stage_mask, const void* 
 
 int lzh_compress_kernel_only(int codec, int level, const void* d_in, size_t n, size_t in_readable,
                              size_t chunk_size, void* d_stage, uint32_t* d_csizes, void* hip_stream) {
+    if (is_frame(codec)) return LZH_EARG;   // (framed layouts: lzh_compress_async)
     return lzh_compress_kernel_stage(codec, level, 3, d_in, n, in_readable, chunk_size, d_stage, d_csizes, hip_stream);
 }
 
@@ -159,6 +245,22 @@ int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t 
     }
     if (temp_bytes < lzh_compress_temp_bytes(codec, n, chunk_size) || !d_temp) return LZH_ESPACE;
     if (packed_cap < lzh_max_packed_bytes(codec, n, chunk_size)) return LZH_ESPACE;
+    if (is_frame(codec)) {   // blocks -> frame sizes -> frame offsets -> frames
+        if (!frame_level_ok(codec, level)) return LZH_EARG;
+        if (k > 0xffffffffu || chunk_size > 0x7fff0000u) return LZH_EARG;
+        int rc = lzh_compress_kernel_stage(codec, level, 3, d_in, n, in_readable, chunk_size, d_temp, d_csizes, hip_stream);
+        if (rc) return rc;
+        const FrameGeo g = frame_geo(frame_block_bytes(codec, level), n, chunk_size);
+        const FrameTemp t = frame_temp(g);
+        const uint8_t* base = (const uint8_t*)d_temp;
+        Range range("lzh:scan_pack");
+        LZH_CHECK(lzh_launch_scan(d_csizes, k, d_offsets, nullptr, s));
+        LZH_CHECK(lzh_launch_frame_pack(codec, level, (const uint8_t*)d_in, n, in_readable, g.F, g.bs, g.bpf,
+                                        base + t.stage, t.stride, (const uint32_t*)(base + t.bcs),
+                                        (const uint32_t*)(base + t.rel), d_csizes, d_offsets, (uint8_t*)d_packed,
+                                        (uint32_t)g.nblocks, (uint32_t)g.nframes, s));
+        return LZH_OK;
+    }
     int rc = lzh_compress_kernel_only(codec, level, d_in, n, in_readable, chunk_size, d_temp, d_csizes, hip_stream);
     if (rc) return rc;
     return lzh_compress_finish_async(codec, d_in, n, in_readable, chunk_size, d_temp, d_csizes, d_packed, packed_cap,
@@ -187,16 +289,35 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
                          void* d_temp, size_t temp_bytes, void* hip_stream) {
     hipStream_t s = (hipStream_t)hip_stream;
     if (!chunk_size || !d_csizes || !d_status || (n && (!d_out || !d_packed))) return LZH_EARG;
-    if (codec < 0 || codec > LZH_CODEC_ZSTD) return LZH_EARG;
+    if (codec < 0 || codec > LZH_CODEC_NVLZ4) return LZH_EARG;
     if (codec == LZH_CODEC_ZSTD && chunk_size > (1u << 30)) return LZH_EARG;
     const size_t k = lzh_num_chunks(n, chunk_size);
     if (n == 0) return LZH_OK;
     Range range("lzh:decompress");
     const uint64_t* offs = d_offsets;
-    if (!offs) {
+    if (!offs || is_frame(codec)) {
         if (!d_temp || temp_bytes < lzh_decompress_temp_bytes(codec, n, chunk_size)) return LZH_ESPACE;
+    }
+    if (!offs) {
         LZH_CHECK(lzh_launch_scan(d_csizes, k, (uint64_t*)d_temp, nullptr, s));
         offs = (const uint64_t*)d_temp;
+    }
+    if (is_frame(codec)) {   // frame headers -> block descriptors -> blocks -> frame checks
+        if (k > 0xffffffffu || chunk_size > 0x7fff0000u) return LZH_EARG;
+        const uint32_t mb = frame_maxbpf(codec, chunk_size);
+        const size_t nd = k * mb;
+        uint8_t* t = (uint8_t*)d_temp + align_up((k + 1) * sizeof(uint64_t), 256);
+        void* desc = t;
+        int32_t* bstat = (int32_t*)(t + align_up(nd * 32, 256));
+        int32_t* fstat = (int32_t*)(t + align_up(nd * 32, 256) + align_up(nd * 4, 256));
+        if (nd > 0xffffffffu) return LZH_EARG;
+        LZH_CHECK(lzh_launch_frame_parse(codec, (const uint8_t*)d_packed, packed_readable, offs, d_csizes, n, chunk_size,
+                                         mb, desc, fstat, (uint32_t)k, s));
+        LZH_CHECK(lzh_launch_decompress(LZH_CODEC_LZ4, (const uint8_t*)d_packed, packed_readable, nullptr, nullptr, n,
+                                        chunk_size, (uint8_t*)d_out, bstat, (uint32_t)nd, s, desc));
+        LZH_CHECK(lzh_launch_frame_finish(codec, (const uint8_t*)d_packed, offs, d_csizes, n, chunk_size, mb, desc,
+                                          bstat, fstat, (const uint8_t*)d_out, d_status, (uint32_t)k, s));
+        return LZH_OK;
     }
     if (codec == LZH_CODEC_ZSTD)
         LZH_CHECK(lzh_launch_zstd_decompress((const uint8_t*)d_packed, packed_readable, offs, d_csizes, n, chunk_size,
@@ -553,6 +674,8 @@ char* lzbench_hip_lz4_init(size_t chunk_size, size_t level, size_t ngpus) { (voi
 char* lzbench_hip_snappy_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_SNAPPY, chunk_size, ngpus); }
 char* lzbench_hip_memcpy_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_MEMCPY, chunk_size, ngpus); }
 char* lzbench_hip_zstd_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_ZSTD, chunk_size, ngpus); }
+char* lzbench_hip_lz4frame_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_LZ4F, chunk_size, ngpus); }
+char* lzbench_hip_nvcomp_lz4_init(size_t chunk_size, size_t level, size_t ngpus) { (void)level; return ctx_new(LZH_CODEC_NVLZ4, chunk_size, ngpus); }
 
 void lzbench_hip_deinit(char* wm) {
     LzhCtx* c = ctx_of(wm);
@@ -579,6 +702,18 @@ int64_t lzbench_hip_zstd_compress(char* in, size_t insize, char* out, size_t out
 }
 int64_t lzbench_hip_zstd_decompress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
     return one_chunk_decompress(LZH_CODEC_ZSTD, in, insize, out, outsize, wm);
+}
+int64_t lzbench_hip_lz4frame_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t, char* wm) {
+    return one_chunk_compress(LZH_CODEC_LZ4F, in, insize, out, outsize, level, wm);
+}
+int64_t lzbench_hip_lz4frame_decompress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
+    return one_chunk_decompress(LZH_CODEC_LZ4F, in, insize, out, outsize, wm);
+}
+int64_t lzbench_hip_nvcomp_lz4_compress(char* in, size_t insize, char* out, size_t outsize, size_t level, size_t, char* wm) {
+    return one_chunk_compress(LZH_CODEC_NVLZ4, in, insize, out, outsize, level, wm);
+}
+int64_t lzbench_hip_nvcomp_lz4_decompress(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
+    return one_chunk_decompress(LZH_CODEC_NVLZ4, in, insize, out, outsize, wm);
 }
 int64_t lzbench_hip_memcpy(char* in, size_t insize, char* out, size_t outsize, size_t, size_t, char* wm) {
     LzhCtx* c = ctx_of(wm);

@@ -148,3 +148,21 @@ __device__ __forceinline__ void bulk_literals(OutRing& R, const Bytes& in, int s
     if (lane < e - e4) R.put(e4 + lane, in.b(src + (e4 - pos) + lane));
     R.flushed = e4;
 }
+
+// Block i of a chunk list: plain chunks (bpf == 1: chunk i at i * bs), or the blocks of framed
+// layouts (frames of fs bytes, each cut into bpf blocks of bs; the last block of a frame and the
+// frames' last one are ragged).  false = past the input (an empty input still has block 0).
+__device__ __forceinline__ bool block_span(uint64_t i, uint64_t n_total, uint64_t bs, uint64_t fs, uint32_t bpf,
+                                           uint64_t& off, int& n) {
+    uint64_t lim = bs;
+    if (bpf == 1) {
+        off = i * bs;
+    } else {
+        const uint64_t f = i / bpf, b = i - f * bpf;
+        off = f * fs + b * bs;
+        lim = min(bs, fs - b * bs);
+    }
+    if (off >= n_total && !(n_total == 0 && i == 0)) return false;
+    n = (int)min(lim, n_total - off);
+    return true;
+}

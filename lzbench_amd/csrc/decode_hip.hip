@@ -740,26 +740,40 @@ __device__ int snappy_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_
 extern "C" __global__ void __launch_bounds__(64)
 lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                          const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
-                         int32_t* status, uint32_t chunk0) {
+                         int32_t* status, uint32_t chunk0, const uint32_t* desc) {
     // output window | start marks | input ring
     __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + 3 * LZH_WAVE + kRingBytes];
     const int lane = threadIdx.x;
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
-    const uint64_t ooff = chunk * chunk_size;
-    if (ooff >= n_total) return;
+    uint64_t ooff, ioff;
+    int part, cs;
+    bool raw;
+    if (desc) {   // framed layouts: one 32-byte block descriptor each (frame_hip.hip FrameDesc)
+        const uint32_t* d = desc + 8 * chunk;
+        ioff = (uint64_t)uni(d[1]) << 32 | uni(d[0]);
+        ooff = (uint64_t)uni(d[3]) << 32 | uni(d[2]);
+        cs = (int)uni(d[4]);
+        part = (int)uni(d[5]);
+        raw = (uni(d[6]) & 1u) != 0;
+        if (part == 0) { if (lane == 0) status[chunk] = 0; return; }   // unused slot
+    } else {
+        ooff = chunk * chunk_size;
+        if (ooff >= n_total) return;
+        part = (int)min(chunk_size, n_total - ooff);
+        ioff = offsets[chunk];
+        cs = (int)csizes[chunk];
+        raw = cs == part || codec == 2;
+    }
 #if LZH_DEC_STATS
     if (lane < 16) g_dst[lane] = 0;
     DCLK(tk0);
 #endif
-    const int part = (int)min(chunk_size, n_total - ooff);
-    const uint64_t ioff = offsets[chunk];
-    const int cs = (int)csizes[chunk];
     const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
     Bytes rin, rout;
     rin.init(packed + ioff, readable);
     rout.init(out + ooff, (uint64_t)part);
     int r;
-    if (cs == part || codec == 2) {
+    if (raw) {
         copy_raw(rin, rout, part, lane);
         r = part;
     } else {
@@ -1552,10 +1566,10 @@ lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, cons
 #include "launch.h"
 hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                  const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
-                                 int32_t* status, uint32_t nchunks, hipStream_t s) {
+                                 int32_t* status, uint32_t nchunks, hipStream_t s, const void* desc) {
     if (nchunks == 0) return hipSuccess;
     hipLaunchKernelGGL(lzh_decompress_v2_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
-                       offsets, csizes, n_total, chunk_size, out, status, 0u);
+                       offsets, csizes, n_total, chunk_size, out, status, 0u, (const uint32_t*)desc);
     return hipGetLastError();
 }
 

@@ -10,9 +10,10 @@ hipError_t lzh_launch_lz4_compress_v2(const uint8_t* in, uint64_t n_total, uint6
 hipError_t lzh_launch_snappy_compress_v2(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                                          uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
                                          hipStream_t s);
+// desc: 32-byte block descriptors (frame_hip.hip) instead of chunk geometry + offsets / csizes
 hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                  const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
-                                 int32_t* status, uint32_t nchunks, hipStream_t s);
+                                 int32_t* status, uint32_t nchunks, hipStream_t s, const void* desc = nullptr);
 hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                       const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                       int32_t* status, uint32_t nchunks, hipStream_t s);
@@ -27,12 +28,30 @@ hipError_t lzh_launch_zstd_compress(const uint8_t* in, uint64_t n_total, uint64_
                                     uint8_t* scratch, hipStream_t s);
 size_t lzh_zstd_scratch_stride(size_t chunk_size, int level);
 int lzh_zstd_level_ok(int level, size_t chunk_size);
+// frame_size / bpf: framed layouts (LZ4 frame, nvcomp container) -- block i is block i mod bpf of
+// frame i / bpf (frames of frame_size bytes cut into blocks of chunk_size); bpf <= 1: plain chunks
 hipError_t lzh_launch_lz4_split(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                                 uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
-                                int stage_mask, hipStream_t s);
+                                int stage_mask, hipStream_t s, uint64_t frame_size = 0, uint32_t bpf = 1);
 size_t lzh_lz4_rec_stride(uint64_t chunk_size);
 hipError_t lzh_launch_snappy_split(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                                    uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
                                    int stage_mask, hipStream_t s);
 size_t lzh_snappy_rec_stride(uint64_t chunk_size);
 uint32_t lzh_snappy_frags(uint64_t chunk_size);
+
+// framed LZ4 layouts (frame_hip.hip); codec 4 = LZ4 frame, 5 = nvcomp LZ4 container
+hipError_t lzh_launch_frame_sizes(int codec, int params, uint64_t n_total, uint64_t fs, uint64_t bs, uint32_t bpf,
+                                  const uint32_t* bcs, uint32_t* rel, uint32_t* csizes, uint32_t nframes, hipStream_t s);
+hipError_t lzh_launch_frame_pack(int codec, int params, const uint8_t* in, uint64_t n_total, uint64_t in_readable,
+                                 uint64_t fs, uint64_t bs, uint32_t bpf, const uint8_t* stage, uint64_t stride,
+                                 const uint32_t* bcs, const uint32_t* rel, const uint32_t* csizes,
+                                 const uint64_t* offsets, uint8_t* packed, uint32_t nblocks, uint32_t nframes,
+                                 hipStream_t s);
+hipError_t lzh_launch_frame_parse(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                                  const uint32_t* csizes, uint64_t n_total, uint64_t fs, uint32_t maxbpf, void* desc,
+                                  int32_t* fstat, uint32_t nframes, hipStream_t s);
+hipError_t lzh_launch_frame_finish(int codec, const uint8_t* packed, const uint64_t* offsets, const uint32_t* csizes,
+                                   uint64_t n_total, uint64_t fs, uint32_t maxbpf, const void* desc,
+                                   const int32_t* bstat, const int32_t* fstat, const uint8_t* out, int32_t* status,
+                                   uint32_t nframes, hipStream_t s);

@@ -1137,12 +1137,12 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
-                     uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr) {
+                     uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint64_t frame_size, uint32_t bpf) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + (LZH_PARSE_NORING ? 0 : lz4v3::kRing / 4 + 8)];   // table | ring + mirror
     const uint64_t chunk = blockIdx.x;
-    const uint64_t off = chunk * chunk_size;
-    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
-    const int n = (int)min(chunk_size, n_total - off);
+    uint64_t off;
+    int n;
+    if (!block_span(chunk, n_total, chunk_size, frame_size, bpf, off, n)) return;
     const uint64_t readable = min<uint64_t>(in_readable - off, (uint64_t)n + 64);
     Bytes rin, rout;
     rin.init(in + off, readable);
@@ -1239,14 +1239,14 @@ __device__ void put_seq_wave(OutR& R, const Bytes& in, int op, int anchor, int l
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                     const uint8_t* recs, uint64_t rec_stride, const uint32_t* rec_hdr, uint8_t* stage, uint64_t stride,
-                    uint32_t* csizes) {
+                    uint32_t* csizes, uint64_t frame_size, uint32_t bpf) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[lz4e::kRingB];
     __shared__ __attribute__((aligned(16))) uint32_t ibuf[lz4e::kSpan / 4 + 4];   // input span of a group
     const int lane = threadIdx.x;
     const uint64_t chunk = blockIdx.x;
-    const uint64_t off = chunk * chunk_size;
-    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
-    const int n = (int)min(chunk_size, n_total - off);
+    uint64_t off;
+    int n;
+    if (!block_span(chunk, n_total, chunk_size, frame_size, bpf, off, n)) return;
     Bytes in_b;
     in_b.init(in + off, min<uint64_t>(in_readable - off, (uint64_t)n + 64));
     const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
@@ -1360,16 +1360,17 @@ hipError_t lzh_launch_lz4_compress_v2(const uint8_t* in, uint64_t n_total, uint6
 // stage_mask bit 0 = parse, bit 1 = emit (profiling runs one of them)
 hipError_t lzh_launch_lz4_split(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                                 uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
-                                int stage_mask, hipStream_t s) {
+                                int stage_mask, hipStream_t s, uint64_t frame_size, uint32_t bpf) {
     if (nchunks == 0) return hipSuccess;
+    if (bpf <= 1) { bpf = 1; frame_size = chunk_size; }
     const uint64_t rs = lzh_lz4_rec_stride(chunk_size);
     uint32_t* hdr = (uint32_t*)(recs + rs * nchunks);
     if (stage_mask & 1)
         hipLaunchKernelGGL(lzh_lz4_parse_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable, chunk_size,
-                           acc, recs, rs, hdr);
+                           acc, recs, rs, hdr, frame_size, bpf);
     if (stage_mask & 2)
         hipLaunchKernelGGL(lzh_lz4_emit_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable, chunk_size,
-                           (const uint8_t*)recs, rs, (const uint32_t*)hdr, stage, stride, csizes);
+                           (const uint8_t*)recs, rs, (const uint32_t*)hdr, stage, stride, csizes, frame_size, bpf);
     return hipGetLastError();
 }
 

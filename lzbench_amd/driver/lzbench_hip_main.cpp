@@ -16,6 +16,7 @@
 #include <dirent.h>
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <strings.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -102,12 +103,19 @@ static compressor_desc_t comp_desc[] = {
      lzbench_hip_deinit, lzbench_hip_compress_batch, lzbench_hip_decompress_batch},
     {"hip_zstd_fast", "1.5.2", -5, -1, 1, 0, lzbench_hip_zstd_compress, lzbench_hip_zstd_decompress,
      lzbench_hip_zstd_init, lzbench_hip_deinit, lzbench_hip_compress_batch, lzbench_hip_decompress_batch},
+    // framed formats: an LZ4 frame per chunk (level = LZH_LZ4F_PARAMS: 4..7 = block size 64 KiB..4 MiB), and
+    // the nvcomp_lz4 row's container (lzbench.h:218, levels 0..5 = chunks of 32 KiB << level)
+    {"hip_lz4frame", "1.9.3", 4, 7, 1, 0, lzbench_hip_lz4frame_compress, lzbench_hip_lz4frame_decompress,
+     lzbench_hip_lz4frame_init, lzbench_hip_deinit, lzbench_hip_compress_batch, lzbench_hip_decompress_batch},
+    {"hip_nvcomp_lz4", "1.2.2", 0, 5, 1, 0, lzbench_hip_nvcomp_lz4_compress, lzbench_hip_nvcomp_lz4_decompress,
+     lzbench_hip_nvcomp_lz4_init, lzbench_hip_deinit, lzbench_hip_compress_batch, lzbench_hip_decompress_batch},
 };
 static const int kRows = (int)(sizeof(comp_desc) / sizeof(comp_desc[0]));
 
 struct alias_t { const char* name; const char* params; };
 static const alias_t aliases[] = {
     {"hip", "hipMemcpy/hip_lz4/hip_lz4fast,3,17/hip_snappy/hip_zstd,1"},
+    {"cuda", "hipMemcpy/hip_nvcomp_lz4,0,1,3,5"},   // the reference's GPU alias (lzbench.h:255) on its drop-in rows
     {"fast", "lz4/lz4fast,3,17/hip_lz4/hip_lz4fast,3,17/hip_snappy/hip_zstd_fast,-1/hip_zstd,1"},
     {"all", "lz4/lz4fast,3,17/hipMemcpy/hip_lz4/hip_lz4fast,3,17/hip_snappy/hip_zstd_fast/hip_zstd"},
 };
@@ -349,8 +357,6 @@ static const compressor_desc_t* find_row(const char* name) {
 static void bench_list(params_t* P, std::vector<size_t>& fs, const char* list, uint8_t* in, size_t insize, uint8_t* comp,
                        size_t compsize, uint8_t* dec) {
     std::string s(list);
-    for (const alias_t& a : aliases)
-        if (s == a.name) s = a.params;
     size_t pos = 0;
     while (pos <= s.size()) {
         size_t e = s.find('/', pos);
@@ -358,6 +364,14 @@ static void bench_list(params_t* P, std::vector<size_t>& fs, const char* list, u
         std::string item = s.substr(pos, e - pos);
         pos = e + 1;
         if (item.empty()) continue;
+        // an item naming an alias (case-insensitively) runs the alias' list (lzbench.cpp:493-501)
+        const alias_t* al = nullptr;
+        for (const alias_t& a : aliases)
+            if (!strcasecmp(item.c_str(), a.name)) al = &a;
+        if (al) {
+            bench_list(P, fs, al->params, in, insize, comp, compsize, dec);
+            continue;
+        }
         std::vector<std::string> parts;
         size_t q = 0;
         while (q <= item.size()) {

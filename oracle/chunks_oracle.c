@@ -18,17 +18,23 @@
 
 static int64_t compress_one(int codec, int level, const uint8_t* in, size_t part, uint8_t* out) {
     if (codec == 2) return oracle_zstd_compress(in, part, out, level);
+    if (codec == 3) return oracle_lz4f_compress(in, part, out, level);
+    if (codec == 4) return oracle_nvlz4_compress(in, part, out, level);
     if (codec == 0) return oracle_lz4_compress(in, (int)part, out, level < 1 ? 1 : level);
     return (int64_t)oracle_snappy_compress(in, part, out);
 }
 
 static size_t bound_one(int codec, size_t part) {
     if (codec == 2) return oracle_zstd_bound(part) + 64;
+    if (codec == 3) return oracle_lz4f_bound(part, 4);   /* (64 KiB blocks: the most block words, raw at worst) */
+    if (codec == 4) return oracle_nvlz4_bound(part, 0);
     return codec == 0 ? (size_t)oracle_lz4_bound((int)part) : oracle_snappy_bound(part);
 }
 
 static int64_t decompress_one(int codec, const uint8_t* in, size_t csize, uint8_t* out, size_t cap) {
     if (codec == 2) return -1;   /* zstd decoding: the reference build is the checker */
+    if (codec == 3) return oracle_lz4f_decompress(in, csize, out, cap);
+    if (codec == 4) return oracle_nvlz4_decompress(in, csize, out, cap);
     if (codec == 0) return oracle_lz4_decompress_safe(in, (int)csize, out, (int)cap);
     return oracle_snappy_uncompress(in, csize, out, cap);
 }

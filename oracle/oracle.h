@@ -44,9 +44,22 @@ int64_t oracle_snappy_uncompress(const uint8_t* src, size_t csize, uint8_t* dst,
 int64_t oracle_zstd_compress(const uint8_t* src, size_t n, uint8_t* dst, int level);
 size_t oracle_zstd_bound(size_t n);
 
+/* Framed LZ4 formats (frame_oracle.c).  LZ4 frame as LZ4F_compressFrame writes it with
+ * independent blocks (lz4frame.c:373-1019); params: bits 0-2 blockSizeID (0 = default 64 KiB, 4..7),
+ * 0x10 block checksum, 0x20 content checksum, 0x40 content size, bits 8-15 acceleration.
+ * nvcomp LZ4 container (nvcomp/LZ4Metadata.h): chunks of 1 << (15 + level) bytes, LZ4 blocks.
+ * Decoders return the decoded size, -1 on malformed input, -2 for an unsupported feature. */
+uint32_t oracle_xxh32(const uint8_t* p, size_t len, uint32_t seed);
+size_t  oracle_lz4f_bound(size_t n, int params);
+int64_t oracle_lz4f_compress(const uint8_t* src, size_t n, uint8_t* dst, int params);
+int64_t oracle_lz4f_decompress(const uint8_t* src, size_t csize, uint8_t* dst, size_t cap);
+size_t  oracle_nvlz4_bound(size_t n, int level);
+int64_t oracle_nvlz4_compress(const uint8_t* src, size_t n, uint8_t* dst, int level);
+int64_t oracle_nvlz4_decompress(const uint8_t* src, size_t csize, uint8_t* dst, size_t cap);
+
 /* lzbench chunk loop (reference _lzbench/lzbench.cpp:266-298): compress every chunk,
  * store raw when clen<=0 || clen==part, pack contiguously. codec: 0=lz4 1=snappy 2=zstd
- * (compression only).
+ * (compression only) 3=lz4 frame 4=nvcomp lz4 container (level = their params).
  * level: lz4 acceleration (0 or 1 -> default). Returns total packed bytes. */
 int64_t oracle_compress_chunks(int codec, int level, const uint8_t* in, size_t n,
                                size_t chunk_size, uint8_t* out, uint64_t* csizes);

@@ -13,13 +13,21 @@
  *   snappy adapters    /root/reference/_lzbench/compressors.cpp:1282-1292
  *   zstd adapters      /root/reference/_lzbench/compressors.cpp:1745-1778 (codec 2: ZSTD_getParams(level,
  *                      part, 0), contentSizeFlag = 1, ZSTD_compress_advanced; ZSTD_decompressDCtx)
+ *   codec 3            one LZ4 frame per chunk: LZ4F_compressFrame (lz4/lz4frame.c:429-470) with
+ *                      independent blocks and the requested block size / checksums / content size;
+ *                      LZ4F_decompress (lz4frame.c:1384) over the whole frame
+ *   codec 4            one nvcomp LZ4 container per chunk (nvcomp/LZ4Metadata.h layout, restated as in
+ *                      oracle/frame_oracle.c: nvcomp itself cannot be built) around reference
+ *                      LZ4_compress_default blocks of 1 << (15 + level) bytes
  */
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <memory>
 #include <thread>
 #include <vector>
 #include "lz4.h"
+#include "lz4frame.h"
 #include "snappy.h"
 #define ZSTD_STATIC_LINKING_ONLY   /* ZSTD_compress_advanced, as lzbench uses it */
 #include "zstd.h"
@@ -58,7 +66,86 @@ int64_t ref_zstd_decompress(const char* in, size_t csize, char* out, size_t cap)
 }
 int ref_zstd_version(void) { return (int)ZSTD_versionNumber(); }
 
+/* params as oracle_lz4f_compress: bits 0-2 blockSizeID (0 default), 0x10 block checksum, 0x20 content
+ * checksum, 0x40 content size, bits 8-15 acceleration (compressionLevel = -(acc - 1)) */
+static LZ4F_preferences_t lz4f_prefs(size_t n, int params) {
+    LZ4F_preferences_t p;
+    memset(&p, 0, sizeof(p));
+    p.frameInfo.blockSizeID = (LZ4F_blockSizeID_t)(params & 7);
+    p.frameInfo.blockMode = LZ4F_blockIndependent;
+    p.frameInfo.blockChecksumFlag = (params & 0x10) ? LZ4F_blockChecksumEnabled : LZ4F_noBlockChecksum;
+    p.frameInfo.contentChecksumFlag = (params & 0x20) ? LZ4F_contentChecksumEnabled : LZ4F_noContentChecksum;
+    p.frameInfo.contentSize = (params & 0x40) ? (unsigned long long)n : 0;
+    const int acc = (params >> 8) & 0xff;
+    p.compressionLevel = acc > 1 ? -(acc - 1) : 0;
+    return p;
+}
+size_t ref_lz4f_bound(size_t n, int params) {
+    LZ4F_preferences_t p = lz4f_prefs(n, params);
+    return LZ4F_compressFrameBound(n, &p);
+}
+int64_t ref_lz4f_compress(const char* in, size_t n, char* out, size_t cap, int params) {
+    LZ4F_preferences_t p = lz4f_prefs(n, params);
+    const size_t r = LZ4F_compressFrame(out, cap, in, n, &p);
+    return LZ4F_isError(r) ? -1 : (int64_t)r;
+}
+/* whole frame -> decoded size, -1 on any LZ4F error or a frame that does not end exactly at csize */
+int64_t ref_lz4f_decompress(const char* in, size_t csize, char* out, size_t cap) {
+    LZ4F_dctx* d = nullptr;
+    if (LZ4F_isError(LZ4F_createDecompressionContext(&d, LZ4F_VERSION))) return -1;
+    size_t ip = 0, op = 0;
+    int64_t res = -1;
+    for (;;) {
+        size_t isz = csize - ip, osz = cap - op;
+        const size_t r = LZ4F_decompress(d, out + op, &osz, in + ip, &isz, nullptr);
+        if (LZ4F_isError(r)) break;
+        ip += isz;
+        op += osz;
+        if (r == 0) { res = ip == csize ? (int64_t)op : -1; break; }
+        if (isz == 0 && osz == 0) break;   /* needs input it does not have: truncated */
+    }
+    LZ4F_freeDecompressionContext(d);
+    return res;
+}
+
+static void put64(char* p, uint64_t v) { memcpy(p, &v, 8); }   /* (x86: little endian) */
+int64_t ref_nvlz4_compress(const char* in, size_t n, char* out, size_t cap, int level) {
+    const size_t C = (size_t)1 << (15 + level), k = (n + C - 1) / C;
+    const uint64_t M = (4 + k + 1) * 8;
+    if (cap < M) return -1;
+    put64(out, 4); put64(out + 8, M); put64(out + 16, n); put64(out + 24, C);
+    uint64_t off = M;
+    for (size_t i = 0; i < k; i++) {
+        put64(out + 32 + 8 * i, off);
+        const int bs = (int)std::min(C, n - i * C);
+        const int r = LZ4_compress_default(in + i * C, out + off, bs, (int)(cap - off));
+        if (r <= 0) return -1;
+        off += (uint64_t)r;
+    }
+    put64(out + 32 + 8 * k, off);
+    return (int64_t)off;
+}
+int64_t ref_nvlz4_decompress(const char* in, size_t csize, char* out, size_t cap) {
+    uint64_t h[4];
+    if (csize < 40) return -1;
+    memcpy(h, in, 32);
+    if (h[0] != 4 || h[3] == 0 || h[2] > cap) return -1;
+    const uint64_t k = (h[2] + h[3] - 1) / h[3];
+    if (h[1] != (4 + k + 1) * 8 || h[1] > csize) return -1;
+    for (uint64_t i = 0; i < k; i++) {
+        uint64_t a, b;
+        memcpy(&a, in + 32 + 8 * i, 8);
+        memcpy(&b, in + 40 + 8 * i, 8);
+        const int bs = (int)std::min<uint64_t>(h[3], h[2] - i * h[3]);
+        if (a < h[1] || b < a || b > csize) return -1;
+        if (LZ4_decompress_safe(in + a, out + i * h[3], (int)(b - a), bs) != bs) return -1;
+    }
+    return (int64_t)h[2];
+}
+
 static int64_t one_compress(int codec, int level, const char* in, size_t part, char* out, size_t outpart) {
+    if (codec == 3) { const int64_t r = ref_lz4f_compress(in, part, out, outpart, level); return r < 0 ? 0 : r; }
+    if (codec == 4) { const int64_t r = ref_nvlz4_compress(in, part, out, outpart, level); return r < 0 ? 0 : r; }
     if (codec == 2) {
         const int64_t r = ref_zstd_compress(in, part, out, outpart, level);   /* zstd_fast rows pass -5..-1 */
         return r < 0 ? 0 : r;
@@ -74,6 +161,8 @@ static int64_t one_compress(int codec, int level, const char* in, size_t part, c
 
 static int64_t one_decompress(int codec, const char* in, size_t csize, char* out, size_t osize) {
     if (codec == 2) return ref_zstd_decompress(in, csize, out, osize);
+    if (codec == 3) return ref_lz4f_decompress(in, csize, out, osize);
+    if (codec == 4) return ref_nvlz4_decompress(in, csize, out, osize);
     if (codec == 0) { LZ4_decompress_fast(in, out, (int)osize); return (int64_t)osize; }
     snappy::RawUncompress(in, csize, out);
     return (int64_t)osize;

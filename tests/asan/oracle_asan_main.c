@@ -11,12 +11,12 @@ size_t lzb_datagen(int kind, uint64_t seed, uint8_t* buf, size_t n);
 
 static int roundtrip(int codec, const uint8_t* in, size_t n, size_t chunk, int level) {
     size_t k = (n + chunk - 1) / chunk;
-    uint8_t* packed = (uint8_t*)malloc(n + n / 6 + 16384 + 64 * k);
+    uint8_t* packed = (uint8_t*)malloc(n + n / 6 + 16384 + 64 * k + 64);
     uint64_t* cs = (uint64_t*)calloc(k ? k : 1, 8);
     uint8_t* out = (uint8_t*)malloc(n + 64);
     int64_t tot = oracle_compress_chunks(codec, level, in, n, chunk, packed, cs);
     int64_t tot_mt = 0;
-    uint8_t* packed2 = (uint8_t*)malloc(n + n / 6 + 16384 + 64 * k);
+    uint8_t* packed2 = (uint8_t*)malloc(n + n / 6 + 16384 + 64 * k + 64);
     uint64_t* cs2 = (uint64_t*)calloc(k ? k : 1, 8);
     tot_mt = oracle_compress_chunks_mt(codec, level, in, n, chunk, packed2, cs2, 3);
     int bad = tot <= 0 || tot != tot_mt || memcmp(packed, packed2, (size_t)tot) != 0;
@@ -44,6 +44,11 @@ int main(void) {
         bad |= roundtrip(2, buf, n, 131072, 1);
         bad |= roundtrip(2, buf, n, 262144, 1);
         bad |= roundtrip(2, buf, n, 65536, -3);
+        bad |= roundtrip(3, buf, n, 65536, 0);          /* LZ4 frames */
+        bad |= roundtrip(3, buf, n, 200000, 0x74);
+        bad |= roundtrip(3, buf, n, n, 7 | 0x30);
+        bad |= roundtrip(4, buf, n, 65536, 0);          /* nvcomp LZ4 containers */
+        bad |= roundtrip(4, buf, n, 300000, 2);
     }
     /* malformed streams must be rejected without reading or writing out of bounds */
     for (int t = 0; t < 2000; t++) {
@@ -51,6 +56,10 @@ int main(void) {
         for (int i = 0; i < 300; i++) junk[i] = (uint8_t)(rand() & 0xff);
         (void)oracle_lz4_decompress_safe(junk, 1 + t % 300, out, (int)sizeof(out));
         (void)oracle_snappy_uncompress(junk, 1 + t % 300, out, sizeof(out));
+        if (t & 1) { junk[0] = 0x04; junk[1] = 0x22; junk[2] = 0x4d; junk[3] = 0x18; }   /* LZ4F magic */
+        else { memset(junk, 0, 8); junk[0] = 4; }                                         /* nvcomp flag */
+        (void)oracle_lz4f_decompress(junk, 1 + t % 300, out, sizeof(out));
+        (void)oracle_nvlz4_decompress(junk, 1 + t % 300, out, sizeof(out));
     }
     free(buf);
     printf(bad ? "FAIL\n" : "ok\n");

@@ -42,6 +42,18 @@ def oracle():
         L.oracle_compress_chunks_mt.argtypes = [C.c_int, C.c_int, _P, _SZ, _SZ, _P, _P, C.c_int]
         L.oracle_decompress_chunks.restype = _I64
         L.oracle_decompress_chunks.argtypes = [C.c_int, _P, _P, _SZ, _SZ, _P]
+        L.oracle_lz4f_compress.restype = _I64
+        L.oracle_lz4f_compress.argtypes = [_P, _SZ, _P, C.c_int]
+        L.oracle_lz4f_decompress.restype = _I64
+        L.oracle_lz4f_decompress.argtypes = [_P, _SZ, _P, _SZ]
+        L.oracle_lz4f_bound.restype = _SZ
+        L.oracle_lz4f_bound.argtypes = [_SZ, C.c_int]
+        L.oracle_nvlz4_compress.restype = _I64
+        L.oracle_nvlz4_compress.argtypes = [_P, _SZ, _P, C.c_int]
+        L.oracle_nvlz4_decompress.restype = _I64
+        L.oracle_nvlz4_decompress.argtypes = [_P, _SZ, _P, _SZ]
+        L.oracle_xxh32.restype = C.c_uint32
+        L.oracle_xxh32.argtypes = [_P, _SZ, C.c_uint32]
         L.oracle_decompress_chunks_mt.restype = _I64
         L.oracle_decompress_chunks_mt.argtypes = [C.c_int, _P, _P, _SZ, _SZ, _P, C.c_int]
         _orc = L
@@ -78,11 +90,17 @@ def ref():
         L.ref_zstd_decompress.restype = _I64
         L.ref_zstd_decompress.argtypes = [_P, _SZ, _P, _SZ]
         L.ref_zstd_version.restype = C.c_int
+        L.ref_lz4f_compress.restype = _I64
+        L.ref_lz4f_compress.argtypes = [_P, _SZ, _P, _SZ, C.c_int]
+        L.ref_lz4f_decompress.restype = _I64
+        L.ref_lz4f_decompress.argtypes = [_P, _SZ, _P, _SZ]
+        L.ref_lz4f_bound.restype = _SZ
+        L.ref_lz4f_bound.argtypes = [_SZ, C.c_int]
         _ref = L
     return _ref
 
 
-CODEC_ID = {"lz4": 0, "lz4fast": 0, "snappy": 1, "zstd": 2}   # zstd: reference build only
+CODEC_ID = {"lz4": 0, "lz4fast": 0, "snappy": 1, "zstd": 2, "lz4f": 3, "nvlz4": 4}   # zstd decode: reference build only
 
 
 def lz4_compress(data: np.ndarray, acc: int = 1) -> bytes:
@@ -108,7 +126,7 @@ def compress_chunks(data: np.ndarray, codec: str, chunk: int, level: int = 1, us
     out = np.zeros(n + n // 6 + 16384 + 64 * k + 64, np.uint8)
     cs = np.zeros(k, np.uint64)
     c = CODEC_ID[codec]
-    lvl = level if codec in ("lz4fast", "zstd") else (1 if codec == "lz4" else 0)
+    lvl = level if codec in ("lz4fast", "zstd", "lz4f", "nvlz4") else (1 if codec == "lz4" else 0)
     if use_ref is None:
         use_ref = codec == "zstd" and have_ref()
     if use_ref:
@@ -127,7 +145,7 @@ def decompress_chunks(packed: np.ndarray, csizes: np.ndarray, n: int, codec: str
     c = CODEC_ID[codec]
     packed = np.ascontiguousarray(packed)
     cs = np.ascontiguousarray(csizes, dtype=np.uint64)
-    if use_ref or codec == "zstd":
+    if use_ref or codec == "zstd":   # (lz4f / nvlz4: the restatement unless use_ref)
         L = ref()
         r = (L.ref_decompress_chunks_mt(c, packed.ctypes.data, cs.ctypes.data, n, chunk, out.ctypes.data, threads)
              if threads else L.ref_decompress_chunks(c, packed.ctypes.data, cs.ctypes.data, n, chunk, out.ctypes.data))

@@ -98,7 +98,7 @@ def _full_rows(out):
     """(name, orig size, compr size, filename) of each row in the text+origSize format."""
     res = []
     for line in out.splitlines():
-        if "MB/s" in line:
+        if "MB/s" in line and not line.startswith("memcpy"):   # (memcpy's speed columns can run wide)
             p = line[23:].split()
             res.append((line[:23].strip(), int(p[4]), int(p[5]), " ".join(p[7:])))
     return res
@@ -142,3 +142,23 @@ def test_recursive_directories(tmp_path):
     assert names == ["a.txt", "b.json"]
     r = subprocess.run([EXE, "-elz4", "-t0,0", str(tmp_path)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "is a directory" in r.stderr
+
+
+def test_list_has_framed_rows_and_cuda_alias():
+    out = run(["-l"])
+    assert "hip_lz4frame 1.9.3" in out and "hip_nvcomp_lz4 1.2.2" in out
+    assert "cuda - alias for hipMemcpy/hip_nvcomp_lz4,0,1,3,5" in out
+
+
+@pytest.mark.gpu
+def test_gpu_framed_rows_match_restatement(sample):
+    """-ecuda (the reference's GPU alias) and the LZ4 frame row: sizes as the CPU restatement's."""
+    path, data = sample
+    out = run(["-ecuda/hip_lz4frame,4,7", "-b128", "-t0,0", "-i1,1", path])
+    assert "ERROR" not in out, out
+    r = rows(out)
+    for name, codec, lvl in (("hip_nvcomp_lz4 1.2.2 -0", "nvlz4", 0), ("hip_nvcomp_lz4 1.2.2 -5", "nvlz4", 5),
+                             ("hip_lz4frame 1.9.3 -4", "lz4f", 4), ("hip_lz4frame 1.9.3 -7", "lz4f", 7)):
+        key = [k for k in r if k.startswith(name)]
+        assert key, (name, out)
+        assert int(r[key[0]][4]) == len(O.compress_chunks(data, codec, 131072, lvl)[0]), (name, out)

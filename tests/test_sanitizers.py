@@ -19,7 +19,8 @@ def test_oracle_and_datagen_under_asan_ubsan(tmp_path):
         pytest.skip("gcc not available")
     exe = tmp_path / "oracle_asan"
     src = [os.path.join(ROOT, "tests", "asan", "oracle_asan_main.c")] + \
-          [os.path.join(ROOT, "oracle", f) for f in ("lz4_oracle.c", "snappy_oracle.c", "zstd1_oracle.c", "chunks_oracle.c")] + \
+          [os.path.join(ROOT, "oracle", f) for f in ("lz4_oracle.c", "snappy_oracle.c", "zstd1_oracle.c", "chunks_oracle.c",
+                                                     "frame_oracle.c")] + \
           [os.path.join(ROOT, "lzbench_amd", "csrc", "datagen.c")]
     subprocess.run(["gcc", "-std=gnu11", "-pthread", *SAN, "-o", str(exe), *src, "-lm"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=ENV, timeout=600)

@@ -8,7 +8,7 @@ out=$root/build/exp/$name
 mkdir -p $out
 cd $root/lzbench_amd/csrc
 objs=""
-for f in lz4c_hip snappyc_hip decode_hip pack_hip zstdc_hip; do
+for f in lz4c_hip snappyc_hip decode_hip pack_hip zstdc_hip frame_hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $flags -c $f.hip -o $out/$f.o &
   objs="$objs $out/$f.o"
 done
