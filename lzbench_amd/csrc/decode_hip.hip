@@ -819,14 +819,70 @@ extern "C" int lzh_debug_dec_stats(unsigned long long* host, int reset) {
 // frame content size is known), and the sequences are executed with the LZ4 decoder's group
 // emitter: up to 64 sequences per group, one output byte per lane per pass, through the LDS
 // output window.
-// Scope: frames as lzbench writes them (content size present, no dictionary, no checksum);
+// Scope: frames as lzbench writes them (content size present, no dictionary), with or without the
+// XXH64 content checksum (verified);
 // others return kErrUnsupported.  Valid frames decode to the reference's bytes; corrupt frames
 // are rejected without faulting (verdicts on corrupt input are not pinned to the reference's).
 namespace zstdd {
 
 constexpr int kZW = 2048;               // LDS output window (zstd offsets are mostly far anyway)
 typedef owin::SinkT<kZW> ZSink;
-constexpr int kErrCorrupt = -1, kErrUnsupported = -2;
+constexpr int kErrCorrupt = -1, kErrUnsupported = -2, kErrChecksum = -1;
+
+// XXH64 (seed 0) of out[0, len) -- /root/reference/zstd/lib/common/xxhash.h XXH64_endian_align --
+// by the whole wave: lane j loads 32-byte stripe j of each 2 KiB batch (L1-bypassing: the bytes
+// were just stored by this wave), the four accumulators take the stripes in order (wave-uniform)
+__device__ __forceinline__ uint64_t xxh_rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t xxh64_round(uint64_t acc, uint64_t in) {
+    return xxh_rotl64(acc + in * 0xC2B2AE3D27D4EB4FULL, 31) * 0x9E3779B185EBCA87ULL;
+}
+__device__ uint64_t xxh64_wave(const Bytes& b, int len, int lane) {
+    constexpr uint64_t P1 = 0x9E3779B185EBCA87ULL, P2 = 0xC2B2AE3D27D4EB4FULL, P3 = 0x165667B19E3779F9ULL,
+                       P4 = 0x85EBCA77C2B2AE63ULL, P5 = 0x27D4EB2F165667C5ULL;
+    auto rd32 = [&](int q) -> uint32_t {
+        return b.b_sc1(q) | (b.b_sc1(q + 1) << 8) | (b.b_sc1(q + 2) << 16) | (b.b_sc1(q + 3) << 24);
+    };
+    uint64_t h;
+    int p = 0;
+    if (len >= 32) {
+        uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0ull - P1;
+        const int ns = len / 32;
+        for (int s0 = 0; s0 < ns; s0 += 64) {
+            const int q = (s0 + lane) * 32;
+            const bool in = s0 + lane < ns;
+            uint32_t w[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) w[k] = in ? rd32(q + 4 * k) : 0u;
+            const int m = min(64, ns - s0);
+            for (int j = 0; j < m; j++) {
+                v1 = xxh64_round(v1, (uint64_t)rdlane(w[1], j) << 32 | rdlane(w[0], j));
+                v2 = xxh64_round(v2, (uint64_t)rdlane(w[3], j) << 32 | rdlane(w[2], j));
+                v3 = xxh64_round(v3, (uint64_t)rdlane(w[5], j) << 32 | rdlane(w[4], j));
+                v4 = xxh64_round(v4, (uint64_t)rdlane(w[7], j) << 32 | rdlane(w[6], j));
+            }
+        }
+        p = ns * 32;
+        h = xxh_rotl64(v1, 1) + xxh_rotl64(v2, 7) + xxh_rotl64(v3, 12) + xxh_rotl64(v4, 18);
+        h = (h ^ xxh64_round(0, v1)) * P1 + P4;
+        h = (h ^ xxh64_round(0, v2)) * P1 + P4;
+        h = (h ^ xxh64_round(0, v3)) * P1 + P4;
+        h = (h ^ xxh64_round(0, v4)) * P1 + P4;
+    } else {
+        h = P5;
+    }
+    h += (uint64_t)len;
+    for (; p + 8 <= len; p += 8) {
+        const uint64_t k = (uint64_t)uni(rd32(p + 4)) << 32 | uni(rd32(p));
+        h = xxh_rotl64(h ^ xxh64_round(0, k), 27) * P1 + P4;
+    }
+    if (p + 4 <= len) {
+        h = xxh_rotl64(h ^ ((uint64_t)uni(rd32(p)) * P1), 23) * P2 + P3;
+        p += 4;
+    }
+    for (; p < len; p++) h = xxh_rotl64(h ^ ((uint64_t)uni(b.b_sc1(p)) * P5), 11) * P1;
+    h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+    return h;
+}
 #ifndef LZH_ZSTD_DEBUG
 #define LZH_ZSTD_DEBUG 0
 #endif
@@ -1466,7 +1522,7 @@ __device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout,
     const uint32_t fhd = fbyte(fw, 4, lane);
     const int fcsf = (int)(fhd >> 6), single = (int)((fhd >> 5) & 1u);
     if (fhd & 8u) return ZC;                  // reserved bit
-    if (fhd & 4u) return kErrUnsupported;              // content checksum
+    const int ccrc = (fhd & 4u) ? 4 : 0;      // content checksum: XXH64 low 32 bits after the last block
     int p = 5;
     if (!single) {
         const uint32_t wd = fbyte(fw, p++, lane);
@@ -1525,7 +1581,14 @@ __device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout,
     ZCLK(F, 7);
     if (LZH_ZSTD_STATS && stats && lane == 0)
         for (int i = 0; i < kZClk; i++) atomicAdd(&stats[i], (unsigned long long)F.clk[i]);
-    if (op != n || p != cs) return ZC;
+    if (op != n || p + ccrc != cs) return ZC;
+    if (ccrc) {   // ZSTD_decompressFrame's checksum check (zstd_decompress.c:1011-1020), once the output is out
+        O.flush(op, lane);
+        wait_vm();
+        const uint32_t want = fword(fw, p, lane);
+        if ((uint32_t)xxh64_wave(O.out, op, lane) != want) return kErrChecksum;
+        O.flushed = op;
+    }
     return op;
 }
 

@@ -60,6 +60,15 @@ int64_t ref_zstd_compress(const char* in, size_t n, char* out, size_t cap, int l
     const size_t r = ZSTD_compress_advanced(zctx().c, out, cap, in, n, NULL, 0, p);
     return ZSTD_isError(r) ? -1 : (int64_t)r;
 }
+/* the same frame with the XXH64 content checksum (fParams.checksumFlag), for the decoder's checksum path */
+int64_t ref_zstd_compress_checksum(const char* in, size_t n, char* out, size_t cap, int level) {
+    ZSTD_parameters p = ZSTD_getParams(level, n, 0);
+    ZSTD_CCtx_setParameter(zctx().c, ZSTD_c_compressionLevel, level);
+    p.fParams.contentSizeFlag = 1;
+    p.fParams.checksumFlag = 1;
+    const size_t r = ZSTD_compress_advanced(zctx().c, out, cap, in, n, NULL, 0, p);
+    return ZSTD_isError(r) ? -1 : (int64_t)r;
+}
 int64_t ref_zstd_decompress(const char* in, size_t csize, char* out, size_t cap) {
     const size_t r = ZSTD_decompressDCtx(zctx().d, out, cap, in, csize);
     return ZSTD_isError(r) ? -1 : (int64_t)r;

@@ -90,6 +90,8 @@ def ref():
         L.ref_zstd_decompress.restype = _I64
         L.ref_zstd_decompress.argtypes = [_P, _SZ, _P, _SZ]
         L.ref_zstd_version.restype = C.c_int
+        L.ref_zstd_compress_checksum.restype = _I64
+        L.ref_zstd_compress_checksum.argtypes = [_P, _SZ, _P, _SZ, C.c_int]
         L.ref_lz4f_compress.restype = _I64
         L.ref_lz4f_compress.argtypes = [_P, _SZ, _P, _SZ, C.c_int]
         L.ref_lz4f_decompress.restype = _I64

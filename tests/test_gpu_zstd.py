@@ -121,3 +121,75 @@ def test_corrupt_frames(torch_cuda, corpus_kind):
         assert r == st[i], f"stream {i}: gpu accepted {st[i]} bytes, reference {r}"
         assert (out[i * chunk: i * chunk + r] == dst[:r]).all(), f"stream {i}: bytes differ"
     assert accepted > 0
+
+
+def _ref_checksum_frames(data, chunk, level):
+    R = O.ref()
+    frames = []
+    for i in range(0, len(data), chunk):
+        part = np.ascontiguousarray(data[i:i + chunk])
+        out = np.zeros(len(part) + len(part) // 8 + 1024, np.uint8)
+        r = R.ref_zstd_compress_checksum(part.ctypes.data, len(part), out.ctypes.data, len(out), level)
+        assert r > 0
+        frames.append(out[:r].tobytes())
+    return frames
+
+
+@pytest.mark.parametrize("kind,chunk,level", [("text", 131072, 1), ("json", 65536, 1), ("mixed", 1 << 20, 1),
+                                              ("random", 131072, 1), ("binary", 100000, -3)])
+def test_checksummed_frames(torch_cuda, kind, chunk, level):
+    """Frames with the XXH64 content checksum (fParams.checksumFlag): decoded and verified."""
+    if not O.have_ref():
+        pytest.skip("reference build (oracle/_ref) not present")
+    torch = torch_cuda
+    n = 3 * chunk + 777
+    data = L.datagen(kind, n, seed=13)
+    frames = _ref_checksum_frames(data, chunk, level)
+    frames = [f if len(f) != min(chunk, n - i * chunk) else None for i, f in enumerate(frames)]
+    if any(f is None for f in frames):
+        pytest.skip("a frame came out exactly chunk-sized (would read as stored raw)")
+    st, out = gpu_decode(torch, np.frombuffer(b"".join(frames), np.uint8), [len(f) for f in frames], n, chunk)
+    assert (st == expected_sizes(n, chunk)).all() and (out == data).all()
+    # a wrong checksum is rejected, as by the reference
+    bad = [bytearray(f) for f in frames]
+    for b in bad:
+        b[-1 - (len(b) % 4)] ^= 0x10
+    st2, _ = gpu_decode(torch, np.frombuffer(b"".join(bytes(b) for b in bad), np.uint8), [len(b) for b in bad], n, chunk)
+    R = O.ref()
+    for i, b in enumerate(bad):
+        src = np.frombuffer(bytes(b), np.uint8).copy()
+        dst = np.zeros(chunk + 64, np.uint8)
+        r = R.ref_zstd_decompress(src.ctypes.data, len(b), dst.ctypes.data, chunk)
+        assert (st2[i] >= 0) == (r >= 0), (i, st2[i], r)
+
+
+@pytest.mark.parametrize("corpus_kind", ["text", "json"])
+def test_corrupt_checksummed_frames_verdicts(torch_cuda, corpus_kind):
+    """Corrupted checksummed frames: with the content checksum on, the GPU decoder's verdict equals
+    the reference's (ZSTD_decompressDCtx) frame for frame, and accepted frames decode identically."""
+    if not O.have_ref():
+        pytest.skip("reference build (oracle/_ref) not present")
+    torch = torch_cuda
+    chunk = 32768
+    rng = np.random.default_rng(17 + len(corpus_kind))
+    data = L.datagen(corpus_kind, 8 * chunk, 41)
+    valid = _ref_checksum_frames(data, chunk, 1)
+    streams = []
+    while len(streams) < 1024:
+        s = _corrupt(rng, valid[int(rng.integers(0, len(valid)))])
+        if 0 < len(s) != chunk:
+            streams.append(s)
+    blob = np.frombuffer(b"".join(streams), np.uint8)
+    st, out = gpu_decode(torch, blob, [len(s) for s in streams], len(streams) * chunk, chunk)
+    R = O.ref()
+    mism = []
+    for i, s in enumerate(streams):
+        src = np.frombuffer(s, np.uint8).copy()
+        dst = np.zeros(chunk + 64, np.uint8)
+        r = R.ref_zstd_decompress(src.ctypes.data, len(s), dst.ctypes.data, chunk)
+        # (a frame of another content size is not this chunk's: lzbench's length check fails it)
+        if (st[i] == chunk) != (r == chunk):
+            mism.append((i, int(st[i]), int(r)))
+        elif r >= 0:
+            assert (out[i * chunk:(i + 1) * chunk] == dst[:chunk]).all(), f"stream {i}: bytes differ"
+    assert not mism, mism[:10]
