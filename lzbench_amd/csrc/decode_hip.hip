@@ -1257,48 +1257,77 @@ __device__ __forceinline__ int read_huf(ZWin& fw, const Bytes& src, int pos, int
     return used;
 }
 
-// literals of one Huffman stream set into out[dst .. dst + rs): 1 or 4 streams (1X1 / 4X1)
+// literals of one Huffman stream set into out[dst .. dst + rs): 1 or 4 streams (1X1 / 4X1,
+// huf_decompress.c HUF_decompress1X1 / 4X1_usingDTable), one stream per lane.  Lane j holds
+// stream j's backward bit container as in BackBits (64 bits c at bit offset D8, position P): a
+// container refill always moves down by exactly one dword (P - tl < D8 happens only once P is
+// within tl bits of D8), so the next dwords below are prefetched per lane, four at a time
+// (bank a in use, bank b in flight); the symbol lookup is a per-lane LDS read and each step
+// stores one byte per stream.  The streams' decoding chains run side by side in the lanes.
 __device__ __forceinline__ int huf_streams(const Bytes& src, int pos, int csize, int nstreams, const Bytes& out, int dst, int rs,
                             int tl, LDSA Lds& L, int lane) {
-    if (nstreams == 1) {
-        BackBits b;
-        if (!b.init(src, pos, csize, lane)) return ZC;
-        for (int i = 0; i < rs; i++) {
-            const uint32_t e = lds_u16(&L.huf[b.peek(tl, lane)]);
-            b.skip((int)(e >> 8));
-            if (lane == 0) out.st8(dst + i, e & 0xffu);
-        }
-        return b.left() == 0 ? 0 : ZC;
-    }
-    if (csize < 10) return ZC;
-    ZWin fw;
-    fw.bind(src, nullptr);
-    fw.load(pos, lane);
-    const int z1 = (int)(fword(fw, pos, lane) & 0xffffu), z2 = (int)(fword(fw, pos + 2, lane) & 0xffffu),
-              z3 = (int)(fword(fw, pos + 4, lane) & 0xffffu);
-    const int z4 = csize - 6 - z1 - z2 - z3;
-    if (z4 < 1) return ZC;
-    const int seg = (rs + 3) / 4, last = rs - 3 * seg;
-    if (last < 0) return ZC;
-    BackBits b0, b1, b2, b3;
-    const int p1 = pos + 6;
-    if (!b0.init(src, p1, z1, lane) || !b1.init(src, p1 + z1, z2, lane) || !b2.init(src, p1 + z1 + z2, z3, lane) ||
-        !b3.init(src, p1 + z1 + z2 + z3, z4, lane))
+    int seg = rs, last = rs, s0 = pos, sz = csize;   // this lane's stream: [s0, s0 + sz), seg (or last) symbols
+    if (nstreams == 4) {
+        if (csize < 10) return ZC;
+        ZWin fw;
+        fw.bind(src, nullptr);
+        fw.load(pos, lane);
+        const int z1 = (int)(fword(fw, pos, lane) & 0xffffu), z2 = (int)(fword(fw, pos + 2, lane) & 0xffffu),
+                  z3 = (int)(fword(fw, pos + 4, lane) & 0xffffu);
+        const int z4 = csize - 6 - z1 - z2 - z3;
+        if (z4 < 1) return ZC;
+        seg = (rs + 3) / 4;
+        last = rs - 3 * seg;
+        if (last < 0) return ZC;
+        if (z1 <= 0 || z2 <= 0 || z3 <= 0) return ZC;
+        const int p1 = pos + 6;
+        s0 = lane == 0 ? p1 : (lane == 1 ? p1 + z1 : (lane == 2 ? p1 + z1 + z2 : p1 + z1 + z2 + z3));
+        sz = lane == 0 ? z1 : (lane == 1 ? z2 : (lane == 2 ? z3 : z4));
+    } else if (csize <= 0) {
         return ZC;
-    for (int i = 0; i < seg; i++) {
-        const uint32_t e0 = lds_u16(&L.huf[b0.peek(tl, lane)]);
-        const uint32_t e1 = lds_u16(&L.huf[b1.peek(tl, lane)]);
-        const uint32_t e2 = lds_u16(&L.huf[b2.peek(tl, lane)]);
-        b0.skip((int)(e0 >> 8)); b1.skip((int)(e1 >> 8)); b2.skip((int)(e2 >> 8));
-        uint32_t e3 = 0;
-        if (i < last) {
-            e3 = lds_u16(&L.huf[b3.peek(tl, lane)]);
-            b3.skip((int)(e3 >> 8));
-        }
-        const uint32_t v = lane == 0 ? e0 : (lane == 1 ? e1 : (lane == 2 ? e2 : e3));
-        if (lane < 3 || (lane == 3 && i < last)) out.st8(dst + lane * seg + i, v & 0xffu);
     }
-    return (b0.left() == 0 && b1.left() == 0 && b2.left() == 0 && b3.left() == 0) ? 0 : ZC;
+    const bool on = lane < nstreams;
+    const int nsym = lane == 3 ? last : seg;           // symbols of this lane's stream
+    const rsrc_t r = src.r;
+    const int x0 = s0 + src.sh;
+    const int X = x0 + sz - 1;                          // the stream's last byte holds the end mark
+    const uint32_t lastb = on ? ld_u8(r, X) : 1u;
+    if (ballot(on && lastb == 0)) return ZC;
+    const int lo = 8 * x0;
+    int P = 8 * X + hb32(lastb);
+    int D8 = ((P - 32) >> 5) << 5;
+    int D = D8 >> 3;                                    // (dword aligned; below 0 reads as 0)
+    uint64_t c = on ? (((uint64_t)ld_b32(r, D + 4) << 32) | ld_b32(r, D)) : 0ull;
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+    if (on) {
+        a0 = ld_b32(r, D - 4); a1 = ld_b32(r, D - 8); a2 = ld_b32(r, D - 12); a3 = ld_b32(r, D - 16);
+        b0 = ld_b32(r, D - 20); b1 = ld_b32(r, D - 24); b2 = ld_b32(r, D - 28); b3 = ld_b32(r, D - 32);
+    }
+    int na = 4, nxt = D - 36;                           // dwords left in bank a; next dword to fetch
+    const uint32_t mask = (1u << tl) - 1u;
+    for (int i = 0; i < seg; i++) {
+        const bool act = on && i < nsym;
+        if (act && P - tl < D8) {                       // container refill: one dword down
+            c = (c << 32) | a0;
+            a0 = a1; a1 = a2; a2 = a3;
+            D8 -= 32;
+            if (--na == 0) {                            // bank b becomes a, the next four are fetched
+                a0 = b0; a1 = b1; a2 = b2; a3 = b3;
+                b0 = ld_b32(r, nxt); b1 = ld_b32(r, nxt - 4); b2 = ld_b32(r, nxt - 8); b3 = ld_b32(r, nxt - 12);
+                nxt -= 16;
+                na = 4;
+            }
+        }
+        const int sh = P - tl - D8;
+        uint32_t v = (uint32_t)(c >> (sh & 63)) & mask;
+        if (P - tl < lo) v &= (uint32_t)(~0ull << min(lo - (P - tl), 63));   // zero-padded below the start
+        const uint32_t e = ((volatile const LDSA uint16_t*)L.huf)[act ? v : 0];
+        if (act) {
+            P -= (int)(e >> 8);
+            out.st8(dst + lane * seg + i, e & 0xffu);
+        }
+    }
+    return ballot(on && P != lo) ? ZC : 0;
 }
 
 struct FrameState {
