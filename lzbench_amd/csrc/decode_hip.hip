@@ -933,6 +933,7 @@ struct Lds {
     uint8_t weights[256];
     int16_t norm[256];
     uint16_t next[256];
+    uint32_t base[36 + 53];             // literal-length / match-length baselines (kLLBase, kMLBase)
 };
 
 __device__ __forceinline__ uint32_t lds_u32(const LDSA uint32_t* p) { return uni(*(volatile const LDSA uint32_t*)p); }
@@ -1019,6 +1020,59 @@ struct BackBits {
         return v;
     }
     __device__ __forceinline__ void skip(int n) { P -= n; }
+};
+
+// value in a VGPR as far as the compiler knows (keeps wave-uniform chains out of the SGPR budget)
+__device__ __forceinline__ int vgpr(int x) {
+    int y;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+    return y;
+}
+
+// The sequences' backward bit stream with its state in vector registers (BackBits' container
+// semantics): every read takes n <= 32 bits after making sure P - n >= D8, so a refill always
+// moves the 64-bit container down by exactly one dword; the next eight dwords below are kept
+// prefetched (bank a in use, bank b in flight).
+struct SeqBits {
+    rsrc_t r;
+    int P, D8, lo, na, nxt;
+    uint64_t c;
+    uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+    __device__ __forceinline__ bool init(const Bytes& src, int start, int size) {
+        r = src.r;
+        const int x0 = vgpr(start + src.sh);
+        if (size <= 0) return false;
+        const int X = x0 + size - 1;
+        const uint32_t last = ld_u8(r, X);
+        if (last == 0) return false;
+        lo = 8 * x0;
+        P = 8 * X + hb32(last);
+        D8 = ((P - 32) >> 5) << 5;
+        const int D = D8 >> 3;
+        c = ((uint64_t)ld_b32(r, D + 4) << 32) | ld_b32(r, D);
+        a0 = ld_b32(r, D - 4); a1 = ld_b32(r, D - 8); a2 = ld_b32(r, D - 12); a3 = ld_b32(r, D - 16);
+        b0 = ld_b32(r, D - 20); b1 = ld_b32(r, D - 24); b2 = ld_b32(r, D - 28); b3 = ld_b32(r, D - 32);
+        na = 4;
+        nxt = D - 36;
+        return true;
+    }
+    __device__ __forceinline__ int left() const { return P - lo; }
+    __device__ __forceinline__ uint32_t get(int n) {
+        if (P - n < D8) {
+            c = (c << 32) | a0;
+            a0 = a1; a1 = a2; a2 = a3;
+            D8 -= 32;
+            if (--na == 0) {
+                a0 = b0; a1 = b1; a2 = b2; a3 = b3;
+                b0 = ld_b32(r, nxt); b1 = ld_b32(r, nxt - 4); b2 = ld_b32(r, nxt - 8); b3 = ld_b32(r, nxt - 12);
+                nxt -= 16;
+                na = 4;
+            }
+        }
+        const uint32_t v = (uint32_t)((c >> (P - n - D8)) & ((1ull << n) - 1ull));
+        P -= n;
+        return v;
+    }
 };
 
 // FSE_readNCount (entropy_common.c:70-215) over the frame from byte pos: normalized counts
@@ -1429,41 +1483,49 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
         u = seq_table(fw, p, be, (int)((modes >> 2) & 3u), 2, L.ml, F.mlA, F.mlV, L, lane);
         if (u < 0) return ZC;
         p += u;
-        // ---- sequences (ZSTD_decodeSequence), executed a group at a time
+        // ---- sequences (ZSTD_decodeSequence), executed a group at a time.  The decoding chain
+        // (bit reader, FSE states, repcodes, lengths, the group being filled) lives in vector
+        // registers (every lane holds the same value: vgpr() hides the uniformity from the
+        // compiler), so the frame's scalar state is not spilled to VGPR lanes and back around
+        // every sequence; table lookups are LDS reads at one address per wave.
         ZCLK(F, 3);
-        BackBits sb;
-        if (!sb.init(rin, p, be - p, lane)) return ZC;
-        uint32_t sLL = sb.get(F.llA, lane), sOF = sb.get(F.ofA, lane), sML = sb.get(F.mlA, lane);
-        int k = 0, glit = 0, gout = 0;                // group: members, literal bytes, output bytes
+        SeqBits sb;
+        if (!sb.init(rin, p, be - p)) return ZC;
+        uint32_t sLL = sb.get(F.llA), sOF = sb.get(F.ofA), sML = sb.get(F.mlA);
+        int rep0 = vgpr(F.rep0), rep1 = vgpr(F.rep1), rep2 = vgpr(F.rep2);
+        int k = vgpr(0), glit = vgpr(0), gout = vgpr(0);   // group: members, literal bytes, output bytes
+        const int lrem0 = vgpr(rs - lp), opv = vgpr(op), fcsv = vgpr(fcs);
         uint32_t g_lit = 0, g_ml = 0, g_off = 0, g_ex = 0, g_lrel = 0;
-        bool pend_big = false;
-        int big_ll = 0, big_ml = 0, big_off = 0;
+        const volatile LDSA uint32_t* llT = (const volatile LDSA uint32_t*)L.ll;
+        const volatile LDSA uint32_t* mlT = (const volatile LDSA uint32_t*)L.ml;
+        const volatile LDSA uint32_t* ofT = (const volatile LDSA uint32_t*)L.of;
+        int lpv = 0, opg = 0;                         // literals / output bytes of the groups emitted
         for (int i = 0; i < nseq; i++) {
-            const Cell eL = lds_cell(&L.ll[sLL]), eO = lds_cell(&L.of[sOF]), eM = lds_cell(&L.ml[sML]);
+            const Cell eL = llT[sLL], eO = ofT[sOF], eM = mlT[sML];
             const int ofc = (int)c_sym(eO);
-            int off;
             const int llc = (int)c_sym(eL), mlc = (int)c_sym(eM);
             const int ll0 = llc == 0;                 // (only literal-length code 0 has baseline 0)
+            int off;
             if (ofc > 1) {
-                off = (int)((1u << ofc) - 3u + sb.get(ofc, lane));
-                F.rep2 = F.rep1; F.rep1 = F.rep0; F.rep0 = off;
+                off = (int)((1u << ofc) - 3u + sb.get(ofc));
+                rep2 = rep1; rep1 = rep0; rep0 = off;
             } else if (ofc == 0) {
-                off = ll0 ? F.rep1 : F.rep0;
-                if (ll0) { F.rep1 = F.rep0; F.rep0 = off; }
+                off = ll0 ? rep1 : rep0;
+                if (ll0) { rep1 = rep0; rep0 = off; }
             } else {
-                const int idx = 1 + ll0 + (int)sb.get(1, lane);   // 1..3
-                int t = idx == 3 ? F.rep0 - 1 : (idx == 1 ? F.rep1 : F.rep2);
+                const int idx = 1 + ll0 + (int)sb.get(1);   // 1..3
+                int t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
                 t += t == 0;                          // (as the reference: offset 0 becomes 1)
-                if (idx != 1) F.rep2 = F.rep1;
-                F.rep1 = F.rep0;
-                F.rep0 = off = t;
+                if (idx != 1) rep2 = rep1;
+                rep1 = rep0;
+                rep0 = off = t;
             }
-            const int ml = (int)kMLBase[mlc] + (int)sb.get(c_add(eM), lane);
-            const int ll = (int)kLLBase[llc] + (int)sb.get(c_add(eL), lane);
+            const int ml = (int)L.base[36 + mlc] + (int)sb.get(c_add(eM));
+            const int ll = (int)L.base[llc] + (int)sb.get(c_add(eL));
             if (i + 1 < nseq) {                       // state updates: LL, ML, OF
-                sLL = c_next(eL) + sb.get(c_nb(eL), lane);
-                sML = c_next(eM) + sb.get(c_nb(eM), lane);
-                sOF = c_next(eO) + sb.get(c_nb(eO), lane);
+                sLL = c_next(eL) + sb.get(c_nb(eL));
+                sML = c_next(eM) + sb.get(c_nb(eM));
+                sOF = c_next(eO) + sb.get(c_nb(eO));
                 if (sb.left() < 0) return ZC;
             } else {
                 // the reference also updates the states after the last sequence and then accepts
@@ -1472,37 +1534,35 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
                 if (sb.left() > extra || sb.left() < 0) return ZC;
             }
             // validity (ZSTD_execSequence): literals available, offset within the output, room
-            const int o0 = op + gout;                 // output position of this sequence
-            if (ll > rs - lp - glit || off > o0 + ll || (int64_t)o0 + ll + ml > (int64_t)(fcs - (rs - lp - glit - ll)))
-                return ZC;
+            const int lrem = lrem0 - lpv - glit;      // literals not yet taken
+            const int o0 = opv + opg + gout;          // output position of this sequence
+            if (ll > lrem || off > o0 + ll || (int64_t)o0 + ll + ml > (int64_t)(fcsv - (lrem - ll))) return ZC;
             const bool big = ll > 255 || ml > 4095;
             if (big || k == LZH_WAVE || glit + ll > 384) {
                 // emit the pending group
                 if (k > 0) {
-                    const int ip = lpos + lp;
-                    if (!lw.covers(ip, ip + glit + 16)) lw.load(ip, lane);
-                    const uint64_t keep = k == LZH_WAVE ? ~0ull : ((1ull << k) - 1ull);
+                    const int kk = unii(k), gl = unii(glit), go = unii(gout), lpu = unii(lpv), opu = unii(op + opg);
+                    const int ip = lpos + lp + lpu;
+                    if (!lw.covers(ip, ip + gl + 16)) lw.load(ip, lane);
+                    const uint64_t keep = kk == LZH_WAVE ? ~0ull : ((1ull << kk) - 1ull);
                     ZCLK(F, 4);
-                    groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kZW, ip, op, gout, keep, (int)g_ex,
+                    groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kZW, ip, opu, go, keep, (int)g_ex,
                                        g_lit | (g_ml << 16), g_lrel, (int)g_off, lane);
                     ZCLK(F, 5);
-                    op += gout;
-                    lp += glit;
+                    opg += gout;
+                    lpv += glit;
                     k = 0; glit = 0; gout = 0;
                 }
-                pend_big = big;
-                big_ll = ll; big_ml = ml; big_off = off;
-            }
-            if (pend_big) {                           // a long sequence on its own
-                ZCLK(F, 4);
-                O.literals(lw, lsrc, lpos + lp, op, big_ll, lane);
-                op += big_ll;
-                lp += big_ll;
-                O.match(op, big_off, big_ml, lane);
-                op += big_ml;
-                ZCLK(F, 6);
-                pend_big = false;
-                continue;
+                if (big) {                            // a long sequence on its own
+                    const int bl = unii(ll), bm = unii(ml), bo = unii(off), lpu = unii(lpv), opu = unii(op + opg);
+                    ZCLK(F, 4);
+                    O.literals(lw, lsrc, lpos + lp + lpu, opu, bl, lane);
+                    O.match(opu + bl, bo, bm, lane);
+                    ZCLK(F, 6);
+                    opg += ll + ml;
+                    lpv += ll;
+                    continue;
+                }
             }
             g_lit = lane == k ? (uint32_t)ll : g_lit;
             g_ml = lane == k ? (uint32_t)ml : g_ml;
@@ -1513,17 +1573,21 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
             glit += ll;
             gout += ll + ml;
         }
-        if (k > 0) {
-            const int ip = lpos + lp;
-            if (!lw.covers(ip, ip + glit + 16)) lw.load(ip, lane);
-            const uint64_t keep = k == LZH_WAVE ? ~0ull : ((1ull << k) - 1ull);
+        if (unii(k) > 0) {
+            const int kk = unii(k), gl = unii(glit), go = unii(gout), lpu = unii(lpv), opu = unii(op + opg);
+            const int ip = lpos + lp + lpu;
+            if (!lw.covers(ip, ip + gl + 16)) lw.load(ip, lane);
+            const uint64_t keep = kk == LZH_WAVE ? ~0ull : ((1ull << kk) - 1ull);
             ZCLK(F, 4);
-            groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kZW, ip, op, gout, keep, (int)g_ex, g_lit | (g_ml << 16),
+            groups::emit_group(lw, O, (LDSA uint8_t*)L.win + kZW, ip, opu, go, keep, (int)g_ex, g_lit | (g_ml << 16),
                                g_lrel, (int)g_off, lane);
             ZCLK(F, 5);
-            op += gout;
-            lp += glit;
+            opg += gout;
+            lpv += glit;
         }
+        op += unii(opg);
+        lp += unii(lpv);
+        F.rep0 = unii(rep0); F.rep1 = unii(rep1); F.rep2 = unii(rep2);
     } else if (p != be) {
         return ZC;
     }
@@ -1623,7 +1687,10 @@ __device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout,
 
 }  // namespace zstdd
 
-extern "C" __global__ void __launch_bounds__(64)
+#ifndef LZH_ZSTD_MINW
+#define LZH_ZSTD_MINW 1   // waves per SIMD the register allocation must allow (LDS allows 3)
+#endif
+extern "C" __global__ void __launch_bounds__(64, LZH_ZSTD_MINW)
 lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                            const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                            int32_t* status, uint32_t chunk0, unsigned long long* stats) {
@@ -1647,6 +1714,8 @@ lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, cons
         r = part;
     } else {
         zstdd::ZSink O{(LDSA uint8_t*)L.win, rout, 0, 0};
+        for (int i = lane; i < 36 + 53; i += LZH_WAVE) L.base[i] = i < 36 ? zstdd::kLLBase[i] : zstdd::kMLBase[i - 36];
+        wave_lds_fence();
         Bytes lout;
         lout.init(out + ooff, (uint64_t)part + 3);
         r = zstdd::decode_frame(rin, lout, cs, O, L, part, lane, stats);
