@@ -306,49 +306,72 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             A = A32; D = D32; s = s32; nx = n32;
         }
         if (ended) break;
-        // ---- the match
-        int mstart, mpos, len, cur0, ip1;
+        // ---- the match.  m0 / p0: its start and source before the backward extension; the bytes
+        // of the backward and forward compares and the literal run [anchor, m0) are loaded in one
+        // round trip (the forward count from m0 + 4 does not depend on the backward extension; the
+        // literal copy writes past the final literal count when it extends, and the next run
+        // overwrites those bytes)
+        int m0, p0, bmax, cur0, ip1;
         uint32_t offBase;
         if (kind == 1) {
-            mstart = eA + eD;
-            mpos = mstart - (int)r1;
-            const int back = in.b(mstart - 1) == in.b(mpos - 1);
-            mstart -= back;
-            mpos -= back;
-            len = 4 + back;
+            m0 = eA + eD;
+            p0 = m0 - (int)r1;
+            bmax = 1;                                     // ip0[-1] == match0[-1], zstd_fast.c:204-211
             offBase = 1;
             cur0 = eA;
             ip1 = eA + 1;
         } else {
-            mstart = kind == 2 ? eA : eA + 1;
-            mpos = ecand - 1;
+            m0 = kind == 2 ? eA : eA + 1;
+            p0 = ecand - 1;
             r2 = r1;
-            r1 = (uint32_t)(mstart - mpos);
+            r1 = (uint32_t)(m0 - p0);
             offBase = r1 + 3;
-            cur0 = mstart;
+            cur0 = m0;
             ip1 = kind == 2 ? eA + 1 : eA + eD;
-            const int bmax = min(mstart - anchor, mpos - pstart);
-            const int bk = bmax > 0 ? count_bwd(in, mstart, mpos, bmax, lane) : 0;
-            mstart -= bk;
-            mpos -= bk;
-            len = 4 + bk;
+            bmax = max(0, min(m0 - anchor, p0 - pstart));
         }
-        len += count_fwd(in, mstart + len, mpos + len, be - (mstart + len), lane);
-        copy_span(in, anchor, O.lits, O.nl, mstart - anchor, lane, LZH_WAVE);
+        const int fmax = be - (m0 + 4);
+        const bool bl = lane < bmax, fl = 4 * lane < fmax;
+        const uint32_t ba = bl ? in.b(m0 - 1 - lane) : 0u, bb = bl ? in.b(p0 - 1 - lane) : 0u;
+        const uint32_t fa = fl ? ld_u32(in.r, m0 + 4 + 4 * lane + in.sh) : 0u,
+                       fb = fl ? ld_u32(in.r, p0 + 4 + 4 * lane + in.sh) : 0u;
+        copy_span(in, anchor, O.lits, O.nl, m0 - anchor, lane, LZH_WAVE);
+        int bk;
+        {
+            const uint64_t m = ballot(!bl || ba != bb);
+            bk = m ? ffs64(m) : LZH_WAVE;
+            if (!m && bmax > LZH_WAVE) bk = LZH_WAVE + count_bwd(in, m0 - LZH_WAVE, p0 - LZH_WAVE, bmax - LZH_WAVE, lane);
+            bk = min(bk, bmax);
+        }
+        int fw;
+        {
+            const uint32_t x = fa ^ fb;
+            int eq = x ? (int)(__builtin_ctz(x) >> 3) : 4;
+            if (4 * lane + eq > fmax) eq = fmax - 4 * lane;
+            const bool st = fl && eq < 4;
+            const uint64_t m = ballot(st);
+            if (m) fw = 4 * ffs64(m) + (int)rdlane((uint32_t)eq, ffs64(m));
+            else fw = fmax <= 256 ? max(fmax, 0) : 256 + count_fwd(in, m0 + 4 + 256, p0 + 4 + 256, fmax - 256, lane);
+        }
+        const int mstart = m0 - bk;
+        const int len = 4 + bk + fw;
         O.nl += mstart - anchor;
         O.put(lane, (uint32_t)(mstart - anchor), offBase, (uint32_t)len);
         ip = mstart + len;
         anchor = ip;
-        if (lane == 0) {
-            if (ip1 < ip) tab_put_pos(T, in, ip1, P);
-            if (ip <= ilimit) {
-                tab_put_pos(T, in, cur0 + 2, P);
-                tab_put_pos(T, in, ip - 2, P);
+        {   // table fills (zstd_fast.c:216-231) and the immediate repcode check: loads in one round trip
+            const uint64_t h1 = ld64(in, ip1), h2 = ld64(in, cur0 + 2), h3 = ld64(in, ip - 2);
+            const uint32_t c0 = in.w32(ip), c1 = in.w32(ip - (int)r2);
+            if (lane == 0) {
+                if (ip1 < ip) T.put(zhash(h1, P.hlog, P.mls), (uint32_t)ip1 + 1);
+                if (ip <= ilimit) {
+                    T.put(zhash(h2, P.hlog, P.mls), (uint32_t)cur0 + 3);
+                    T.put(zhash(h3, P.hlog, P.mls), (uint32_t)ip - 1);
+                }
             }
-        }
-        T.fence();
-        if (ip <= ilimit && r2 > 0) {
-            while (ip <= ilimit && in.w32(ip) == in.w32(ip - (int)r2)) {
+            T.fence();
+            bool more = ip <= ilimit && r2 > 0 && c0 == c1;
+            while (more) {
                 const int rl = 4 + count_fwd(in, ip + 4, ip + 4 - (int)r2, be - (ip + 4), lane);
                 const uint32_t t = r2; r2 = r1; r1 = t;
                 if (lane == 0) tab_put_pos(T, in, ip, P);
@@ -356,6 +379,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 O.put(lane, 0, 1, (uint32_t)rl);
                 ip += rl;
                 anchor = ip;
+                more = ip <= ilimit && r2 > 0 && in.w32(ip) == in.w32(ip - (int)r2);
             }
         }
     }
