@@ -44,7 +44,8 @@ extern "C" {
 /* LZH_CODEC_ZSTD: zstd 1.5.2 frames as lzbench's zstd rows write them, one frame per chunk
  * (ZSTD_getParams(level, chunk, 0) + content size, no dictionary, no checksum).  Compression:
  * the fast-strategy levels (zstd 1, 2 where fast, zstd_fast -1..-5), bit-exact with the reference;
- * other levels return LZH_EARG.  Decoding: any frame of that shape. */
+ * other levels return LZH_EARG.  Decoding: any frame of that shape, also with the XXH64 content
+ * checksum (verified); dictionary ids, a missing content size or windows over 2^27 report -2. */
 /* LZH_CODEC_LZ4F: one LZ4 frame per chunk as LZ4F_compressFrame writes it (lz4/lz4frame.c:429-470)
  * with independent blocks; level = LZH_LZ4F_PARAMS(blockSizeID 0|4..7, flags, acceleration).
  * Decoding: frames with independent blocks (or one block), every block but the last full, no
@@ -115,8 +116,8 @@ int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t 
                        void* d_packed, size_t packed_cap, uint32_t* d_csizes, uint64_t* d_offsets,
                        void* d_temp, size_t temp_bytes, void* hip_stream);
 /* d_offsets may be NULL (then derived from d_csizes into d_temp).  d_status: nchunks i32,
- * decoded size per chunk or negative on malformed input (zstd: -1 corrupt, -2 unsupported
- * frame feature).  A chunk whose compressed size equals its size is stored raw (all codecs).
+ * decoded size per chunk or negative on malformed input (zstd / LZ4 frame / nvcomp container:
+ * -1 corrupt, -2 unsupported frame feature).  A chunk whose compressed size equals its size is stored raw (all codecs).
  * Replaces (zstd): lzbench_zstd_decompress, compressors.cpp:1767-1773 (ZSTD_decompressDCtx). */
 int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable, const uint32_t* d_csizes,
                          const uint64_t* d_offsets, size_t n, size_t chunk_size, void* d_out, int32_t* d_status,

@@ -20,7 +20,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, codec, chunk, n, q):
+def _worker(rank, world, port, codec, chunk, n, q, hip=False):
     import torch.distributed as dist
     import lzbench_amd as L
     from lzbench_amd.shard import sharded_compress
@@ -28,7 +28,13 @@ def _worker(rank, world, port, codec, chunk, n, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     data = L.datagen("json", n, seed=77)
-    res = sharded_compress(data, chunk, rank, world, lambda shard: O.compress_chunks(shard, codec, chunk))
+    if hip:   # the HIP codec through the C-ABI on this rank's device (one GPU box: both ranks on cuda:0)
+        import torch
+        torch.cuda.set_device(rank % torch.cuda.device_count())
+        fn = lambda shard: L.compress_chunks(shard, codec, chunk)
+    else:
+        fn = lambda shard: O.compress_chunks(shard, codec, chunk)
+    res = sharded_compress(data, chunk, rank, world, fn)
     # max-over-ranks timing reduction of bench.py's control plane
     import torch
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
@@ -58,6 +64,33 @@ def test_two_rank_shard_gather_equals_single(codec, chunk):
     assert np.frombuffer(packed, np.uint8).tobytes() == ep.tobytes()
     assert cs == ec.tolist()
     assert tmax == 2.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec,chunk", [("lz4", 65536), ("snappy", 262144), ("lz4frame", 65536)])
+def test_two_rank_shard_gather_hip_codec(codec, chunk):
+    """The same protocol with the HIP codec on each rank (gloo control plane, host gather):
+    byte-identical to the single-process CPU chunk loop."""
+    import torch
+    import lzbench_amd as L
+    if torch.cuda.device_count() < 1:   # (device_count does not initialise the GPU in this parent)
+        pytest.skip("no HIP device")
+    n = 3 * chunk + 12345
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, codec, chunk, n, q, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    packed, cs, tmax = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    data = L.datagen("json", n, seed=77)
+    oc = {"lz4frame": "lz4f"}.get(codec, codec)
+    ep, ec = O.compress_chunks(data, oc, chunk, 0 if codec == "lz4frame" else 1)
+    assert np.frombuffer(packed, np.uint8).tobytes() == ep.tobytes()
+    assert cs == ec.tolist()
 
 
 def test_shard_ranges_cover_all_chunks():
