@@ -1520,12 +1520,17 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
                 rep1 = rep0;
                 rep0 = off = t;
             }
-            const int ml = (int)L.base[36 + mlc] + (int)sb.get(c_add(eM));
-            const int ll = (int)L.base[llc] + (int)sb.get(c_add(eL));
-            if (i + 1 < nseq) {                       // state updates: LL, ML, OF
-                sLL = c_next(eL) + sb.get(c_nb(eL));
-                sML = c_next(eM) + sb.get(c_nb(eM));
-                sOF = c_next(eO) + sb.get(c_nb(eO));
+            // match-length then literal-length extra bits (<= 16 each), one read of both
+            const int am = c_add(eM), al = c_add(eL);
+            const uint32_t xb = sb.get(am + al);
+            const int ml = (int)L.base[36 + mlc] + (int)(xb >> al);
+            const int ll = (int)L.base[llc] + (int)(xb & ((1u << al) - 1u));
+            if (i + 1 < nseq) {                       // state updates LL, ML, OF: one read (<= 27 bits)
+                const int nl = c_nb(eL), nm = c_nb(eM), no = c_nb(eO);
+                const uint32_t sbits = sb.get(nl + nm + no);
+                sLL = c_next(eL) + (sbits >> (nm + no));
+                sML = c_next(eM) + ((sbits >> no) & ((1u << nm) - 1u));
+                sOF = c_next(eO) + (sbits & ((1u << no) - 1u));
                 if (sb.left() < 0) return ZC;
             } else {
                 // the reference also updates the states after the last sequence and then accepts

@@ -1459,7 +1459,10 @@ hipError_t lzh_launch_zstd_compress(const uint8_t* in, uint64_t n_total, uint64_
     const size_t fstride = lzh_zstd_scratch_stride(chunk_size, level);
     const Layout Lo = layout_for(PF.bsize, 16);   // offsets below tab_off do not depend on hlog
     const uint32_t nblocks = (uint32_t)((std::min<uint64_t>(chunk_size, std::max<uint64_t>(n_total, 1)) + PF.bsize - 1) / PF.bsize);
-    const uint32_t lds_tab = (4u << PF.hlog) <= 65536u ? (4u << PF.hlog) : 0u;
+#ifndef LZH_ZSTD_LDS_MAX
+#define LZH_ZSTD_LDS_MAX 65536u   // largest hash table kept in LDS (else in the frame's scratch, via L2)
+#endif
+    const uint32_t lds_tab = (4u << PF.hlog) <= (uint32_t)LZH_ZSTD_LDS_MAX ? (4u << PF.hlog) : 0u;
     for (uint32_t k = 0; k < std::max(nblocks, 1u); k++) {
         hipLaunchKernelGGL(lzh_zstd_match_kernel, dim3(nchunks), dim3(64), lds_tab, s, in, n_total, in_readable,
                            chunk_size, level, (int)k, scratch, (uint64_t)fstride, Lo.seq_off, Lo.lit_off, Lo.tab_off,
