@@ -126,6 +126,21 @@ struct LdsTab {
     __device__ __forceinline__ void put(uint32_t h, uint32_t v) const { ((volatile LDSA uint32_t*)t)[h] = v; }
     __device__ __forceinline__ void fence() const { wave_lds_fence(); }
 };
+// the same table as 16-bit low halves + 8-bit high bytes (3 bytes an entry: 6 waves per CU instead of
+// 5 at hashLog 13), for frames below 16 MiB.  A claim writes both halves with the same lanes to the
+// same slots, so the hardware's choice among colliding lanes is the same for both stores.
+struct LdsTab24 {
+    LDSA uint16_t* lo;
+    LDSA uint8_t* hi;
+    __device__ __forceinline__ uint32_t get(uint32_t h) const {
+        return (uint32_t)((volatile LDSA uint16_t*)lo)[h] | ((uint32_t)((volatile LDSA uint8_t*)hi)[h] << 16);
+    }
+    __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
+        ((volatile LDSA uint16_t*)lo)[h] = (uint16_t)v;
+        ((volatile LDSA uint8_t*)hi)[h] = (uint8_t)(v >> 16);
+    }
+    __device__ __forceinline__ void fence() const { wave_lds_fence(); }
+};
 struct GlbTab {
     rsrc_t r;
     __device__ __forceinline__ uint32_t get(uint32_t h) const {
@@ -426,7 +441,16 @@ lzh_zstd_match_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable,
     uint32_t rep[2] = {1u, 4u};                          // repStartValue
     if (k > 0) { rep[0] = uni(ld_b32(hdr, 16)); rep[1] = uni(ld_b32(hdr, 20)); }
     const uint32_t tbytes = 4u << P.hlog;
-    if (tbytes <= lds_table_bytes) {
+    const uint32_t nent = 1u << P.hlog;
+    if (chunk_size < (16u << 20) && 3u * nent <= lds_table_bytes) {
+        LdsTab24 T{(LDSA uint16_t*)zlds, (LDSA uint8_t*)zlds + 2 * nent};
+        rsrc_t save = make_rsrc(fs + tab_off, tbytes);
+        for (uint32_t i = lane; i < nent; i += 64) T.put(i, k == 0 ? 0u : ld_b32(save, (int)(i * 4)));
+        T.fence();
+        fast_block(T, in_b, P, bs, be, rep, O, lane);
+        if ((uint64_t)k + 1 < nblocks)
+            for (uint32_t i = lane; i < nent; i += 64) st_b32(save, (int)(i * 4), T.get(i));
+    } else if (tbytes <= lds_table_bytes) {
         LdsTab T{(LDSA uint32_t*)zlds};
         rsrc_t save = make_rsrc(fs + tab_off, tbytes);
         for (uint32_t i = lane; i < tbytes / 4; i += 64) T.put(i, k == 0 ? 0u : ld_b32(save, (int)(i * 4)));
@@ -1462,7 +1486,9 @@ hipError_t lzh_launch_zstd_compress(const uint8_t* in, uint64_t n_total, uint64_
 #ifndef LZH_ZSTD_LDS_MAX
 #define LZH_ZSTD_LDS_MAX 65536u   // largest hash table kept in LDS (else in the frame's scratch, via L2)
 #endif
-    const uint32_t lds_tab = (4u << PF.hlog) <= (uint32_t)LZH_ZSTD_LDS_MAX ? (4u << PF.hlog) : 0u;
+    // 3-byte entries (LdsTab24) below 16 MiB chunks, else 4-byte ones
+    const uint32_t ebytes = chunk_size < (16u << 20) ? 3u : 4u;
+    const uint32_t lds_tab = (4u << PF.hlog) <= (uint32_t)LZH_ZSTD_LDS_MAX ? (ebytes << PF.hlog) : 0u;
     for (uint32_t k = 0; k < std::max(nblocks, 1u); k++) {
         hipLaunchKernelGGL(lzh_zstd_match_kernel, dim3(nchunks), dim3(64), lds_tab, s, in, n_total, in_readable,
                            chunk_size, level, (int)k, scratch, (uint64_t)fstride, Lo.seq_off, Lo.lit_off, Lo.tab_off,
