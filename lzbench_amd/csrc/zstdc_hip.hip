@@ -533,6 +533,15 @@ __device__ __forceinline__ uint32_t ml_code(uint32_t mb) {
     }
     return hb32(mb) + 36;
 }
+// extra bits of a literal-length / match-length code (kLLB / kMLB below) from the length itself: the
+// single-lane sequence encoder runs under lane 0, where a table lookup would be a vector load from
+// constant memory (a memory round trip per lookup) instead of a scalar one
+__device__ __forceinline__ uint32_t ll_bits(uint32_t ll) {
+    return ll < 16 ? 0u : ll < 24 ? 1u : ll < 32 ? 2u : ll < 48 ? 3u : ll < 64 ? 4u : (uint32_t)hb32(ll);
+}
+__device__ __forceinline__ uint32_t ml_bits(uint32_t mb) {
+    return mb < 32 ? 0u : mb < 40 ? 1u : mb < 48 ? 2u : mb < 64 ? 3u : mb < 96 ? 4u : mb < 128 ? 5u : (uint32_t)hb32(mb);
+}
 __device__ __constant__ uint8_t kLLB[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3,
                                             4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
 __device__ __constant__ uint8_t kMLB[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
@@ -1298,8 +1307,8 @@ __device__ int encode_sequences(LDSA Lds& L, const Bytes& att, int pos, rsrc_t s
                     fse_encode(b, L.fse[2], sML, mlc);
                     fse_encode(b, L.fse[0], sLL, llc);
                 }
-                b.add(ll, kLLB[llc]);
-                b.add(ml - 3, kMLB[mlc]);
+                b.add(ll, ll_bits(ll));
+                b.add(ml - 3, ml_bits(ml - 3));
                 b.add(off, ofc);
             }
         }
