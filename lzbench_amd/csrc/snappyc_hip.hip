@@ -914,8 +914,11 @@ lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readabl
 
 namespace sne {
 
-constexpr int kRingB = 2048;            // LDS output ring (bytes)
-constexpr int kSpan = 2048;             // LDS copy of a record group's input span (bytes)
+#ifndef LZH_SNE_RING
+#define LZH_SNE_RING 2048
+#endif
+constexpr int kRingB = LZH_SNE_RING;    // LDS output ring (bytes)
+constexpr int kSpan = LZH_SNE_RING;     // LDS copy of a record group's input span (bytes)
 
 __device__ __forceinline__ int wave_max(int v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
@@ -974,6 +977,10 @@ struct OutR {
 };
 
 constexpr int kBulk = 256;   // literal runs at least this long go straight to HBM (bulk_literals)
+// longest literal run the lane-parallel group layout takes (<= 256: a tag and one length byte)
+#ifndef LZH_SNE_LITMAX
+#define LZH_SNE_LITMAX 64
+#endif
 
 }  // namespace sne
 
@@ -1026,7 +1033,7 @@ __device__ __forceinline__ int emit_records(OutR& R, const Bytes& in_b, rsrc_t r
         int T;
         const int pos = op + sne::wave_excl_scan(S, T);
         const int litmax = (int)uni((uint32_t)sne::wave_max(lit));
-        if (T <= sne::kRingB / 2 && litmax <= 64 && Lt + 8 <= sne::kSpan) {
+        if (T <= sne::kRingB / 2 && litmax <= LZH_SNE_LITMAX && Lt + 8 <= sne::kSpan) {
             // the group's input span [ia, ia + Lt) into LDS (literal bytes are read from there)
             const int X0 = (ia + in_b.sh) & ~3;
             const int nd = (ia + in_b.sh + Lt - X0 + 3) >> 2;
