@@ -885,31 +885,36 @@ lzh_snappy_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 // 8-byte records; lzh_snappy_emit_kernel (no hash table: high occupancy) writes the varint header
 // (snappy.cc:1047-1050) and lays out EmitLiteral / EmitCopy (:342-443) for 64 records at a time.
 
+// Records of fragment f of a chunk with more than one fragment start at record f * kFragRecs of the
+// chunk's record slot (a 64 KiB fragment has at most 16 384 copies of >= 4 bytes and one closing
+// literal-only record), so every fragment is parsed by a wave of its own: snappy starts each
+// fragment with a fresh table (snappy.cc:1042-1072), and 64 KiB units balance the CUs better than
+// whole chunks at -b256 and above.
+constexpr int kFragRecs = 16384 + 32;
+
 extern "C" __global__ void __launch_bounds__(64)
 lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                         uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint32_t frags) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + (LZH_SN_PARSE_NORING ? 0 : 256 + 8)];   // table | ring + mirror
-    const uint64_t chunk = blockIdx.x;
+    const uint64_t chunk = blockIdx.x / frags;
+    const uint32_t f = blockIdx.x - (uint32_t)chunk * frags;
     const uint64_t off = chunk * chunk_size;
     if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
     const uint32_t n = (uint32_t)min(chunk_size, n_total - off);
     const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
-    Bytes rout;
-    rout.init(nullptr, 0);
-    int nrec = 0;
-    uint32_t* hdr = rec_hdr + chunk * frags;       // cumulative record count after each fragment
-    uint32_t f = 0;
-    for (uint32_t fpos = 0; fpos < n; fpos += 65536u, f++) {
+    uint32_t* hdr = rec_hdr + chunk * frags;       // end record (exclusive) of each fragment
+    int nrec = frags > 1 ? (int)f * kFragRecs : 0;
+    const uint32_t fpos = f << 16;
+    if (fpos < n) {
         const int fn = (int)min(65536u, n - fpos);
         const uint64_t readable = min<uint64_t>(in_readable - off - fpos, (uint64_t)fn + 64);
-        Bytes rin;
+        Bytes rin, rout;
         rin.init(in + off + fpos, readable);
+        rout.init(nullptr, 0);
         snv2::compress_fragment<true>(rin, fn, rout, 0, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13), nullptr,
                                       nullptr, rr, nrec, (int)fpos);
-        if (threadIdx.x == 0) hdr[f] = (uint32_t)nrec;
     }
-    for (; f < frags; f++)
-        if (threadIdx.x == 0) hdr[f] = (uint32_t)nrec;
+    if (threadIdx.x == 0) hdr[f] = (uint32_t)nrec;
 }
 
 namespace sne {
@@ -979,7 +984,7 @@ struct OutR {
 constexpr int kBulk = 256;   // literal runs at least this long go straight to HBM (bulk_literals)
 // longest literal run the lane-parallel group layout takes (<= 256: a tag and one length byte)
 #ifndef LZH_SNE_LITMAX
-#define LZH_SNE_LITMAX 64
+#define LZH_SNE_LITMAX 256
 #endif
 
 }  // namespace sne
@@ -1144,7 +1149,7 @@ __device__ __forceinline__ void emit_chunk(LDSA uint8_t* rings, LDSA uint32_t* i
     } else {
     // sizes of all fragments but the last (the last one's end is the chunk's compressed size)
     for (int f = wave; f < nf - 1; f += W) {
-        const int r0 = f == 0 ? 0 : (int)uni(hdr[f - 1]), r1 = (int)uni(hdr[f]);
+        const int r0 = f * kFragRecs, r1 = (int)uni(hdr[f]);
         const int bytes = frag_bytes(rr, r0, r1, f << 16, lane);
         if (lane == 0) fsz[f] = (uint32_t)bytes;
     }
@@ -1158,7 +1163,7 @@ __device__ __forceinline__ void emit_chunk(LDSA uint8_t* rings, LDSA uint32_t* i
     int base = nb;
     for (int f = 0; f < nf; f++) {
         if ((f % W) == wave) {
-            const int r0 = f == 0 ? 0 : (int)uni(hdr[f - 1]), r1 = (int)uni(hdr[f]);
+            const int r0 = f * kFragRecs, r1 = (int)uni(hdr[f]);
             OutR<kMulti> R{ring, so, f == 0 ? 0 : base};
             if (f == 0 && lane < nb) R.put(lane, vb);
             const int e = emit_records(R, in_b, rr, r0, r1, f << 16, base, ibuf, lane);
@@ -1200,7 +1205,9 @@ lzh_snappy_emit_frag_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_rea
 #include "launch.h"
 uint32_t lzh_snappy_frags(uint64_t chunk_size) { return (uint32_t)((chunk_size + 65535) >> 16); }
 size_t lzh_snappy_rec_stride(uint64_t chunk_size) {
-    return ((chunk_size / 4 + chunk_size / 65536 + 8) * 8 + 255) / 256 * 256;
+    const uint32_t frags = lzh_snappy_frags(chunk_size);
+    if (frags > 1) return (size_t)frags * kFragRecs * 8;   // (kFragRecs * 8 is a multiple of 256)
+    return ((chunk_size / 4 + 8) * 8 + 255) / 256 * 256;
 }
 
 // parse kernel + emit kernel (records: nchunks x rec_stride bytes, then a u32 count per chunk);
@@ -1213,7 +1220,7 @@ hipError_t lzh_launch_snappy_split(const uint8_t* in, uint64_t n_total, uint64_t
     uint32_t* hdr = (uint32_t*)(recs + rs * nchunks);
     const uint32_t frags = lzh_snappy_frags(chunk_size);
     if (stage_mask & 1)
-        hipLaunchKernelGGL(lzh_snappy_parse_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable,
+        hipLaunchKernelGGL(lzh_snappy_parse_kernel, dim3(nchunks * frags), dim3(64), 0, s, in, n_total, in_readable,
                            chunk_size, recs, rs, hdr, frags);
     if (stage_mask & 2) {
         if (frags > (uint32_t)sne::kMaxFrags) return hipErrorInvalidValue;
