@@ -124,6 +124,9 @@ namespace owin {
 #ifndef LZH_DEC_KW
 #define LZH_DEC_KW 4096
 #endif
+#ifndef LZH_DEC_WIDE
+#define LZH_DEC_WIDE 2   // wider output windows for launches with few chunks: 0 off, 1 up to 8 KiB, 2 up to 16 KiB
+#endif
 constexpr int kW = LZH_DEC_KW;   // LDS output window bytes (power of two)
 
 template <int KW>
@@ -223,7 +226,8 @@ namespace checked {
 
 using owin::kW;
 
-__device__ __forceinline__ int lz4_one(const Bytes& in, int cs, owin::Sink& O, Win& w, int cap, int& ip, int& op,
+template <class SinkType>
+__device__ __forceinline__ int lz4_one(const Bytes& in, int cs, SinkType& O, Win& w, int cap, int& ip, int& op,
                                        int lane) {
     if (ip >= cs) return -ip - 1;
     w.ensure(ip, lane);
@@ -546,7 +550,8 @@ __device__ __forceinline__ uint64_t chain_members(int link, int lane) {
     return ballot(x == lane && link != 255);
 }
 
-__device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* mark, LDSA uint8_t* ring, int cap,
+template <class SinkType>
+__device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* mark, LDSA uint8_t* ring, int cap,
                           int lane) {
     if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
     if (cs <= 0) return -1;
@@ -623,7 +628,8 @@ __device__ int lz4_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* 
 // of snappy_decode below (snappy.cc:848-952) are checked per member against the prefix sum, and
 // the group is cut before the first failure (which, like 2..4-byte literal lengths, runs through
 // the checked per-tag path).
-__device__ int snappy_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_t* mark, LDSA uint8_t* ring, int cap,
+template <class SinkType>
+__device__ int snappy_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* mark, LDSA uint8_t* ring, int cap,
                              int lane) {
     Win w;
     w.bind(in, ring);
@@ -737,12 +743,15 @@ __device__ int snappy_decode(const Bytes& in, int cs, owin::Sink& O, LDSA uint8_
 
 }  // namespace groups
 
-extern "C" __global__ void __launch_bounds__(64)
-lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
-                         const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
-                         int32_t* status, uint32_t chunk0, const uint32_t* desc) {
-    // output window | start marks | input ring
-    __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + 3 * LZH_WAVE + kRingBytes];
+// One chunk (or framed block) per wave; KW = bytes of the LDS output window.  The window sets the
+// share of match sources read from the LDS instead of the flushed output in global memory, and the
+// LDS per wave (hence waves per CU): lzh_launch_decompress picks the largest window whose occupancy
+// still holds every chunk of the launch at once.
+template <int KW>
+__device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, const uint8_t* packed,
+                                                 uint64_t packed_readable, const uint64_t* offsets,
+                                                 const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size,
+                                                 uint8_t* out, int32_t* status, uint32_t chunk0, const uint32_t* desc) {
     const int lane = threadIdx.x;
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     uint64_t ooff, ioff;
@@ -777,8 +786,8 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
         copy_raw(rin, rout, part, lane);
         r = part;
     } else {
-        owin::Sink O{(LDSA uint8_t*)win, rout, 0, 0};
-        LDSA uint8_t* mark = (LDSA uint8_t*)win + owin::kW;
+        owin::SinkT<KW> O{win, rout, 0, 0};
+        LDSA uint8_t* mark = win + KW;
         LDSA uint8_t* ring = mark + 3 * LZH_WAVE;
         r = codec == 0 ? groups::lz4_decode(rin, cs, O, mark, ring, part, lane)
                        : groups::snappy_decode(rin, cs, O, mark, ring, part, lane);
@@ -791,6 +800,21 @@ lzh_decompress_v2_kernel(int codec, const uint8_t* packed, uint64_t packed_reada
     if (lane < 16) atomicAdd(&lzh_dec_stats_buf[lane], g_dst[lane]);
 #endif
 }
+
+// output window | start marks | input ring
+#define LZH_DEC_KERNEL(NAME, KW)                                                                            \
+    extern "C" __global__ void __launch_bounds__(64)                                                       \
+    NAME(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,              \
+         const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out, int32_t* status,     \
+         uint32_t chunk0, const uint32_t* desc) {                                                          \
+        __shared__ __attribute__((aligned(16))) uint8_t win[KW + 3 * LZH_WAVE + kRingBytes];              \
+        decompress_chunk<KW>((LDSA uint8_t*)win, codec, packed, packed_readable, offsets, csizes, n_total,  \
+                             chunk_size, out, status, chunk0, desc);                                       \
+    }
+LZH_DEC_KERNEL(lzh_decompress_v2_kernel, owin::kW)
+LZH_DEC_KERNEL(lzh_decompress_w8k_kernel, 8192)
+LZH_DEC_KERNEL(lzh_decompress_w16k_kernel, 16384)
+#undef LZH_DEC_KERNEL
 
 #if LZH_DEC_STATS
 extern "C" int lzh_debug_dec_stats(unsigned long long* host, int reset) {
@@ -1734,8 +1758,24 @@ hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t pack
                                  const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                  int32_t* status, uint32_t nchunks, hipStream_t s, const void* desc) {
     if (nchunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(lzh_decompress_v2_kernel, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable,
-                       offsets, csizes, n_total, chunk_size, out, status, 0u, (const uint32_t*)desc);
+    // waves per CU by LDS (160 KiB; allocation in 512-byte granules; at most 32 waves), per window
+    static int cus[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 0;
+    auto fits = [&](int kw) {
+        const int lds = (kw + 3 * LZH_WAVE + kRingBytes + 511) / 512 * 512;
+        return (uint64_t)nchunks <= (uint64_t)cus[dev] * (uint64_t)min(32, 160 * 1024 / lds);
+    };
+    auto k = lzh_decompress_v2_kernel;
+    if (LZH_DEC_WIDE && cus[dev] > 0) {
+        if (LZH_DEC_WIDE >= 2 && fits(16384)) k = lzh_decompress_w16k_kernel;
+        else if (fits(8192)) k = lzh_decompress_w8k_kernel;
+    }
+    hipLaunchKernelGGL(k, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable, offsets, csizes, n_total,
+                       chunk_size, out, status, 0u, (const uint32_t*)desc);
     return hipGetLastError();
 }
 
