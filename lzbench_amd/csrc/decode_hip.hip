@@ -1802,6 +1802,15 @@ lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, cons
 }
 
 #include "launch.h"
+// Test hook: force the LZ4 / snappy decoder's output window (4096, 8192 or 16384; 0 = by chunk count)
+// so that the parity tests run every window kernel on the same streams.
+static int g_force_window = 0;
+extern "C" int lzh_debug_force_decode_window(int kw) {
+    if (kw != 0 && kw != 4096 && kw != 8192 && kw != 16384) return -1;
+    g_force_window = kw;
+    return 0;
+}
+
 hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                  const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                  int32_t* status, uint32_t nchunks, hipStream_t s, const void* desc) {
@@ -1818,7 +1827,10 @@ hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t pack
         return (uint64_t)nchunks <= (uint64_t)cus[dev] * (uint64_t)min(32, 160 * 1024 / lds);
     };
     auto k = lzh_decompress_v2_kernel;
-    if (LZH_DEC_WIDE && cus[dev] > 0) {
+    if (g_force_window) {
+        if (g_force_window == 8192) k = lzh_decompress_w8k_kernel;
+        else if (g_force_window == 16384) k = lzh_decompress_w16k_kernel;
+    } else if (LZH_DEC_WIDE && cus[dev] > 0) {
         if (LZH_DEC_WIDE >= 2 && fits(16384)) k = lzh_decompress_w16k_kernel;
         else if (fits(8192)) k = lzh_decompress_w8k_kernel;
     }
