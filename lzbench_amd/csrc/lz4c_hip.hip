@@ -1165,6 +1165,10 @@ namespace lz4e {
 constexpr int kRingB = 2048;            // LDS output ring (bytes)
 constexpr int kSpan = 2048;             // LDS copy of a record group's input span (bytes)
 // (4 KiB of LDS per wave: the emission kernel runs at the full 8 waves per SIMD)
+// longest literal run the lane-parallel group layout takes (<= 269: one literal-length byte)
+#ifndef LZH_LZ4E_LITMAX
+#define LZH_LZ4E_LITMAX 64
+#endif
 
 __device__ __forceinline__ int wave_max(int v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
@@ -1299,11 +1303,11 @@ lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, u
         const int pos = op + lz4e::wave_excl_scan(S, lane, T);
         const int litv = v ? lit : 0;
         const int litmax = (int)uni((uint32_t)lz4e::wave_max(litv));
-        if (T <= lz4e::kRingB / 2 && litmax <= 64 && span) {
+        if (T <= lz4e::kRingB / 2 && litmax <= LZH_LZ4E_LITMAX && span) {
             const LDSA uint8_t* ib = (const LDSA uint8_t*)ibuf;
             const int ioff = ia + in_b.sh - X0 - ia;   // input position p lives at ib[p + ioff]
             // every lane writes its own sequence (lz4.c:1022-1135): token, one literal-length byte
-            // when lit >= 15 (lit <= 64 here), the literals (a lane-parallel copy as long as the
+            // when lit >= 15 (lit <= LZH_LZ4E_LITMAX <= 269 here), the literals (a lane-parallel copy as long as the
             // group's longest run), offset, match-length bytes
             if (op + T - R.flushed > lz4e::kRingB - 8) R.flush(op, false, lane);
             const int lx = lz4e::ext_len(lit), mx = lz4e::ext_len(mlx);
