@@ -8,11 +8,14 @@ HBM when the timed region starts.  value = comp+decomp MB/s (MB = 1e6 B, lzbench
 = bytes processed by all ranks / (max over ranks of the timed wall time).
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, each owns a contiguous 1 GiB shard of the chunk list (weak scaling).  The only exchange is
-the host-side gather of SURVEY.md 8(e): after the timed region the ranks all-gather their packed
-totals (a few bytes, control plane), and each copies its packed slab straight into one shared
-host buffer at its chunk-order offset; that gather is timed and reported (`gather`).  No
-collective touches the data path.
+GPU, each owns a contiguous 1 GiB shard of the chunk list (weak scaling; every shard is the same
+seed-12345 input, so every rank's output is checked against the one reference digest).  The only
+exchange is the host-side gather of SURVEY.md 8(e): after the timed region the ranks all-gather
+their packed totals (a few bytes, control plane), and each copies its packed slab straight into
+one shared host buffer at its chunk-order offset (lzbench_amd/shard.py gather_slabs); that gather
+is timed and reported (`gather`).  No collective touches the data path.  Rank 0 then also times
+the in-process N-device product path (`e2e`: lzbench_hip_compress_batch / _decompress_batch with
+ngpus = N over the N shards' bytes, what `lzbench_hip -gN` runs).
 
 Also reported (rank 0):
   roofline / roofline_decompress  the codec kernels, HIP events on the stream they run on
@@ -22,8 +25,11 @@ Also reported (rank 0):
                                   sources) on this host, 1 thread, lzbench semantics (N=1 only)
   cpu_baseline_all_cores          the same on every host core this process may use
   e2e                             host-to-host through the batched lzbench rows
-                                  (lzbench_hip_compress_batch / _decompress_batch) on the same
-                                  input, beside the hipMemcpy round-trip bound (PCIe; never value)
+                                  (lzbench_hip_compress_batch / _decompress_batch, ngpus = N) on
+                                  the same input (N copies at N > 1), beside the hipMemcpy
+                                  round-trip bound (PCIe; never value)
+  roofline_compress_stage         the whole compress stage (parse + emit + scan + pack) against
+                                  the same N + C algorithmic bytes
 """
 from __future__ import annotations
 
@@ -158,10 +164,13 @@ def sha(*arrays):
     return h.hexdigest()
 
 
-def e2e_rows(L, host, codec, chunk, level, ngpus, iters):
-    """Host-to-host through the batched lzbench rows (what lzbench_hip -b runs): best of `iters`
-    compress_batch and decompress_batch passes, and the hipMemcpy round trip (H2D + D2H of the
-    same bytes, pinned) as the PCIe bound beside them."""
+def e2e_rows(L, host, codec, chunk, level, ngpus, iters, dig=None):
+    """Host-to-host through the batched lzbench rows (what lzbench_hip -b -g<ngpus> runs): best of
+    `iters` compress_batch and decompress_batch passes over `host` (its chunk list sharded over
+    ngpus devices, api.cpp make_plan), and the hipMemcpy round trip (H2D + D2H of the same bytes,
+    pinned, one device) as the PCIe bound beside them.  dig: the reference digest of one copy of
+    the per-GPU input (host = ngpus copies of it): every copy's slab of the packed output and of
+    compr_sizes must hash to it."""
     import torch
     n = len(host)
     cs = L.chunk_sizes_for(n, chunk)
@@ -184,9 +193,19 @@ def e2e_rows(L, host, codec, chunk, level, ngpus, iters):
                                                  back.ctypes.data, len(back), lvl, ngpus, row.wm)
             best_d = min(best_d, time.perf_counter() - t)
     ok = tot > 0 and r == n and bool((back[:n] == host).all())
-    pin = torch.from_numpy(host).pin_memory()
-    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
-    hb = torch.empty(n, dtype=torch.uint8).pin_memory()
+    exact = None
+    if dig is not None and tot > 0:
+        reps, per = n // dig["size"], len(cs) // (n // dig["size"])
+        c64 = comp.astype("<u8")
+        offs = np.concatenate([[0], np.cumsum(comp.astype(np.int64))])
+        exact = reps * dig["size"] == n and all(
+            sha(c64[i * per:(i + 1) * per]) == dig["csizes_sha256"] and
+            sha(out[offs[i * per]:offs[(i + 1) * per]]) == dig["packed_sha256"] for i in range(reps))
+    del back
+    pin = torch.from_numpy(host[:min(n, 1 << 30)]).pin_memory()
+    n1 = len(pin)
+    dev = torch.empty(n1, dtype=torch.uint8, device="cuda")
+    hb = torch.empty(n1, dtype=torch.uint8).pin_memory()
     best_m = float("inf")
     for _ in range(iters):
         torch.cuda.synchronize()
@@ -200,53 +219,15 @@ def e2e_rows(L, host, codec, chunk, level, ngpus, iters):
         "comp_MBps": round(n / best_c / 1e6, 2),
         "decomp_MBps": round(n / best_d / 1e6, 2),
         "comp+decomp_MBps": round(n / (best_c + best_d) / 1e6, 2),
-        "hipMemcpy_roundtrip_MBps": round(n / best_m / 1e6, 2),
+        "hipMemcpy_roundtrip_MBps": round(n1 / best_m / 1e6, 2),
+        "hipMemcpy_roundtrip_note": "one device, pinned, %d bytes" % n1,
         "ngpus": ngpus,
         "roundtrip_ok": ok,
+        "bit_exact": exact,
         "bytes": n,
         "note": "host pageable buffers (page-locked once per row), H2D + kernels + D2H pipelined over "
                 "128 MiB sub-batches; best of %d passes; PCIe-bound, reported beside value, never as value" % iters,
     }
-
-
-def gather_to_host(torch, dist, codec_obj, rank, world):
-    """SURVEY 8(e)'s single host-side gather: the ranks exchange packed totals (control plane),
-    then each copies its packed slab into one shared host buffer (/dev/shm) at its chunk-order
-    offset.  Returns {ms, bytes, GBps} (max over ranks)."""
-    import mmap
-    total = codec_obj.packed_total()
-    tt = torch.tensor([total], dtype=torch.int64)
-    alltot = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(alltot, tt)
-    sizes = [int(x.item()) for x in alltot]
-    base = sum(sizes[:rank])
-    grand = sum(sizes)
-    path = f"/dev/shm/lzh_bench_gather_{os.environ.get('MASTER_PORT', '0')}"
-    if rank == 0:
-        with open(path, "wb") as f:
-            f.truncate(grand)
-    dist.barrier()
-    fd = os.open(path, os.O_RDWR)
-    mm = mmap.mmap(fd, grand)
-    host = torch.frombuffer(mm, dtype=torch.uint8)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t = time.perf_counter()
-    host[base:base + total].copy_(codec_obj.packed[:total])
-    torch.cuda.synchronize()
-    dist.barrier()
-    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    del host
-    mm.close()
-    os.close(fd)
-    dist.barrier()
-    if rank == 0:
-        os.unlink(path)
-    ms = float(el.item()) * 1e3
-    return {"ms": round(ms, 3), "bytes": grand, "GBps": round(grand / (ms * 1e-3) / 1e9, 2),
-            "how": "all_gather of packed totals, then each rank D2H-copies its slab into one shared host buffer "
-                   "at its chunk-order offset (pageable mmap); timed after the timed region, max over ranks"}
 
 
 def main():
@@ -280,7 +261,7 @@ def main():
 
     n = args.size_mib << 20
     chunk = args.chunk_kib << 10
-    seed = 12345 + rank
+    seed = 12345                       # every rank's shard is the digest-pinned input (see docstring)
     t = time.perf_counter()
     host = L.datagen(args.corpus, n, seed=seed)
     log(f"[rank {rank}] generated {n >> 20} MiB {args.corpus} in {time.perf_counter() - t:.1f}s")
@@ -329,25 +310,40 @@ def main():
     f_ms = float(np.mean([e[4].elapsed_time(e[2]) for e in timed]))
     d_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in timed]))
     comp_total = codec.packed_total()
+    k_chunks = int(codec.k)
     roundtrip_ok = bool(torch.equal(codec.out[:n], d_in[:n])) and bool((codec.status >= 0).all().item())
     ratio = comp_total / n
 
     result_extra = {}
     if dist:
-        result_extra["gather"] = gather_to_host(torch, dist, codec, rank, world)
+        from lzbench_amd.shard import gather_slabs
+        g, _ = gather_slabs(codec.packed[:comp_total], codec.csizes[:codec.k], rank, world, keep=False)
+        g["how"] = ("all_gather of packed totals, then each rank copies its HBM slab (and its compr_sizes) into one "
+                    "shared host buffer at its chunk-order offset (lzbench_amd/shard.py gather_slabs); timed after "
+                    "the timed region, max over ranks")
+        result_extra["gather"] = g
 
-    # bit-exactness of the WHOLE output vs the reference chunk loop's digest
+    # bit-exactness of the WHOLE output vs the reference chunk loop's digest, on every rank
     dig = fullsize_digest(args.corpus, args.codec, chunk, args.level, n, seed)
-    if rank == 0:
-        if dig is not None:
-            cs64 = codec.csizes.cpu().numpy().astype("<u8")
-            result_extra["bit_exact"] = bool(comp_total == dig["packed_bytes"] and sha(cs64) == dig["csizes_sha256"]
-                                             and sha(codec.packed[:comp_total].cpu().numpy()) == dig["packed_sha256"])
-            result_extra["bit_exact_bytes"] = n
-            result_extra["bit_exact_against"] = "tests/golden/fullsize.json (reference chunk loop, oracle/_ref)"
-        else:
-            result_extra["bit_exact"] = None
-            result_extra["bit_exact_against"] = "no committed reference digest for this workload"
+    exact = None
+    if dig is not None:
+        cs64 = codec.csizes.cpu().numpy().astype("<u8")
+        exact = bool(comp_total == dig["packed_bytes"] and sha(cs64) == dig["csizes_sha256"]
+                     and sha(codec.packed[:comp_total].cpu().numpy()) == dig["packed_sha256"])
+    ranks_exact = [exact]
+    if dist:
+        flag = torch.tensor([-1 if exact is None else int(exact)], dtype=torch.int64)
+        flags = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(flags, flag)
+        ranks_exact = [None if int(f.item()) < 0 else bool(f.item()) for f in flags]
+    if dig is not None:
+        result_extra["bit_exact"] = all(ranks_exact)
+        result_extra["bit_exact_ranks"] = ranks_exact
+        result_extra["bit_exact_bytes"] = n * world
+        result_extra["bit_exact_against"] = "tests/golden/fullsize.json (reference chunk loop, oracle/_ref)"
+    else:
+        result_extra["bit_exact"] = None
+        result_extra["bit_exact_against"] = "no committed reference digest for this workload"
 
     cpu = None
     usable, cpuinfo = host_cpus()
@@ -356,10 +352,18 @@ def main():
         result_extra["cpu_baseline_all_cores"] = cpu_baseline(host, args.codec, chunk, args.level, args.cpu_iters,
                                                               usable)
     result_extra["host_cpu"] = cpuinfo
-    if rank == 0 and world == 1 and not args.no_e2e:
-        del d_in
+    if not args.no_e2e:
+        # the in-process product path over all N devices, by rank 0 while the other ranks wait
+        del d_in, codec
         torch.cuda.empty_cache()
-        result_extra["e2e"] = e2e_rows(L, host, args.codec, chunk, args.level, 1, 3)
+        if dist:
+            dist.barrier()
+        if rank == 0:
+            big = host if world == 1 else np.tile(host, world)
+            result_extra["e2e"] = e2e_rows(L, big, args.codec, chunk, args.level, world, 3, dig)
+            del big
+        if dist:
+            dist.barrier()
 
     algo_bytes = n + comp_total                      # compress reads N, writes C
     achieved = algo_bytes / (k_ms * 1e-3) / 1e9
@@ -382,14 +386,14 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": f"synthetic {args.corpus} corpus (SURVEY.md 8(d) stand-in; enwik8/Silesia unavailable offline), "
-                f"generated per rank (seed 12345 + rank), resident in HBM",
+                f"the same seed-12345 shard on every rank, resident in HBM",
         "config": {
             "workload": f"{args.codec}{',' + str(args.level) if args.codec in ('lz4fast', 'zstd') else ''} "
                         f"-b{args.chunk_kib} on {size_label(n)} {args.corpus} per GPU, comp+decomp pass",
             "codec": args.codec,
             "chunk_kib": args.chunk_kib,
             "bytes_per_gpu": n,
-            "chunks_per_gpu": int(codec.k),
+            "chunks_per_gpu": k_chunks,
             "parallelism": f"chunk-sharded x{world} (contiguous shard per GPU, host-side gather, no collective)",
         },
         "roofline": {
@@ -403,6 +407,15 @@ def main():
             "kernel": kname,
             "kernel_ms": round(k_ms, 3),
             "algorithmic_bytes_per_launch": int(algo_bytes),
+        },
+        "roofline_compress_stage": {
+            "bound": "hbm",
+            "achieved": round(algo_bytes / ((k_ms + x_ms + f_ms) * 1e-3) / 1e9, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(algo_bytes / ((k_ms + x_ms + f_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "kernels": f"{kname} + emit + lzh_scan_kernel + lzh_pack_kernel",
+            "stage_ms": round(k_ms + x_ms + f_ms, 3),
         },
         "roofline_decompress": {
             "bound": "hbm",

@@ -24,7 +24,12 @@
  *     lzbench_compress / lzbench_decompress (lzbench.cpp:266-298 / :301-329) including the
  *     raw-store rule (clen <= 0 || clen == part -> stored raw, compr_size = part) and the
  *     contiguous packing in chunk order.  Chunks are sharded over the GPUs given to init
- *     (param2 = ngpus) by contiguous index ranges with one host-side gather.
+ *     (param2 = ngpus): the chunk list is cut into ~128 MiB sub-batches of consecutive chunks,
+ *     dealt round-robin to the devices (each pipelines copy-in / kernels / copy-out on its own
+ *     streams), and one host-side gather copies every sub-batch's packed bytes to its chunk-order
+ *     offset as soon as its sizes land -- so no device's copy-out waits for the devices before it
+ *     to finish their whole share.  (One process per GPU under torchrun instead gives each rank
+ *     one contiguous slab, lzbench_amd/shard.py)
  *
  *  3. device-resident API -- inputs already in HBM, asynchronous on a caller stream
  *     (the nvcomp batched API analogue, reference nvcomp/lz4.h:239-371).  The input is n

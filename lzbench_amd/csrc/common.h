@@ -98,6 +98,13 @@ struct Bytes {
         sh = (int)uni((uint32_t)a & 3u);
         r = make_rsrc((const void*)(a - (uint64_t)sh), (uint32_t)(bytes + (uint64_t)sh));
     }
+    // the same view with its range ending at the dword that holds the last byte: unaligned dword
+    // reads of bytes < `bytes` see no zeros, and nothing past that dword (always mapped) is read
+    __device__ __forceinline__ void init_dw(const void* p, uint64_t bytes) {
+        const uint64_t a = (uint64_t)p;
+        sh = (int)uni((uint32_t)a & 3u);
+        r = make_rsrc((const void*)(a - (uint64_t)sh), (uint32_t)((bytes + (uint64_t)sh + 3u) & ~3ull));
+    }
     __device__ __forceinline__ uint32_t b(int pos) const { return ld_u8(r, pos + sh); }
     __device__ __forceinline__ uint32_t w32(int pos) const { return ld_u32(r, pos + sh); }
     __device__ __forceinline__ uint64_t w40(int pos) const { return ld_u40(r, pos + sh); }

@@ -881,7 +881,8 @@ extern "C" int lzh_debug_dec_stats(unsigned long long* host, int reset) {
 //   literals, sequences  zstd/lib/decompress/zstd_decompress_block.c (ZSTD_decodeLiteralsBlock,
 //                        ZSTD_decodeSeqHeaders, ZSTD_buildFSETable, ZSTD_decodeSequence,
 //                        ZSTD_decompressSequences_body)
-//   Huffman              zstd/lib/decompress/huf_decompress.c (HUF_readDTableX1, 1X1 / 4X1 streams)
+//   Huffman              zstd/lib/decompress/huf_decompress.c (HUF_readDTableX1, 1X1 / 4X1 streams;
+//                        the 1X2 / 4X2 acceptance rules where HUF_selectDecoder picks X2)
 //   FSE headers          zstd/lib/common/entropy_common.c (FSE_readNCount, HUF_readStats),
 //                        zstd/lib/common/fse_decompress.c (weights: two interleaved states)
 // One wave per frame.  Entropy decoding is inherently sequential, so it runs as wave-uniform
@@ -894,7 +895,7 @@ extern "C" int lzh_debug_dec_stats(unsigned long long* host, int reset) {
 // Scope: frames as lzbench writes them (content size present, no dictionary), with or without the
 // XXH64 content checksum (verified);
 // others return kErrUnsupported.  Valid frames decode to the reference's bytes; corrupt frames
-// are rejected without faulting (verdicts on corrupt input are not pinned to the reference's).
+// are rejected without faulting, with the reference's accept / reject verdict (tests/test_gpu_zstd.py).
 namespace zstdd {
 
 constexpr int kZW = 2048;               // LDS output window (zstd offsets are mostly far anyway)
@@ -967,7 +968,7 @@ __device__ uint64_t xxh64_wave(const Bytes& b, int len, int lane) {
 constexpr int kZClk = 8;
 #define ZCLK(F, i) do { if (LZH_ZSTD_STATS) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); (F).clk[i] += t_ - (F).clk_last; (F).clk_last = t_; } } while (0)
 constexpr int kBlockMax = 128 * 1024;
-constexpr int kHufLogMax = 11;          // the reference encoder's maximum (HUF_TABLELOG_DEFAULT)
+constexpr int kHufLogMax = 12;          // HUF_TABLELOG_MAX (huf.h:119): the decoder accepts 12
 
 // literal-length / match-length codes: baseline and extra bits (RFC 8878 3.1.1.3.2.1.1;
 // common/zstd_internal.h LL_bits / ML_bits) and the predefined distributions (3.1.1.3.2.2;
@@ -1453,6 +1454,108 @@ __device__ __forceinline__ int huf_streams(const Bytes& src, int pos, int csize,
             out.st8(dst + lane * seg + i, e & 0xffu);
         }
     }
+    return ballot(on && P != lo) ? 1 : 0;              // 1: some stream not exactly consumed
+}
+
+// HUF_selectDecoder (huf_decompress.c:1565-1615): 1 when the reference decodes a 4-stream literal
+// section it has just read a tree for with the double-symbol decoder (X2)
+__constant__ uint16_t kAlgoTime[16][4] = {
+    {0, 0, 1, 1}, {0, 0, 1, 1}, {150, 216, 381, 119}, {170, 205, 514, 112}, {177, 199, 539, 110},
+    {197, 194, 644, 107}, {221, 192, 735, 107}, {256, 189, 881, 106}, {359, 188, 1167, 109},
+    {582, 187, 1570, 114}, {688, 187, 1712, 122}, {825, 186, 1965, 136}, {976, 185, 2131, 150},
+    {1180, 186, 2070, 175}, {1377, 185, 1731, 202}, {1412, 185, 1695, 202}};
+__device__ __forceinline__ bool huf_select_x2(int dstSize, int cSrcSize) {
+    const int Q = cSrcSize >= dstSize ? 15 : (int)((uint32_t)cSrcSize * 16u / (uint32_t)dstSize);
+    const uint32_t D256 = (uint32_t)dstSize >> 8;
+    const uint32_t t0 = kAlgoTime[Q][0] + kAlgoTime[Q][1] * D256;
+    uint32_t t1 = kAlgoTime[Q][2] + kAlgoTime[Q][3] * D256;
+    t1 += t1 >> 5;
+    return t1 < t0;
+}
+
+// The double-symbol decoder's verdict (HUF_decompress1X2 / 4X2_usingDTable_internal_body,
+// huf_decompress.c:1176-1363), run when the single-symbol walk of huf_streams did not consume some
+// stream exactly and the reference table is X2.  Both decoders emit the same symbols wherever the
+// bits are read inside the stream (an X2 cell of targetLog = max(11, tl) bits holds the next code
+// and, when both fit, the code after it: HUF_fillDTableX2), and a stream X1 accepts X2 accepts
+// with the same bytes.  X2 differs on corrupt streams in three ways, restated here per lane (one
+// stream per lane, lookups in lock step):
+//  * the last symbol of a stream (HUF_decodeLastSymbolX2, :1148-1163): a two-symbol cell skips
+//    both codes and clamps an overrun to the stream start, so the stream ends exactly consumed
+//    whenever it had bits left; with none left the cell comes from the top bits of the 64-bit
+//    container loaded at the stream start (bitsConsumed == 64: the shift wraps to 0);
+//  * the 4-stream loop (:1294-1342) decodes 4 cells per stream per round, 1 or 2 symbols each,
+//    until some stream's reload pointer is within 8 bytes of its start or stream 4 is within 7
+//    bytes of its end; a stream 1..3 that wrote past its segment by then is corrupt (:1345-1347).
+//    After a round's reload the pointer is ceil(r / 8) - 8 bytes above the stream start
+//    (BIT_reloadDStreamFast, r = bits left), before the first one srcSize - 8 (or 0 below 8 bytes);
+//  * anything consumed below the stream start is never recovered (bitsConsumed > 64), except by
+//    the last-symbol clamp above.
+// Symbols are written in place of the X1 walk's; returns 0 (accepted) or ZC.
+__device__ __attribute__((noinline)) int huf_streams_x2(const Bytes& src, int pos, int csize, int nstreams, const Bytes& out,
+                                                         int dst, int rs, int tl, LDSA Lds& L, int lane) {
+    const rsrc_t r = src.r;
+    int seg = rs, last = rs, s0 = pos, sz = csize;
+    if (nstreams == 4) {                               // (geometry validated by huf_streams)
+        const int b = pos + src.sh;
+        const int z1 = (int)(ld_u8(r, b) | ld_u8(r, b + 1) << 8), z2 = (int)(ld_u8(r, b + 2) | ld_u8(r, b + 3) << 8),
+                  z3 = (int)(ld_u8(r, b + 4) | ld_u8(r, b + 5) << 8);
+        seg = (rs + 3) / 4;
+        last = rs - 3 * seg;
+        const int p1 = pos + 6;
+        s0 = lane == 0 ? p1 : (lane == 1 ? p1 + z1 : (lane == 2 ? p1 + z1 + z2 : p1 + z1 + z2 + z3));
+        sz = lane == 0 ? z1 : (lane == 1 ? z2 : (lane == 2 ? z3 : csize - 6 - z1 - z2 - z3));
+    }
+    const bool on = lane < nstreams;
+    const int nsym = lane == 3 ? last : seg;
+    const int x0 = s0 + src.sh, lo = 8 * x0, X = x0 + sz - 1;
+    const uint32_t lastb = on ? ld_u8(r, X) : 1u;
+    int P = 8 * X + hb32(lastb | 1u);
+    const int T = tl <= 11 ? 11 : 12;                  // HUF_readDTableX2: maxTableLog, :1081
+    const uint32_t tmask = (1u << T) - 1u;
+    const uint32_t b6 = on && sz >= 7 ? ld_u8(r, x0 + 6) : 0u, b7 = on && sz >= 8 ? ld_u8(r, x0 + 7) : 0u;
+    const uint32_t top = ((b7 << 8) | b6) >> (16 - T);   // BIT_initDStream's container, top T bits
+    int q = sz >= 8 ? sz - 8 : 0;                      // reload pointer - start, bytes
+    bool joint = nstreams == 4 && last >= 8;           // (oend - op4 >= 8 and op4 < olimit)
+    int op = 0;
+    for (int t = 0;; t++) {
+        if (joint && t > 0 && (t & 3) == 0) {          // end of a round: the four reloads, the loop test
+            const bool cont = q >= 8 && !(lane == 3 && op >= last - 7);
+            if (ballot(on && !cont)) {
+                joint = false;
+                if (ballot(on && lane < 3 && op > seg)) return ZC;
+            } else {
+                q = ((P - lo + 7) >> 3) - 8;
+            }
+        }
+        const bool act = on && (joint || op < nsym);
+        if (!ballot(act)) break;
+        if (!act) continue;
+        uint32_t v;
+        if (P == lo) {
+            v = top;
+        } else {
+            const int qb = (P - T) >> 3, sh = (P - T) & 7;
+            const uint32_t w = ld_u8(r, qb) | ld_u8(r, qb + 1) << 8 | ld_u8(r, qb + 2) << 16;
+            v = (w >> sh) & tmask;
+            if (P - T < lo) v &= (uint32_t)(~0ull << min(lo - (P - T), 32));   // zero-padded below the start
+        }
+        const uint32_t e1 = ((volatile const LDSA uint16_t*)L.huf)[v >> (T - tl)];
+        const int n1 = (int)(e1 >> 8);
+        const uint32_t e2 = ((volatile const LDSA uint16_t*)L.huf)[((v << n1) & tmask) >> (T - tl)];
+        const int n2 = (int)(e2 >> 8);
+        const bool dbl = n1 + n2 <= T;
+        if (op < nsym) out.st8(dst + lane * seg + op, e1 & 0xffu);
+        if (!joint && op == nsym - 1) {                // HUF_decodeLastSymbolX2
+            if (!dbl) P -= n1;
+            else if (P > lo) P = max(P - n1 - n2, lo);
+            op++;
+        } else {
+            if (dbl && op + 1 < nsym) out.st8(dst + lane * seg + op + 1, e2 & 0xffu);
+            P -= dbl ? n1 + n2 : n1;
+            op += dbl ? 2 : 1;
+        }
+    }
     return ballot(on && P != lo) ? ZC : 0;
 }
 
@@ -1460,6 +1563,7 @@ struct FrameState {
     int rep0, rep1, rep2;
     int llA, ofA, mlA;                  // accuracy logs of the current tables
     bool llV, ofV, mlV, hufV;           // tables valid for "repeat" / treeless modes
+    bool hufX2;                         // the reference's table type (HUF_DTable tableType: 1 = X2)
     int hufTl;
     uint64_t clk[kZClk], clk_last;      // (LZH_ZSTD_STATS)
 };
@@ -1510,6 +1614,8 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
             if (u < 0) return u;
             F.hufV = true;
             F.hufTl = tl;
+            // (ZSTD_decodeLiteralsBlock: a 1-stream tree is read as X1, a 4-stream one by HUF_selectDecoder)
+            F.hufX2 = sf != 0 && huf_select_x2(rs, cs);
             p += u;
         } else if (!F.hufV) {
             return ZC;
@@ -1517,7 +1623,10 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
         lsrc = lout;
         lpos = fcs - rs;
         ZCLK(F, 0);
-        const int hr = huf_streams(rin, p, bs + hsz + cs - p, sf == 0 ? 1 : 4, O.out, lpos, rs, F.hufTl, L, lane);
+        if (rs == 0 && sf != 0 && ltype == 2) return ZC;   // HUF_decompress4X_hufOnly: dstSize 0
+        int hr = huf_streams(rin, p, bs + hsz + cs - p, sf == 0 ? 1 : 4, O.out, lpos, rs, F.hufTl, L, lane);
+        if (hr == 1)
+            hr = F.hufX2 ? huf_streams_x2(rin, p, bs + hsz + cs - p, sf == 0 ? 1 : 4, O.out, lpos, rs, F.hufTl, L, lane) : ZC;
         ZCLK(F, 2);
         if (hr < 0) return hr;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // literal stores visible to the window loads
@@ -1711,7 +1820,7 @@ __device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout,
     p += fsz;
     if (fcs > (uint64_t)cap) return ZC;
     const int n = (int)fcs;
-    FrameState F{1, 4, 8, 0, 0, 0, false, false, false, false, 0, {0, 0, 0, 0, 0, 0, 0, 0}, 0};
+    FrameState F{1, 4, 8, 0, 0, 0, false, false, false, false, false, 0, {0, 0, 0, 0, 0, 0, 0, 0}, 0};
     if (LZH_ZSTD_STATS) F.clk_last = __builtin_amdgcn_s_memtime();
     ZWin lw;
     lw.bind(rin, nullptr);

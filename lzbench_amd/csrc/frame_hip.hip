@@ -65,7 +65,7 @@ __device__ uint32_t xxh32_wave(const Bytes& b, uint32_t len, int lane) {
     const uint32_t tw[4] = {uni(t), uni(t2), uni(t3), uni(t4)};
     int k = 0;
     for (; p + 4 <= len; p += 4, k++) h = rotl(h + tw[k] * P3, 17) * P4;
-    for (int i = 0; p < len; p++, i++) h = rotl(h + ((tw[k] >> (8 * i)) & 0xffu) * P5, 11) * P1;
+    for (; p < len; p++) h = rotl(h + uni(b.b((int)p)) * P5, 11) * P1;   // (bytewise: exact-size views)
     h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
     return h;
 }
@@ -247,12 +247,15 @@ lzh_frame_parse_kernel(int codec, const uint8_t* packed, uint64_t packed_readabl
     const uint32_t cs = csizes[f];
     FrameDesc* D = desc + f * maxbpf;
     for (uint32_t b = (uint32_t)lane; b < maxbpf; b += 64) D[b] = FrameDesc{0, 0, 0, 0, 0, 0};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the zeroing before lane 0's descriptor stores
+    __syncthreads();
     if (cs == s) {   // stored raw by the chunk loop (lzbench.cpp:318-321)
         if (lane == 0) { D[0] = FrameDesc{ioff, foff, cs, (uint32_t)s, 1, 0}; fstat[f] = 0; }
         return;
     }
     Bytes fr;
-    fr.init(packed + ioff, ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0);
+    const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+    fr.init(packed + ioff, readable);
     auto rd = [&](uint32_t p) -> uint32_t { return uni(fr.w32((int)p)); };
     int st = 0;
     if (codec == 4) {
@@ -264,7 +267,7 @@ lzh_frame_parse_kernel(int codec, const uint8_t* packed, uint64_t packed_readabl
         if (cs < 7 || w0 != 0x184D2204u || (flg >> 6) != 1 || (flg & 2) || (bd & 0x8f) || bid < 4 || cs < hl) st = -1;
         if (!st) {   // header checksum over FLG .. the optional fields
             const uint32_t hcb = (rd(hl - 1) & 0xffu);
-            const uint32_t hw[3] = {rd(4), rd(8), rd(12)};
+            const uint32_t hw[4] = {rd(4), rd(8), rd(12), rd(16)};   // bytes 4 .. hl - 2 (up to 17)
             const int n = (int)hl - 5;
             uint32_t h = frm::P5 + (uint32_t)n;
             int p = 0;
@@ -292,7 +295,7 @@ lzh_frame_parse_kernel(int codec, const uint8_t* packed, uint64_t packed_readabl
             if (raw && sz != ds) { st = sz > ds ? -1 : -2; break; }
             if (bcrc) {
                 Bytes bb;
-                bb.init(packed + ioff + ip, sz + 16);
+                bb.init_dw(packed + ioff + ip, min<uint64_t>(sz, readable > ip ? readable - ip : 0));
                 const uint32_t h = frm::xxh32_wave(bb, sz, lane);
                 if (h != rd(ip + sz)) { st = -1; break; }
             }
@@ -349,7 +352,7 @@ lzh_frame_finish_kernel(int codec, const uint8_t* packed, const uint64_t* offset
         const uint32_t flg = uni(fr.w32(4)) & 0xffu;
         if ((flg >> 2) & 1) {
             Bytes o, tail;
-            o.init(out + foff, s + 16);
+            o.init_dw(out + foff, s);
             const uint32_t h = frm::xxh32_wave(o, (uint32_t)s, lane);
             tail.init(packed + offsets[f] + csizes[f] - 4, 4);   // (bytewise: the range ends at the frame's end)
             const uint32_t c = tail.b(0) | tail.b(1) << 8 | tail.b(2) << 16 | tail.b(3) << 24;

@@ -2,15 +2,24 @@
 
 Chunks are independent (reference _lzbench/lzbench.cpp:366-373: each chunk is compressed on its
 own), so rank r of W takes the contiguous chunk range [r*K/W, (r+1)*K/W) of the lzbench chunk
-list, compresses it on its own GPU, and the packed slabs are gathered to rank 0 in chunk order
-(the host-side gather; no collective on the data path beyond moving the finished bytes).  The
-result is byte-identical to the single-process chunk loop.
+list and compresses it on its own GPU.  The one exchange is SURVEY 8(e)'s single host-side
+gather: the ranks all-gather their packed totals and chunk counts (a few bytes, control plane),
+then every rank copies its packed slab and its compr_sizes straight into one shared host buffer
+(a /dev/shm mapping) at its chunk-order offset -- the layout of lzbench's compbuf
+(lzbench.cpp:266-298: chunk i at sum(clen[<i])).  No collective moves codec bytes.  The result is
+byte-identical to the single-process chunk loop.  bench.py times the same gather on HBM-resident
+slabs.
 """
 from __future__ import annotations
 
+import mmap
+import os
+import time
 from typing import Callable, Optional, Tuple
 
 import numpy as np
+
+_seq = [0]
 
 
 def shard_range(nchunks: int, rank: int, world: int) -> Tuple[int, int]:
@@ -25,33 +34,75 @@ def shard_bytes(n: int, chunk_size: int, rank: int, world: int) -> Tuple[int, in
     return min(c0 * chunk_size, n), min(c1 * chunk_size, n)
 
 
+def gather_slabs(packed, csizes, rank: int, world: int, group=None, keep: bool = True):
+    """Place every rank's packed slab and compr_sizes in one shared host buffer in chunk order.
+
+    packed: this rank's packed bytes (numpy u8 array, or a torch u8 tensor on the host or the GPU);
+    csizes: its per-chunk compressed sizes (numpy / torch, any integer type).  Returns
+    ({"ms", "bytes", "GBps"} of the slab copies, max over ranks; (packed_all, csizes_all) on rank 0
+    when keep, else None)."""
+    import torch
+    import torch.distributed as dist
+
+    def as_tensor(a, dtype):
+        t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+        return t.reshape(-1).to(dtype) if t.dtype != dtype else t.reshape(-1)
+
+    p = as_tensor(packed, torch.uint8)
+    c = as_tensor(csizes, torch.int64)
+    meta = torch.tensor([p.numel(), c.numel()], dtype=torch.int64)
+    metas = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    sizes = [int(m[0]) for m in metas]
+    counts = [int(m[1]) for m in metas]
+    grand, kall = sum(sizes), sum(counts)
+    base, cbase = sum(sizes[:rank]), sum(counts[:rank])
+    nbytes = grand + 8 * kall
+    tag = f"{os.environ.get('MASTER_PORT', '0')}_{_seq[0]}"
+    _seq[0] += 1
+    path = f"/dev/shm/lzh_gather_{tag}"
+    if rank == 0:
+        with open(path, "wb") as f:
+            f.truncate(max(nbytes, 1))
+    dist.barrier(group=group)
+    fd = os.open(path, os.O_RDWR)
+    mm = mmap.mmap(fd, max(nbytes, 1))
+    host = torch.frombuffer(mm, dtype=torch.uint8, count=max(nbytes, 1))
+    if p.is_cuda:
+        torch.cuda.synchronize()
+    dist.barrier(group=group)
+    t = time.perf_counter()
+    if p.numel():
+        host[base:base + p.numel()].copy_(p)
+    if c.numel():
+        host[grand + 8 * cbase:grand + 8 * (cbase + c.numel())].copy_(c.cpu().view(torch.uint8))
+    if p.is_cuda:
+        torch.cuda.synchronize()
+    dist.barrier(group=group)
+    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX, group=group)
+    res = None
+    if rank == 0 and keep:
+        buf = np.frombuffer(mm, np.uint8, count=nbytes) if nbytes else np.zeros(0, np.uint8)
+        res = (buf[:grand].copy(), buf[grand:].copy().view("<i8").astype(np.uint64))
+        del buf
+    del host
+    dist.barrier(group=group)
+    mm.close()
+    os.close(fd)
+    if rank == 0:
+        os.unlink(path)
+    ms = float(el.item()) * 1e3
+    return {"ms": round(ms, 3), "bytes": grand, "GBps": round(grand / max(ms * 1e-3, 1e-9) / 1e9, 2)}, res
+
+
 def sharded_compress(data: np.ndarray, chunk_size: int, rank: int, world: int,
                      compress: Callable[[np.ndarray], Tuple[np.ndarray, np.ndarray]],
                      group=None) -> Optional[Tuple[np.ndarray, np.ndarray]]:
     """Compress this rank's shard with `compress(shard) -> (packed, csizes)` and gather every
-    rank's slab to rank 0.  Returns (packed, csizes) on rank 0, None elsewhere."""
-    import torch
-    import torch.distributed as dist
-
+    rank's slab into the shared host buffer.  Returns (packed, csizes) on rank 0, None elsewhere."""
     b0, b1 = shard_bytes(len(data), chunk_size, rank, world)
     packed, cs = compress(np.ascontiguousarray(data[b0:b1])) if b1 > b0 else (
         np.zeros(0, np.uint8), np.zeros(0, np.uint64))
-    # sizes first (a few KB), then the slabs themselves: rank 0 lays them out by prefix sums
-    meta = torch.tensor([len(packed), len(cs)], dtype=torch.int64)
-    metas = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(metas, meta, group=group)
-    maxp = int(max(m[0] for m in metas)) or 1
-    maxc = int(max(m[1] for m in metas)) or 1
-    pbuf = torch.zeros(maxp, dtype=torch.uint8)
-    pbuf[: len(packed)] = torch.from_numpy(packed)
-    cbuf = torch.zeros(maxc, dtype=torch.int64)
-    cbuf[: len(cs)] = torch.from_numpy(cs.astype(np.int64))
-    plist = [torch.zeros(maxp, dtype=torch.uint8) for _ in range(world)] if rank == 0 else None
-    clist = [torch.zeros(maxc, dtype=torch.int64) for _ in range(world)] if rank == 0 else None
-    dist.gather(pbuf, plist, dst=0, group=group)
-    dist.gather(cbuf, clist, dst=0, group=group)
-    if rank != 0:
-        return None
-    packed_all = np.concatenate([plist[r][: int(metas[r][0])].numpy() for r in range(world)])
-    cs_all = np.concatenate([clist[r][: int(metas[r][1])].numpy() for r in range(world)]).astype(np.uint64)
-    return packed_all, cs_all
+    _, res = gather_slabs(packed, cs, rank, world, group=group)
+    return res

@@ -152,8 +152,9 @@ int64_t oracle_lz4f_decompress(const uint8_t* src, size_t cs, uint8_t* dst, size
     const int bcrc = (flg >> 4) & 1, csz = (flg >> 3) & 1, ccrc = (flg >> 2) & 1, dict = flg & 1;
     const size_t hl = 7 + 8 * (size_t)csz + 4 * (size_t)dict;
     if (cs < hl) return -1;
-    if (dict) return -2;
+    /* LZ4F_decodeHeader's order (lz4frame.c:1150-1260): the header checksum, then the dictionary id */
     if (src[hl - 1] != (uint8_t)((oracle_xxh32(src + 4, hl - 5, 0) >> 8) & 0xff)) return -1;
+    if (dict) return -2;
     const size_t B = bsid_size(bid);
     size_t ip = hl, op = 0;
     for (int nb = 0;; nb++) {

@@ -27,16 +27,20 @@ sys.path.insert(0, os.path.dirname(HERE))
 import lzbench_amd as L          # noqa: E402  (datagen only)
 import oracle_lib as O           # noqa: E402
 
-# (corpus, codec, chunk, level): the north star, config 3 at 1 GiB, config 4's per-GPU share,
-# config 5's codec at its chunk size on a 1 GiB per-GPU share
+# (corpus, codec, chunk, level, size): the north star, config 3 at 1 GiB, config 4's per-GPU share,
+# config 5's codec at its chunk size on a 1 GiB per-GPU share; then the other sweep lines of
+# tools/config_sweep.sh at their exact sizes: config 2 (256 MiB text), config 5's 8-GPU per-GPU
+# share (512 MiB mixed), lz4fast,3 on the north-star input
 WORKLOADS = [
-    ("text", "lz4", 65536, 1),
-    ("mixed", "snappy", 262144, 0),
-    ("json", "lz4", 65536, 1),
-    ("json", "snappy", 65536, 0),
-    ("mixed", "zstd", 131072, 1),
+    ("text", "lz4", 65536, 1, 1 << 30),
+    ("mixed", "snappy", 262144, 0, 1 << 30),
+    ("json", "lz4", 65536, 1, 1 << 30),
+    ("json", "snappy", 65536, 0, 1 << 30),
+    ("mixed", "zstd", 131072, 1, 1 << 30),
+    ("text", "lz4", 65536, 1, 256 << 20),
+    ("mixed", "zstd", 131072, 1, 512 << 20),
+    ("text", "lz4fast", 65536, 3, 1 << 30),
 ]
-SIZE = 1 << 30
 SEED = 12345
 
 
@@ -53,18 +57,18 @@ def main():
     only = set(sys.argv[1:])
     path = os.path.join(HERE, "fullsize.json")
     out = json.load(open(path)) if os.path.exists(path) else []
-    have = {(e["corpus"], e["codec"], e["chunk"], e["level"]) for e in out}
+    have = {(e["corpus"], e["codec"], e["chunk"], e["level"], e["size"]) for e in out}
     datas = {}
-    for corpus, codec, chunk, level in WORKLOADS:
-        if (corpus, codec, chunk, level) in have or (only and codec not in only):
+    for corpus, codec, chunk, level, size in WORKLOADS:
+        if (corpus, codec, chunk, level, size) in have or (only and codec not in only):
             continue
-        if corpus not in datas:
-            datas = {corpus: L.datagen(corpus, SIZE, seed=SEED)}
-        data = datas[corpus]
+        if (corpus, size) not in datas:
+            datas = {(corpus, size): L.datagen(corpus, size, seed=SEED)}
+        data = datas[(corpus, size)]
         packed, cs = O.compress_chunks(data, codec, chunk, level, use_ref=True, threads=8)
-        e = {"corpus": corpus, "size": SIZE, "seed": SEED, "codec": codec, "chunk": chunk, "level": level,
+        e = {"corpus": corpus, "size": size, "seed": SEED, "codec": codec, "chunk": chunk, "level": level,
              "input_sha256": sha(data), "packed_sha256": sha(packed), "csizes_sha256": sha(cs.astype("<u8")),
-             "packed_bytes": int(len(packed)), "ratio_pct": round(100 * len(packed) / SIZE, 3)}
+             "packed_bytes": int(len(packed)), "ratio_pct": round(100 * len(packed) / size, 3)}
         print(e, flush=True)
         out.append(e)
         with open(path, "w") as f:

@@ -135,3 +135,51 @@ def test_corrupt_frames_verdicts(torch_cuda, codec, params):
             assert out[j * part:(j + 1) * part].tobytes() == dst[:part].tobytes()
         elif r == -2:
             assert st == -2
+
+
+def _with_dict_id(frame: bytes, flip_only: bool) -> bytes:
+    """The frame with FLG's dictionary-id bit set.  flip_only: just the bit (the header checksum no
+    longer matches); else a well-formed header: content size + dictionary id fields, checksum redone."""
+    flg, bd = frame[4], frame[5]
+    csz = (flg >> 3) & 1
+    hl = 7 + 8 * csz
+    if flip_only:
+        b = bytearray(frame)
+        b[4] ^= 1
+        return bytes(b)
+    body = frame[hl:]
+    cs_field = frame[6:6 + 8] if csz else None
+    hdr = bytearray([flg | 0x09, bd]) + (cs_field if csz else bytes(8)) + (0x1234567).to_bytes(4, "little")
+    if not csz:
+        return None
+    h = np.frombuffer(bytes(hdr), np.uint8).copy()
+    hc = (O.oracle().oracle_xxh32(h.ctypes.data, len(h), 0) >> 8) & 0xff
+    return bytes(frame[:4]) + bytes(hdr) + bytes([hc]) + body
+
+
+def test_dict_id_frames(torch_cuda):
+    """A well-formed frame carrying a dictionary id (with content size: the 19-byte header, checksum
+    over bytes 4..17) is refused as unsupported (-2) by the GPU and by the restatement alike; a frame
+    whose dictionary-id bit alone was flipped fails LZ4F_decodeHeader's header checksum first (-1)."""
+    torch = torch_cuda
+    part = 70000
+    data = L.datagen("text", 4 * part, seed=5)
+    packed, cs = O.compress_chunks(data, "lz4f", part, 0x40)      # content size on
+    offs = np.concatenate([[0], np.cumsum(cs)]).astype(np.int64)
+    valid = [packed[offs[i]:offs[i + 1]].tobytes() for i in range(len(cs))]
+    frames = [_with_dict_id(v, False) for v in valid] + [_with_dict_id(v, True) for v in valid]
+    want = [-2] * len(valid) + [-1] * len(valid)
+    orc = O.oracle()
+    for s, w in zip(frames, want):
+        src = np.frombuffer(s, np.uint8).copy()
+        dst = np.zeros(part + 64, np.uint8)
+        assert orc.oracle_lz4f_decompress(src.ctypes.data, len(s), dst.ctypes.data, part) == w
+    blob = b"".join(frames)
+    k = len(frames)
+    d_packed = torch.zeros(len(blob) + 256, dtype=torch.uint8, device="cuda")
+    d_packed[: len(blob)].copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
+    d_cs = torch.tensor([len(s) for s in frames], dtype=torch.int32, device="cuda")
+    dc = L.DeviceCodec("lz4frame", k * part, part)
+    dc.decompress(packed=d_packed, csizes=d_cs)
+    torch.cuda.synchronize()
+    assert dc.status[:k].cpu().numpy().tolist() == want

@@ -50,6 +50,24 @@ def test_sharded_large_sub_batches(torch_cuda):
     assert (out == data).all()
 
 
+def test_eight_shards_north_star_digest(torch_cuda):
+    """The in-process -g8 product path (api.cpp make_plan: 128 MiB sub-batches dealt round-robin to
+    8 logical shards, per-shard copy / kernel / copy streams, host gather in chunk order) on the whole
+    1 GiB north-star input: packed stream and compr_sizes equal the reference chunk loop's digest
+    (tests/golden/fullsize.json), and the 8-shard decode round-trips."""
+    import hashlib
+    import json
+    big = [e for e in json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize.json")))
+           if (e["corpus"], e["codec"], e["chunk"], e["size"]) == ("text", "lz4", 65536, 1 << 30)][0]
+    data = L.datagen("text", big["size"], seed=big["seed"])
+    packed, cs = L.compress_chunks(data, "lz4", 65536, ngpus=8)
+    assert len(packed) == big["packed_bytes"]
+    assert hashlib.sha256(cs.astype("<u8").tobytes()).hexdigest() == big["csizes_sha256"]
+    assert hashlib.sha256(packed.tobytes()).hexdigest() == big["packed_sha256"]
+    out = L.decompress_chunks(packed, cs, len(data), "lz4", 65536, ngpus=8)
+    assert (out == data).all()
+
+
 @pytest.mark.parametrize("codec", ["lz4", "snappy"])
 def test_single_chunk_whole_input_row(torch_cuda, codec):
     """lzbench without -b: one chunk = the whole file (chunk_size clamped to the file size).

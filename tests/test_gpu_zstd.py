@@ -2,7 +2,7 @@
 zstd 1.5.2 with lzbench's zstd-row parameters (compressors.cpp:1745-1773): the committed golden
 frames, fresh frames over corpora x chunk sizes x levels (raw, RLE and compressed blocks,
 predefined / RLE / FSE / repeat tables, 1- and 4-stream Huffman literals, multi-block frames),
-edge sizes, and corrupted frames (no fault; an accepted frame decodes as the reference does).
+edge sizes, and corrupted frames (no fault; the reference's accept / reject verdict, and its bytes).
 Parity is exact: the decoded bytes must equal the original input.  Run with -m gpu."""
 import numpy as np
 import pytest
@@ -89,37 +89,121 @@ def _corrupt(rng, s: bytes) -> bytes:
     return bytes(b)
 
 
-@pytest.mark.parametrize("corpus_kind", ["text", "json"])
-def test_corrupt_frames(torch_cuda, corpus_kind):
-    """1024 corrupted frames: the decoder never faults; a frame it accepts is one the reference
-    accepts, with the same bytes (it may reject more: verdict parity is not claimed for zstd)."""
-    if not O.have_ref():
-        pytest.skip("reference build (oracle/_ref) not present")
-    torch = torch_cuda
-    chunk = 32768
-    rng = np.random.default_rng(5 + len(corpus_kind))
-    data = L.datagen(corpus_kind, 8 * chunk, 31)
+def _verdicts(torch, streams, chunk):
+    """GPU decode of every stream; the (index, gpu, reference) triples whose accept / reject verdicts
+    differ (lzbench's length check: a frame is accepted when it decodes to exactly `chunk` bytes), and
+    asserts the bytes of every frame both accept are the reference's."""
+    blob = np.frombuffer(b"".join(streams), np.uint8)
+    st, out = gpu_decode(torch, blob, [len(s) for s in streams], len(streams) * chunk, chunk)
+    R = O.ref()
+    mism = []
+    for i, s in enumerate(streams):
+        src = np.frombuffer(s, np.uint8).copy()
+        dst = np.zeros(chunk + 64, np.uint8)
+        r = R.ref_zstd_decompress(src.ctypes.data, len(s), dst.ctypes.data, chunk)
+        if (st[i] == chunk) != (r == chunk):
+            mism.append((i, int(st[i]), int(r)))
+        elif r == chunk:
+            assert (out[i * chunk:(i + 1) * chunk] == dst[:chunk]).all(), f"stream {i}: bytes differ"
+    return mism, int((st == chunk).sum())
+
+
+def _plain_frames(kind, chunk, seed):
+    data = L.datagen(kind, 8 * chunk, seed)
     packed, cs = O.compress_chunks(data, "zstd", chunk, 1)
     offs = np.concatenate([[0], np.cumsum(cs)]).astype(np.int64)
-    valid = [packed[offs[i]:offs[i + 1]].tobytes() for i in range(len(cs))]
+    return [packed[offs[i]:offs[i + 1]].tobytes() for i in range(len(cs)) if cs[i] != chunk]
+
+
+@pytest.mark.parametrize("corpus_kind", ["text", "json", "mixed"])
+def test_corrupt_frames(torch_cuda, corpus_kind):
+    """1024 randomly corrupted plain (unchecksummed) frames per corpus: the decoder never faults and
+    its accept / reject verdict equals ZSTD_decompressDCtx's frame for frame (including the literal
+    sections the reference decodes with the double-symbol Huffman decoder: HUF_selectDecoder,
+    huf_decompress.c:1593-1615), with the same bytes when both accept."""
+    if not O.have_ref():
+        pytest.skip("reference build (oracle/_ref) not present")
+    chunk = 32768
+    rng = np.random.default_rng(5 + len(corpus_kind))
+    valid = _plain_frames(corpus_kind, chunk, 31)
     streams = []
     while len(streams) < 1024:
         s = _corrupt(rng, valid[int(rng.integers(0, len(valid)))])
         if 0 < len(s) != chunk:
             streams.append(s)
-    blob = np.frombuffer(b"".join(streams), np.uint8)
-    st, out = gpu_decode(torch, blob, [len(s) for s in streams], len(streams) * chunk, chunk)
-    R = O.ref()
-    accepted = 0
-    for i, s in enumerate(streams):
-        if st[i] < 0:
-            continue
-        accepted += 1
-        src = np.frombuffer(s, np.uint8).copy()
-        dst = np.zeros(chunk + 64, np.uint8)
-        r = R.ref_zstd_decompress(src.ctypes.data, len(s), dst.ctypes.data, chunk)
-        assert r == st[i], f"stream {i}: gpu accepted {st[i]} bytes, reference {r}"
-        assert (out[i * chunk: i * chunk + r] == dst[:r]).all(), f"stream {i}: bytes differ"
+    mism, accepted = _verdicts(torch_cuda, streams, chunk)
+    assert not mism, mism[:10]
+    assert accepted > 0
+
+
+def _huf_stream_spans(frame: bytes):
+    """Byte ranges [a, b) of the Huffman literal streams of every compressed block of a frame
+    (RFC 8878 3.1.1.3.1; 4-stream sections: the jump table is included as its own 6-byte span)."""
+    fhd = frame[4]
+    p = 5 + (0 if (fhd >> 5) & 1 else 1)
+    p += (0, 1, 2, 4)[fhd & 3]
+    fcsf = fhd >> 6
+    p += (1 if (fhd >> 5) & 1 else 0, 2, 4, 8)[fcsf]
+    spans = []
+    while p + 3 <= len(frame):
+        bh = frame[p] | frame[p + 1] << 8 | frame[p + 2] << 16
+        p += 3
+        last, btype, bsz = bh & 1, (bh >> 1) & 3, bh >> 3
+        if btype == 2 and (frame[p] & 3) >= 2:
+            b0, sf = frame[p], (frame[p] >> 2) & 3
+            hsz = 3 if sf <= 1 else (4 if sf == 2 else 5)
+            bits = 10 if sf <= 1 else (14 if sf == 2 else 18)
+            h = int.from_bytes(frame[p:p + hsz], "little")
+            cs = (h >> (4 + bits)) & ((1 << bits) - 1)
+            q = p + hsz
+            if b0 & 3 == 2:
+                hb = frame[q]
+                q += 1 + (hb if hb < 128 else (hb - 127 + 1) // 2)
+            end = p + hsz + cs
+            if sf == 0:
+                spans.append((q, end))
+            else:
+                z1, z2, z3 = (int.from_bytes(frame[q + 2 * j:q + 2 * j + 2], "little") for j in range(3))
+                spans.append((q, q + 6))
+                a = q + 6
+                for z in (z1, z2, z3):
+                    spans.append((a, a + z))
+                    a += z
+                spans.append((a, end))
+        p += bsz if btype != 1 else 1
+        if last:
+            break
+    return [(a, b) for a, b in spans if 0 <= a < b <= len(frame)]
+
+
+@pytest.mark.parametrize("corpus_kind,chunk", [("text", 32768), ("json", 65536), ("mixed", 131072)])
+def test_corrupt_huffman_streams(torch_cuda, corpus_kind, chunk):
+    """1024 frames per case corrupted inside the Huffman literal streams -- their first and last bytes
+    (where the double-symbol decoder's last-symbol step and the 4-stream loop's bounds decide), the
+    jump table, anywhere in a stream: verdict and bytes equal ZSTD_decompressDCtx's."""
+    if not O.have_ref():
+        pytest.skip("reference build (oracle/_ref) not present")
+    rng = np.random.default_rng(91 + chunk)
+    valid = [(f, _huf_stream_spans(f)) for f in _plain_frames(corpus_kind, chunk, 57)]
+    valid = [(f, sp) for f, sp in valid if sp]
+    assert valid
+    streams = []
+    while len(streams) < 1024:
+        f, sp = valid[int(rng.integers(0, len(valid)))]
+        a, b = sp[int(rng.integers(0, len(sp)))]
+        buf = bytearray(f)
+        where = int(rng.integers(0, 3))
+        i = (a + int(rng.integers(0, min(3, b - a)))) if where == 0 else \
+            (b - 1 - int(rng.integers(0, min(3, b - a)))) if where == 1 else int(rng.integers(a, b))
+        if rng.integers(0, 2):
+            buf[i] ^= 1 << int(rng.integers(0, 8))
+        else:
+            buf[i] = int(rng.integers(0, 256))
+        s = bytes(buf)
+        if s != f:
+            streams.append(s)
+    mism, accepted = _verdicts(torch_cuda, streams, chunk)
+    assert not mism, mism[:10]
     assert accepted > 0
 
 
