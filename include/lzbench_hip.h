@@ -114,6 +114,16 @@ size_t lzh_max_packed_bytes(int codec, size_t n, size_t chunk_size);
 size_t lzh_compress_temp_bytes(int codec, size_t n, size_t chunk_size);
 size_t lzh_decompress_temp_bytes(int codec, size_t n, size_t chunk_size);
 size_t lzh_num_chunks(size_t n, size_t chunk_size);
+/* 1 when the GPU codec compresses at `level` for chunks of up to chunk_size bytes, else 0 (the
+ * rows and lzh_compress_async then return LZH_EARG): zstd at the levels whose ZSTD_getParams row
+ * is the fast strategy for every chunk size up to chunk_size (lzbench's zstd level 2 is double-fast
+ * above 256 KiB: compressors.cpp:1752 via clevels.h); LZ4F / nvcomp at the parameters above. */
+int lzh_level_supported(int codec, int level, size_t chunk_size);
+/* The batched rows' sharding plan (api.cpp make_plan) and per-shard buffer sizes for n bytes in
+ * chunks of chunk_size over ngpus shards, into out[0 .. nout): chunks, chunks per sub-batch,
+ * sub-batches, shards, compress input / packed / temp bytes per sub-batch slot, then the sub-batch
+ * slots of shard 0 .. shards-1.  Host arithmetic only (no device call).  Returns the count written. */
+int lzh_debug_plan(size_t ngpus, size_t n, size_t chunk_size, int codec, uint64_t* out, int nout);
 
 /* d_csizes: nchunks u32 (out); d_offsets: nchunks+1 u64 (out; [nchunks] = packed total).
  * level: lz4 acceleration (<=1 -> LZ4_compress_default); zstd level; ignored by snappy. */

@@ -93,6 +93,13 @@ static bool frame_level_ok(int codec, int level) {
     return level >= 0 && level <= 5;
 }
 
+extern "C" int lzh_level_supported(int codec, int level, size_t chunk_size) {
+    if (codec == LZH_CODEC_ZSTD) return lzh_zstd_level_ok(level, chunk_size) ? 1 : 0;
+    if (codec == LZH_CODEC_LZ4F || codec == LZH_CODEC_NVLZ4) return frame_level_ok(codec, level) ? 1 : 0;
+    return codec >= LZH_CODEC_LZ4 && codec <= LZH_CODEC_MEMCPY ? 1 : 0;
+}
+
+
 static FrameGeo frame_geo(size_t B, size_t n, size_t F) {
     FrameGeo g;
     g.F = F;
@@ -495,6 +502,10 @@ struct Plan {
     size_t slots(size_t g) const { return nsb > g ? (nsb - g + G - 1) / G : 0; }
 };
 
+// (a chunk size above the input is one chunk of the input's size: buffers are sized from the bytes
+// present, not from lzbench's 1.79 GB default chunk)
+size_t row_chunk(size_t n, size_t chunk) { return std::max<size_t>(std::min(chunk, n), 1); }
+
 Plan make_plan(size_t ndev, size_t n, size_t chunk) {
     Plan p;
     p.n = n;
@@ -515,6 +526,7 @@ int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t c
                      size_t* compr_sizes) {
     DeviceGuard guard;
     Range range("lzh:row_compress");
+    chunk = row_chunk(n, chunk);
     const Plan P = make_plan(c->devs.size(), n, chunk);
     const size_t sb_in = std::min(n, P.sbk * chunk);                   // largest sub-batch input
     const size_t sb_packed = align_up(lzh_max_packed_bytes(c->codec, sb_in, chunk) + 64, 256);
@@ -579,6 +591,7 @@ int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t c
 int64_t run_decompress(LzhCtx* c, const uint8_t* in, const size_t* compr_sizes, size_t n, size_t chunk, uint8_t* out) {
     DeviceGuard guard;
     Range range("lzh:row_decompress");
+    chunk = row_chunk(n, chunk);
     const Plan P = make_plan(c->devs.size(), n, chunk);
     const size_t k = P.k;
     std::vector<size_t> coff(k + 1, 0);
@@ -648,6 +661,24 @@ int64_t run_decompress(LzhCtx* c, const uint8_t* in, const size_t* compr_sizes, 
     }
     return bad ? LZH_ECORRUPT : sum;
 }
+
+}  // namespace
+
+extern "C" int lzh_debug_plan(size_t ngpus, size_t n, size_t chunk_size, int codec, uint64_t* out, int nout) {
+    if (!out || nout <= 0 || chunk_size == 0) return 0;
+    chunk_size = row_chunk(n, chunk_size);
+    const Plan P = make_plan(std::max<size_t>(std::min<size_t>(ngpus, 64), 1), n, chunk_size);
+    const size_t sb_in = std::min(n, P.sbk * chunk_size);
+    std::vector<uint64_t> v = {P.k, P.sbk, P.nsb, P.G, sb_in,
+                               align_up(lzh_max_packed_bytes(codec, sb_in, chunk_size) + 64, 256),
+                               lzh_compress_temp_bytes(codec, sb_in, chunk_size)};
+    for (size_t g = 0; g < P.G; g++) v.push_back(P.slots(g));
+    const int m = std::min<int>(nout, (int)v.size());
+    for (int i = 0; i < m; i++) out[i] = v[i];
+    return m;
+}
+
+namespace {
 
 int64_t one_chunk_compress(int codec_expect, char* in, size_t insize, char* out, size_t outsize, size_t level, char* wm) {
     LzhCtx* c = ctx_of(wm);

@@ -1138,7 +1138,10 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                      uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint64_t frame_size, uint32_t bpf) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + (LZH_PARSE_NORING ? 0 : lz4v3::kRing / 4 + 8)];   // table | ring + mirror
+#ifndef LZH_PARSE_LDS_PAD
+#define LZH_PARSE_LDS_PAD 0   // (occupancy experiments: extra LDS bytes per wave)
+#endif
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + (LZH_PARSE_NORING ? 0 : lz4v3::kRing / 4 + 8) + LZH_PARSE_LDS_PAD / 4];   // table | ring + mirror
     const uint64_t chunk = blockIdx.x;
     uint64_t off;
     int n;

@@ -276,6 +276,17 @@ static void bench_one(params_t* P, std::vector<size_t>& file_sizes, const compre
     size_t chunk = P->chunk_size > insize ? insize : P->chunk_size;
     if (d->max_block_size && chunk > (size_t)d->max_block_size) chunk = (size_t)d->max_block_size;
     if (!d->compress || !d->decompress || !chunk) return;
+    {   // GPU rows whose level the device codec does not cover for this chunk size (zstd level 2 is
+        // double-fast above 256 KiB chunks): say so instead of an error row
+        const int codec = d->init == lzbench_hip_zstd_init ? LZH_CODEC_ZSTD
+                        : d->init == lzbench_hip_lz4frame_init ? LZH_CODEC_LZ4F
+                        : d->init == lzbench_hip_nvcomp_lz4_init ? LZH_CODEC_NVLZ4 : -1;
+        if (codec >= 0 && !lzh_level_supported(codec, level, chunk)) {
+            LZB_PRINT(1, "%s %s -%d: level not supported by the GPU codec for %zu-byte chunks (skipped)\n", d->name,
+                      d->version, level, chunk);
+            return;
+        }
+    }
     char* wm = d->init ? d->init(chunk, p1, p2) : nullptr;
     if (d->init && !wm) { LZB_PRINT(1, "%s: init failed\n", d->name); return; }
     std::vector<size_t> chunks, cs;
@@ -304,6 +315,11 @@ static void bench_one(params_t* P, std::vector<size_t>& file_sizes, const compre
         if (iters >= P->c_iters && t1 - t_start > P->cmintime * 1000000ull) break;
     }
     if (complen <= 0) err = true;
+    if (const char* dd = getenv("LZH_DUMP_DIR")) {   // test hook: the packed compbuf and compr_sizes of the row
+        std::string nm = std::string(dd) + "/" + d->name + "_" + std::to_string(level);
+        if (FILE* f = fopen((nm + ".bin").c_str(), "wb")) { fwrite(compbuf, 1, (size_t)std::max<int64_t>(complen, 0), f); fclose(f); }
+        if (FILE* f = fopen((nm + ".sizes").c_str(), "wb")) { fwrite(cs.data(), sizeof(size_t), cs.size(), f); fclose(f); }
+    }
     if (!P->compress_only) {
         iters = 0;
         const uint64_t t_dstart = now_ns();

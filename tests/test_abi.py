@@ -88,3 +88,50 @@ def test_product_sources_never_reference_the_oracle():
                 txt = open(os.path.join(d, f)).read()
                 for bad in ("liboracle", "libref", "oracle_lib", "import oracle", "oracle/"):
                     assert bad not in txt, (f, bad)
+
+
+def _plan(ngpus, n, chunk, codec=0):
+    out = (C_U64 * 80)()
+    m = L.lib().lzh_debug_plan(ngpus, n, chunk, codec, out, 80)
+    v = [int(x) for x in out[:m]]
+    k, sbk, nsb, G, sb_in, sb_packed, sb_temp = v[:7]
+    return dict(k=k, sbk=sbk, nsb=nsb, G=G, sb_in=sb_in, sb_packed=sb_packed, sb_temp=sb_temp, slots=v[7:])
+
+
+import ctypes as _C  # noqa: E402
+C_U64 = _C.c_uint64
+
+
+@pytest.mark.parametrize("ngpus", [1, 2, 3, 8, 64])
+@pytest.mark.parametrize("n,chunk", [(0, 65536), (1, 65536), (65537, 65536), (1 << 30, 65536), (3 << 20, 1_790_000_000),
+                                     ((300 << 20) + 77, 65536), (1 << 40, 65536), (8 << 30, 1 << 20), (12345, 100)])
+def test_batched_row_plan_arithmetic(ngpus, n, chunk):
+    """api.cpp make_plan (the batched rows' sharding, host arithmetic only): every chunk in exactly one
+    sub-batch, sub-batches dealt round-robin (shard slot counts differ by at most one), a sub-batch's
+    buffers sized from the bytes actually present (one chunk of lzbench's default 1.79 GB chunk size
+    over a 3 MiB file must not size 1024 chunks: round 1's 1 TB hipMalloc), and no shard's buffers
+    exceed its share of the input by more than one sub-batch."""
+    p = _plan(ngpus, n, chunk)
+    chunk = max(min(chunk, n), 1)                  # (api.cpp row_chunk)
+    k = max(1, -(-n // chunk))
+    assert p["k"] == k
+    assert p["nsb"] * p["sbk"] >= k > (p["nsb"] - 1) * p["sbk"]
+    assert p["G"] == min(ngpus, k, p["nsb"]) and len(p["slots"]) == p["G"]
+    assert sum(p["slots"]) == p["nsb"] and max(p["slots"]) - min(p["slots"]) <= 1
+    assert p["sb_in"] == min(n, p["sbk"] * chunk)
+    assert p["sb_packed"] >= p["sb_in"] and p["sb_packed"] % 256 == 0
+    assert p["sb_packed"] <= p["sb_in"] + p["sbk"] * (chunk // 6 + 300) + 4096
+    assert max(p["slots"]) * p["sb_in"] <= -(-n // p["G"]) + p["sb_in"]
+    if n < (64 << 20):
+        assert p["sb_temp"] < (256 << 20)
+
+
+def test_level_supported():
+    lib = L.lib()
+    assert lib.lzh_level_supported(3, 1, 1 << 20) == 1          # zstd 1: fast strategy at every size
+    assert lib.lzh_level_supported(3, 2, 131072) == 1           # zstd 2: fast up to 256 KiB chunks
+    assert lib.lzh_level_supported(3, 2, 1 << 20) == 0          # ... double-fast above (clevels.h)
+    assert lib.lzh_level_supported(3, 3, 65536) == 0
+    assert lib.lzh_level_supported(3, -5, 1 << 20) == 1
+    assert lib.lzh_level_supported(4, 0x88, 65536) == 0 and lib.lzh_level_supported(4, 0x74, 65536) == 1
+    assert lib.lzh_level_supported(5, 6, 65536) == 0 and lib.lzh_level_supported(0, 1, 65536) == 1

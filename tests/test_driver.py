@@ -65,19 +65,42 @@ def test_csv_format(sample):
 
 
 @pytest.mark.gpu
-def test_gpu_rows_match_reference_sizes(sample):
+def test_gpu_rows_match_reference_bytes(sample, tmp_path):
+    """The CLI's GPU rows: the size column and -- through the LZH_DUMP_DIR hook, which writes each
+    row's compbuf and compr_sizes after its compress loop -- every packed byte and chunk size equal
+    the reference chunk loop's (oracle, pinned to the reference build by tests/test_oracle.py)."""
     path, data = sample
-    out = run(["-ehip_lz4/hip_snappy/hip_lz4fast,3/hipMemcpy", "-b64", "-t0,0", "-i2,2", path])
+    env = dict(os.environ, LZH_DUMP_DIR=str(tmp_path))
+    out = run(["-ehip_lz4/hip_snappy/hip_lz4fast,3/hipMemcpy", "-b64", "-t0,0", "-i2,2", path], env=env)
     r = rows(out)
     assert "ERROR" not in out, out
-    exp = {"hip_lz4": O.compress_chunks(data, "lz4", 65536),
-           "hip_snappy": O.compress_chunks(data, "snappy", 65536),
-           "hip_lz4fast": O.compress_chunks(data, "lz4fast", 65536, 3)}
-    for name, (packed, _) in exp.items():
+    exp = {("hip_lz4", 0): O.compress_chunks(data, "lz4", 65536),
+           ("hip_snappy", 0): O.compress_chunks(data, "snappy", 65536),
+           ("hip_lz4fast", 3): O.compress_chunks(data, "lz4fast", 65536, 3)}
+    for (name, lvl), (packed, cs) in exp.items():
         key = [k for k in r if k.startswith(name + " ")]
         assert key, (name, out)
         assert int(r[key[0]][4]) == len(packed), (name, out)
+        got = np.fromfile(tmp_path / f"{name}_{lvl}.bin", np.uint8)
+        gcs = np.fromfile(tmp_path / f"{name}_{lvl}.sizes", np.uint64)
+        assert len(got) == len(packed) and (got == packed).all(), name
+        assert (gcs == cs).all(), name
     assert any(k.startswith("hipMemcpy") for k in r)
+
+
+@pytest.mark.gpu
+def test_gpu_zstd_level_outside_fast_strategy_is_skipped(tmp_path):
+    """hip_zstd -2 on 1 MiB chunks: zstd 1.5.2 picks double-fast there (clevels.h), which the GPU
+    compressor does not cover -- the row says so and is skipped, level 1 runs and round-trips."""
+    d = L.datagen("json", 2 << 20, seed=9)
+    p = tmp_path / "j.json"
+    p.write_bytes(d.tobytes())
+    out = run(["-ehip_zstd,1,2", "-b1024", "-t0,0", str(p)])
+    assert "hip_zstd 1.5.2 -2: level not supported by the GPU codec" in out, out
+    r = rows(out)
+    key = [k for k in r if k.startswith("hip_zstd 1.5.2 -1")]
+    assert key and "ERROR" not in out, out
+    assert int(r[key[0]][4]) == len(O.compress_chunks(d, "zstd", 1 << 20, 1)[0])
 
 
 @pytest.mark.gpu
