@@ -18,6 +18,9 @@
 // Long catch-ups / matches / literal runs beyond the windows take lane-parallel slow paths.
 #include "common.h"
 
+#define LZH_STR_(x) #x
+#define LZH_STR(x) LZH_STR_(x)
+
 namespace lz4v3 {
 
 // optional per-kernel event counters (debug builds of the launch only; nullptr in production)
@@ -31,7 +34,7 @@ constexpr int kCtr = 13;
 #define LZ_MARK(i) ((void)0)
 #endif
 #define LZ_CLK(i) do { if (!kStats) LZ_MARK(i); if (kStats) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); clk[i] += t_ - clk_last; clk_last = t_; } } while (0)
-constexpr int kClk = 10;
+constexpr int kClk = 12;
 
 constexpr int kMinMatch = 4;
 constexpr int kMfLimit = 12;
@@ -105,6 +108,18 @@ struct Ring {
         fill += 256;
     }
 };
+
+#ifndef LZH_UNI_GO
+#define LZH_UNI_GO 0   // (1 measured 3.5 % slower: 14.47 -> 14.97 ms, profiles/r03_h) the batch loop's exit test through readfirstlane (a uniform loop, no exec-mask latch)
+#endif
+
+#ifndef LZH_LOOP_UNI
+#define LZH_LOOP_UNI 1   // readfirstlane the loop-carried parse state at the top of every batch
+#endif
+
+#ifndef LZH_PARSE_LIFT
+#define LZH_PARSE_LIFT 0   // chain membership by binary lifting (lane gathers) instead of the scalar walk
+#endif
 
 #ifndef LZH_PARSE_NORING
 #define LZH_PARSE_NORING 0   // parse kernel without the LDS input ring (16 KiB LDS: 10 waves per CU)
@@ -584,7 +599,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                                unsigned long long* stats, rsrc_t recs, uint32_t* rec_hdr) {
     const int lane = threadIdx.x;
     Table<kSmall> T{tab};
-    uint64_t clk[kClk] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t clk[kClk] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t ctr[kCtr] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t clk_last = kStats ? __builtin_amdgcn_s_memtime() : 0;
     if (n <= 0) {
@@ -647,13 +662,27 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             PAT = 3ull | (PER << 2);
         }
 
-        for (int guard = 0; go && guard < 4 * n + 64; guard++) {
+        for (int guard = 0; (LZH_UNI_GO ? unii((int)go) != 0 : go) && guard < 4 * n + 64; guard++) {
+#if LZH_LOOP_UNI
             runb = unii(runb) != 0; retest = unii(retest) != 0;
             base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
             op = unii(op); anchor = unii(anchor); rc_tot = unii(rc_tot); nrec = unii(nrec);
             R.fill = unii(R.fill); R.ready = unii(R.ready); O.flushed = unii(O.flushed);
             so = unii(so);
+#endif
             LZ_STAT(0, 1);
+#if defined(LZH_PAD_SALU) || defined(LZH_PAD_VALU)
+            {   // (issue-resource experiments: extra dependent scalar / vector instructions per batch)
+                uint32_t pad_ = (uint32_t)guard;
+#ifdef LZH_PAD_SALU
+                asm volatile(".rept " LZH_STR(LZH_PAD_SALU) "\n s_add_u32 %0, %0, 1\n .endr" : "+s"(pad_));
+#endif
+#ifdef LZH_PAD_VALU
+                asm volatile(".rept " LZH_STR(LZH_PAD_VALU) "\n v_add_u32 %0, %0, 1\n .endr" : "+v"(pad_));
+#endif
+                asm volatile("" ::"v"(pad_));
+            }
+#endif
             if (kFast && runb && base + LZH_WAVE - 1 + acc > mfl1) {
                 // near the chunk end a probe's forwardIp may pass mflimit: stride batches take over
                 // (the pending ip-2 insert first, then the re-test or the next search probe)
@@ -840,15 +869,43 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         bool endip = false;                            // a match ended past mflimit
                         // link: next member lane, or 0x80 for the rare cases (long match, parse end)
                         const int link = (lng || p + kMinMatch + cn >= mfl1) ? 0x80 : f;
+#if LZH_PARSE_LIFT
+                        // chain membership lane-parallel (binary lifting over the links, as the decoder's
+                        // chain_members): jumps of 1, 2, 4, 8 links; a member takes >= 4 lanes, so <= 16
+                        // members per batch and 15 jumps reach all of them.  Codes >= 64 end the chain.
+                        // (the gathers run on every lane: a ds_bpermute does not see exec-masked lanes)
+                        const int J0 = min(link, LZH_WAVE);
+                        const int G1 = (int)lane_gather((uint32_t)J0, J0 & (LZH_WAVE - 1));
+                        const int J1 = J0 < LZH_WAVE ? G1 : LZH_WAVE;
+                        const int G2 = (int)lane_gather((uint32_t)J1, J1 & (LZH_WAVE - 1));
+                        const int J2 = J1 < LZH_WAVE ? G2 : LZH_WAVE;
+                        const int G3 = (int)lane_gather((uint32_t)J2, J2 & (LZH_WAVE - 1));
+                        const int J3 = J2 < LZH_WAVE ? G3 : LZH_WAVE;
+#endif
+                        LZ_CLK(10);                            // (stats: per-lane links)
                         // (links strictly increase, so the walks end)
                         for (;;) {
                             int fs;
+#if LZH_PARSE_LIFT
+                            {   // every lane lifts from sl to the furthest chain lane <= itself
+                                int x = sl, y;
+                                y = (int)lane_gather((uint32_t)J3, x); x = y <= lane ? y : x;
+                                y = (int)lane_gather((uint32_t)J2, x); x = y <= lane ? y : x;
+                                y = (int)lane_gather((uint32_t)J1, x); x = y <= lane ? y : x;
+                                y = (int)lane_gather((uint32_t)J0, x); x = y <= lane ? y : x;
+                                const uint64_t on = ballot(x == lane && lane >= sl);
+                                Mm |= on;
+                                sl = 63 - __builtin_clzll(on);           // the last member
+                                fs = rdlanei(link, sl);
+                            }
+#else
                             for (;;) {                                 // common case: plain links
                                 Mm |= 1ull << sl;
                                 fs = rdlanei(link, sl);
                                 if (fs >= LZH_WAVE) break;
                                 sl = fs;
                             }
+#endif
                             if (fs != 0x80) break;                     // the chain leaves the batch
                             int es;
                             if (rdlane((uint32_t)lng, sl)) {           // match runs past the window
@@ -866,6 +923,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                             sl = fs;
                         }
                         eL = rdlanei(e, sl);
+                        LZ_CLK(11);                            // (stats: the scalar walk)
                         // lanes strictly inside a member's match are not probed; ip-2 is inserted
                         const uint64_t mle = Mm & (below | (1ull << lane));
                         const int j = mle ? 63 - __builtin_clzll(mle) : lane;
@@ -1170,7 +1228,7 @@ constexpr int kSpan = 2048;             // LDS copy of a record group's input sp
 // (4 KiB of LDS per wave: the emission kernel runs at the full 8 waves per SIMD)
 // longest literal run the lane-parallel group layout takes (<= 269: one literal-length byte)
 #ifndef LZH_LZ4E_LITMAX
-#define LZH_LZ4E_LITMAX 64
+#define LZH_LZ4E_LITMAX 255   // (64 -> 255: emit 1.28 -> 1.21 ms per GiB of text, profiles/r03_c/ab.txt)
 #endif
 
 __device__ __forceinline__ int wave_max(int v) {
