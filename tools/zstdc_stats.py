@@ -1,0 +1,33 @@
+"""tools/zstdc_stats.py -- event counters and phase clocks of the zstd match finder (fast_block2).
+Needs a -DLZH_ZSTDC_STATS=1 build: tools/exp_build.sh zst "-DLZH_ZSTDC_STATS=1", then
+LZH_LIB=build/exp/zst/liblzbench_hip.so python tools/zstdc_stats.py [corpus] [chunk_kib] [mib]"""
+import ctypes as C, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch, lzbench_amd as L
+lib = L.lib()
+f = lib.lzh_debug_zstdc_stats
+f.restype = C.c_int
+f.argtypes = [C.c_void_p, C.c_int]
+corpus = sys.argv[1] if len(sys.argv) > 1 else "mixed"
+chunk = int(sys.argv[2] if len(sys.argv) > 2 else 128) << 10
+n = int(sys.argv[3] if len(sys.argv) > 3 else 256) << 20
+host = L.datagen(corpus, n, seed=12345)
+d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda"); d_in[:n].copy_(torch.from_numpy(host))
+dc = L.DeviceCodec("zstd", n, chunk, level=1)
+dc.compress(d_in)
+torch.cuda.synchronize()
+buf = (C.c_ulonglong * 24)()
+assert f(buf, 1) == 0
+dc.compress_kernel_only(d_in)
+torch.cuda.synchronize()
+assert f(buf, 0) == 0
+v = list(buf)
+blocks = max(v[15], 1)
+names = {9: "batches", 10: "pside_global", 11: "fwd_slow", 12: "bwd_slow", 13: "sequences"}
+print(corpus, chunk >> 10, "KiB per block:", {k: round(v[i] / blocks, 1) for i, k in names.items()})
+ph = {0: "schedule", 1: "pside+hash", 2: "table+groups", 3: "window_wait", 4: "eval+restore", 5: "match_finish",
+      6: "literals+record", 7: "fills", 8: "loop/other", 14: "rep_loop", 16: "fills_loads", 17: "fills_puts", 18: "lit_copy"}
+tot = sum(v[i] for i in ph) or 1
+print("  clocks/block %.0f, per sequence %.0f:" % (tot / blocks, tot / max(v[13], 1)),
+      {k: "%.1f%%" % (100 * v[i] / tot) for i, k in ph.items()})
