@@ -124,6 +124,9 @@ struct LdsTab {
     LDSA uint32_t* t;
     __device__ __forceinline__ uint32_t get(uint32_t h) const { return ((volatile LDSA uint32_t*)t)[h]; }
     __device__ __forceinline__ void put(uint32_t h, uint32_t v) const { ((volatile LDSA uint32_t*)t)[h] = v; }
+    __device__ __forceinline__ void claim(uint32_t h, uint32_t v) const { put(h, v); }
+    __device__ __forceinline__ uint32_t back(uint32_t h) const { return get(h); }
+    static constexpr uint32_t kBackMask = ~0u;
     __device__ __forceinline__ void fence() const { wave_lds_fence(); }
 };
 // the same table as 16-bit low halves + 8-bit high bytes (3 bytes an entry: 6 waves per CU instead of
@@ -139,14 +142,45 @@ struct LdsTab24 {
         ((volatile LDSA uint16_t*)lo)[h] = (uint16_t)v;
         ((volatile LDSA uint8_t*)hi)[h] = (uint8_t)(v >> 16);
     }
+    __device__ __forceinline__ void claim(uint32_t h, uint32_t v) const { put(h, v); }
+    __device__ __forceinline__ uint32_t back(uint32_t h) const { return get(h); }
+    static constexpr uint32_t kBackMask = ~0u;
     __device__ __forceinline__ void fence() const { wave_lds_fence(); }
 };
+// 17-bit entries for frames of at most 128 KiB (positions + 1 < 2^17): 16-bit low halves + a bitmap
+// of bit 16 -- 17 KiB at hashLog 13, 9 waves per CU instead of 6.  A put writes the low half and
+// clears / sets the bit with LDS atomics (lanes of one bitmap dword touch different bits).  When lanes
+// of a batch claim the same slot, the hardware's low-half winner and the bit may come from different
+// lanes; such slots are rewritten by a single lane before anything reads them (the batch's restore),
+// and a claim's readback compares low halves only (positions of a batch differ by < 2^16).
+struct LdsTab17 {
+    LDSA uint16_t* lo;
+    LDSA uint32_t* bm;
+    __device__ __forceinline__ uint32_t get(uint32_t h) const {
+        const uint32_t w = ((volatile LDSA uint32_t*)bm)[h >> 5];
+        return (uint32_t)((volatile LDSA uint16_t*)lo)[h] | (((w >> (h & 31u)) & 1u) << 16);
+    }
+    __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
+        ((volatile LDSA uint16_t*)lo)[h] = (uint16_t)v;
+        __atomic_fetch_and(bm + (h >> 5), ~(1u << (h & 31u)), __ATOMIC_RELAXED);
+        __atomic_fetch_or(bm + (h >> 5), ((v >> 16) & 1u) << (h & 31u), __ATOMIC_RELAXED);
+    }
+    // the claim writes whole entries (an uncontested slot keeps it); its readback reads the low half
+    __device__ __forceinline__ void claim(uint32_t h, uint32_t v) const { put(h, v); }
+    __device__ __forceinline__ uint32_t back(uint32_t h) const { return ((volatile LDSA uint16_t*)lo)[h]; }
+    static constexpr uint32_t kBackMask = 0xffffu;
+    __device__ __forceinline__ void fence() const { wave_lds_fence(); }
+};
+
 struct GlbTab {
     rsrc_t r;
     __device__ __forceinline__ uint32_t get(uint32_t h) const {
         return __builtin_amdgcn_raw_buffer_load_b32(r, (int)(h * 4), 0, 1);   // (glc: bypass L1)
     }
     __device__ __forceinline__ void put(uint32_t h, uint32_t v) const { st_b32(r, (int)(h * 4), v); }
+    __device__ __forceinline__ void claim(uint32_t h, uint32_t v) const { put(h, v); }
+    __device__ __forceinline__ uint32_t back(uint32_t h) const { return get(h); }
+    static constexpr uint32_t kBackMask = ~0u;
     __device__ __forceinline__ void fence() const { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 };
 
@@ -267,10 +301,10 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             uint32_t old = 0, back = 0;
             if (valid) old = T.get(h);
             T.fence();
-            if (valid) T.put(h, (uint32_t)q + 1);
+            if (valid) T.claim(h, (uint32_t)q + 1);
             T.fence();
-            if (valid) back = T.get(h);
-            const uint64_t losers = ballot(valid && back != (uint32_t)q + 1);
+            if (valid) back = T.back(h);
+            const uint64_t losers = ballot(valid && back != (((uint32_t)q + 1) & Tab::kBackMask));
             uint64_t grp = 1ull << lane;
             int prev = -1;
             if (losers) {
@@ -280,7 +314,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 const int span = rdlanei(Aj, 62) + 2 - A0;
                 int nbits = 1;
                 while ((1 << nbits) < span) nbits++;
-                const uint32_t wr = back - 1u - (uint32_t)A0;
+                const uint32_t wr = (back - 1u - (uint32_t)A0) & Tab::kBackMask;
                 uint64_t eq = vmask;
                 for (int b = 0; b < nbits; b++) {
                     const bool wb = (wr >> b) & 1u;
@@ -414,6 +448,9 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
 //     (<= 20 bytes) come out of the same round trip as the compare (zstd_fast.c:196-283);
 //   * the table fills and the immediate repcode check after a match (zstd_fast.c:296-311) share a
 //     round trip with the ring's refill for the new front.
+#ifndef LZH_ZSTD_TAB17
+#define LZH_ZSTD_TAB17 1   // 17-bit hash-table entries (LdsTab17) for chunks <= 128 KiB
+#endif
 #ifndef LZH_ZSTD_RING
 #define LZH_ZSTD_RING 0   // (measured slower: 1 GiB mixed -b128 compress 100.7 -> 108.7 ms, text 209 -> 222 ms, profiles/r03_z)
 #endif
@@ -661,10 +698,10 @@ __device__ void fast_block2(const Tab& T, ZRing& Rg, const Bytes& in, const ZPar
             uint32_t old = 0, back = 0;
             if (valid) old = T.get(h);
             T.fence();
-            if (valid) T.put(h, (uint32_t)q + 1);
+            if (valid) T.claim(h, (uint32_t)q + 1);
             T.fence();
-            if (valid) back = T.get(h);
-            const uint64_t losers = ballot(valid && back != (uint32_t)q + 1);
+            if (valid) back = T.back(h);
+            const uint64_t losers = ballot(valid && back != (((uint32_t)q + 1) & Tab::kBackMask));
             uint64_t grp = 1ull << lane;
             int prev = -1;
             if (losers) {
@@ -674,7 +711,7 @@ __device__ void fast_block2(const Tab& T, ZRing& Rg, const Bytes& in, const ZPar
                 const int span = rdlanei(Aj, 62) + 2 - A0;
                 int nbits = 1;
                 while ((1 << nbits) < span) nbits++;
-                const uint32_t wr = back - 1u - (uint32_t)A0;
+                const uint32_t wr = (back - 1u - (uint32_t)A0) & Tab::kBackMask;
                 uint64_t eq = vmask;
                 for (int b = 0; b < nbits; b++) {
                     const bool wb = (wr >> b) & 1u;
@@ -867,7 +904,15 @@ lzh_zstd_match_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable,
     const uint32_t lds_table_bytes = lds_arg & 0x7fffffffu;
     const bool ring = (lds_arg >> 31) != 0;
     ZRing Rg{(LDSA uint32_t*)((LDSA uint8_t*)zlds + ((lds_table_bytes + 15u) & ~15u)), in_b.sh, 0, 0, 0};
-    if (chunk_size < (16u << 20) && 3u * nent <= lds_table_bytes) {
+    const uint32_t bmb = max(nent / 8u, 4u);            // LdsTab17 bitmap bytes
+    if (LZH_ZSTD_TAB17 && chunk_size <= 131072u && nblocks == 1 && 2u * nent + bmb <= lds_table_bytes) {
+        // (single-block frames: the table starts empty and is not saved)
+        LdsTab17 T{(LDSA uint16_t*)zlds, (LDSA uint32_t*)((LDSA uint8_t*)zlds + 2 * nent)};
+        for (uint32_t i = lane; i < (2u * nent + bmb) / 4u; i += 64) ((volatile LDSA uint32_t*)zlds)[i] = 0u;
+        T.fence();
+        if (LZH_ZSTD_RING && ring) fast_block2(T, Rg, in_b, P, bs, be, rep, O, lane);
+        else fast_block(T, in_b, P, bs, be, rep, O, lane);
+    } else if (chunk_size < (16u << 20) && 3u * nent <= lds_table_bytes) {
         LdsTab24 T{(LDSA uint16_t*)zlds, (LDSA uint8_t*)zlds + 2 * nent};
         rsrc_t save = make_rsrc(fs + tab_off, tbytes);
         for (uint32_t i = lane; i < nent; i += 64) T.put(i, k == 0 ? 0u : ld_b32(save, (int)(i * 4)));
@@ -1934,8 +1979,11 @@ hipError_t lzh_launch_zstd_compress(const uint8_t* in, uint64_t n_total, uint64_
 #define LZH_ZSTD_LDS_MAX 65536u   // largest hash table kept in LDS (else in the frame's scratch, via L2)
 #endif
     // 3-byte entries (LdsTab24) below 16 MiB chunks, else 4-byte ones
+    // (17-bit entries, LdsTab17, for chunks of at most 128 KiB)
     const uint32_t ebytes = chunk_size < (16u << 20) ? 3u : 4u;
-    const uint32_t lds_tab = (4u << PF.hlog) <= (uint32_t)LZH_ZSTD_LDS_MAX ? (ebytes << PF.hlog) : 0u;
+    const uint32_t t17 = (2u << PF.hlog) + std::max((1u << PF.hlog) / 8u, 4u);
+    const uint32_t lds_tab = (4u << PF.hlog) > (uint32_t)LZH_ZSTD_LDS_MAX ? 0u
+                             : (LZH_ZSTD_TAB17 && chunk_size <= 131072u) ? ((t17 + 15u) & ~15u) : (ebytes << PF.hlog);
     // (the ring only where table + ring fit the 64 KiB a launch gets without an attribute)
     const bool ring = LZH_ZSTD_RING && ((lds_tab + 15u) & ~15u) + (uint32_t)zc::kZRingLds <= 65536u;
     const uint32_t lds_all = ring ? ((lds_tab + 15u) & ~15u) + (uint32_t)zc::kZRingLds : lds_tab;
