@@ -28,6 +28,11 @@ __device__ unsigned long long lzh_dec_stats_buf[16];
 #define DST(i, v) do {} while (0)
 #define DCLK(t) do {} while (0)
 #endif
+#ifdef LZH_ISA_MARKS
+#define DMARK(i) asm volatile("; DMARK " #i ::: "memory")
+#else
+#define DMARK(i) ((void)0)
+#endif
 
 namespace {
 
@@ -501,6 +506,7 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
     Tail lt;
     Tail& t = kDefer ? *tp : lt;
     for (int pb = 0; pb < total; pb += kP) {
+        DMARK(10);
         ((volatile LDSA uint16_t*)mark)[lane] = 0xffffu;
         wave_lds_fence();
         const bool mine = kmem && excl >= pb && excl < pb + kP;
@@ -527,6 +533,7 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
             ms1 = (int)lane_gather((uint32_t)m_msrc, k1);
             of1 = (int)lane_gather((uint32_t)off, k1);
         }
+        DMARK(11);
         const int pbase = op + pb;
         const int thr = pbase + kP - SinkType::kWin;               // sources below: overwritten in the window
         const int ob0 = pb + 2 * lane, ob1 = ob0 + 1;
@@ -534,6 +541,7 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
         bool done0, done1, far0, far1;
         const uint32_t v0 = owned_byte(w, O, op, pbase, thr, ob0, total, le0, ls0, ms0, of0, src0, done0, far0);
         const uint32_t v1 = owned_byte(w, O, op, pbase, thr, ob1, total, le1, ls1, ms1, of1, src1, done1, far1);
+        DMARK(12);
         t.g0 = t.g1 = 0;
         const bool anyfar = ballot(far0 || far1) != 0;
         if (anyfar) {   // far sources were flushed long ago: their stores must be done
@@ -549,7 +557,9 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
             t.live = true;
             return;
         }
+        DMARK(13);
         pass_tail(O, t, lane);
+        DMARK(14);
     }
 }
 
@@ -603,6 +613,7 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
     tl.live = false;
     for (int guard = 0; guard <= cs; guard++) {
         DCLK(t0);
+        DMARK(0);
         ip = unii(ip); op = unii(op);
         O.flushed = unii(O.flushed); O.ringlo = unii(O.ringlo);
         if (!w.covers(ip, ip + 2 * LZH_WAVE)) w.load(ip, lane);
@@ -621,7 +632,9 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
         const bool cplx = !inwin || (ln == 15 && b1 == 255) || (mc == 15 && b2 == 255);
         const int link = cplx ? 255 : pe - ip;
         // ---- the real chain from lane 0
+        DMARK(1);
         const uint64_t M = chain_members(link, lane);
+        DMARK(2);
         // ---- acceptance rules per member (as lz4_one); the chain ends before the first failure
         const bool mem = lane_on(M);
         const int L = mem ? lit + ml : 0;
@@ -647,6 +660,7 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
         const int total = rdlanei(incl, lastk);
         const int ip_next = ip + rdlanei(pe - ip, lastk);
         DCLK(t1);
+        DMARK(3);
 #ifndef LZH_ABL_NOEMIT
         emit_group<LZH_DEC_DEFER>(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)ml << 16),
                          (uint32_t)(p1 - ip), off, lane, &tl);

@@ -977,9 +977,9 @@ struct Lds {
     uint8_t hdr[264];           // Huffman table header
     uint8_t symAt[512];         // FSE spread workspace
     uint32_t cumul[64];
-    uint32_t sq[64 * 2];        // 64 sequences staged for the single-lane encoder
+    uint32_t sq[64 * 3];        // a group's (nbBits << 16 | bits) per state chain
     int32_t qs[2 * 300];        // quick-sort task stack
-    uint32_t stage[40];         // bit staging window
+    uint32_t stage[192];        // bit staging window (64 sequences of <= 90 bits)
     uint32_t misc[16];
 };
 
@@ -1691,7 +1691,7 @@ __device__ __forceinline__ void seq_unpack(uint32_t lo, uint32_t hi, uint32_t& l
 
 // sequences section after the nbSeq header (zstd_compress.c:2645-2689, ZSTD_buildSequencesStatistics,
 // zstd_compress_sequences.c:157-382); att[pos..); returns its size, 0 = emit the block raw
-__device__ int encode_sequences(LDSA Lds& L, const Bytes& att, int pos, rsrc_t seq, int ns, int lane) {
+__device__ int encode_sequences(LDSA Lds& L, const Bytes& att, const Bytes& tmp, int pos, rsrc_t seq, int ns, int lane) {
     for (int i = lane; i < 3 * 64; i += 64) (&L.cnt3[0][0])[i] = 0;
     wave_lds_fence();
     for (int i = lane; i < ns; i += 64) {
@@ -1758,45 +1758,112 @@ __device__ int encode_sequences(LDSA Lds& L, const Bytes& att, int pos, rsrc_t s
     wave_lds_fence();
     op = (int)uni(L.misc[1]);
     const int lastCount = (int)uni(L.misc[2]);
-    // ZSTD_encodeSequences_body: the last sequence first, 64 sequences staged in LDS at a time
-    BitW<Bytes> b{att, op, 0, 0};
-    uint32_t sML = 0, sOF = 0, sLL = 0;
+    // ZSTD_encodeSequences_body (zstd_compress_sequences.c:268-382), the last sequence first, 64
+    // sequences at a time.  The three FSE state chains (offset, match length, literal length) are
+    // independent: lanes 0 / 1 / 2 run one each (one dependent LDS lookup per sequence), leaving every
+    // sequence's (nbBits, bits) per table in LDS; then every lane places its sequence's six fields --
+    // OF / ML / LL state bits, LL / ML / OF extra bits, in the reference's order -- at bit offsets from
+    // a wave suffix sum, OR-ed into an LDS window of dwords that leaves for the aligned scratch `tmp`.
+    // The stream is copied behind the table descriptions at the end.
+    const int tb = lane == 0 ? 1 : (lane == 1 ? 2 : 0);     // chain lane -> table (OF, ML, LL)
+    uint32_t state = 0;
+    uint32_t bitpos = 0;          // stream bits written so far
+    uint32_t cw = 0;              // the open (partial) dword at bitpos >> 5
     for (int g = ns; g > 0; g -= 64) {
         const int g0 = g >= 64 ? g - 64 : 0, gn = g - g0;
-        if (lane < gn) { L.sq[2 * lane] = ld_b32(seq, 8 * (g0 + lane)); L.sq[2 * lane + 1] = ld_b32(seq, 8 * (g0 + lane) + 4); }
-        wave_lds_fence();
-        if (lane == 0) {
-            for (int i = gn - 1; i >= 0; i--) {
-                const int nidx = g0 + i;
-                uint32_t ll, ml, off;
-                seq_unpack(L.sq[2 * i], L.sq[2 * i + 1], ll, ml, off);
-                const uint32_t llc = ll_code(ll), ofc = hb32(off), mlc = ml_code(ml - 3);
-                if (nidx == ns - 1) {
-                    sML = fse_init_state(L.fse[2], mlc);
-                    sOF = fse_init_state(L.fse[1], ofc);
-                    sLL = fse_init_state(L.fse[0], llc);
-                } else {
-                    fse_encode(b, L.fse[1], sOF, ofc);
-                    fse_encode(b, L.fse[2], sML, mlc);
-                    fse_encode(b, L.fse[0], sLL, llc);
+        const int i = lane;
+        uint32_t ll = 0, ml = 3, off = 0;
+        if (i < gn) seq_unpack(ld_b32(seq, 8 * (g0 + i)), ld_b32(seq, 8 * (g0 + i) + 4), ll, ml, off);
+        const uint32_t llc = ll_code(ll), ofc = hb32(max(off, 1u)), mlc = ml_code(ml - 3);
+        const uint32_t dOF = L.fse[1].dnb[ofc], dML = L.fse[2].dnb[mlc], dLL = L.fse[0].dnb[llc];
+        const int32_t fOF = L.fse[1].dfs[ofc], fML = L.fse[2].dfs[mlc], fLL = L.fse[0].dfs[llc];
+        // ---- state chains (lanes 0..2), sequences gn-1 .. 0 of the group.  Every lane runs the loop
+        // (the others on a copy of lane 2's table, results dropped): inside a lane-divergent branch the
+        // compiler may sink the per-sequence operands of the readlanes into it, leaving the inactive
+        // lanes' values undefined.
+        {
+            const LDSA uint16_t* st = L.fse[tb].st;
+            for (int k = gn - 1; k >= 0; k--) {
+                const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)dOF, k), a1 = (uint32_t)__builtin_amdgcn_readlane((int)dML, k),
+                               a2 = (uint32_t)__builtin_amdgcn_readlane((int)dLL, k);
+                const int32_t b0 = __builtin_amdgcn_readlane(fOF, k), b1 = __builtin_amdgcn_readlane(fML, k),
+                              b2 = __builtin_amdgcn_readlane(fLL, k);
+                const uint32_t dn = lane == 0 ? a0 : (lane == 1 ? a1 : a2);
+                const int32_t df = lane == 0 ? b0 : (lane == 1 ? b1 : b2);
+                uint32_t outw = 0;
+                if (g0 + k == ns - 1) {                       // FSE_initCState2
+                    const uint32_t nbo = (dn + (1u << 15)) >> 16;
+                    const uint32_t v = (nbo << 16) - dn;
+                    state = st[(int32_t)(v >> nbo) + df];
+                } else {                                      // FSE_encodeSymbol
+                    const uint32_t nbo = (state + dn) >> 16;
+                    outw = (nbo << 16) | (state & ((1u << nbo) - 1u));
+                    state = st[(int32_t)(state >> nbo) + df];
                 }
-                b.add(ll, ll_bits(ll));
-                b.add(ml - 3, ml_bits(ml - 3));
-                b.add(off, ofc);
+                if (lane < 3) L.sq[3 * k + lane] = outw;
             }
         }
         wave_lds_fence();
+        // ---- fields of sequence i, its bit offset (the group is written from its last sequence down)
+        const uint32_t wOF = i < gn ? L.sq[3 * i] : 0u, wML = i < gn ? L.sq[3 * i + 1] : 0u, wLL = i < gn ? L.sq[3 * i + 2] : 0u;
+        const uint32_t nOF = wOF >> 16, nML = wML >> 16, nLL = wLL >> 16;
+        const uint32_t nll = i < gn ? ll_bits(ll) : 0u, nml = i < gn ? ml_bits(ml - 3) : 0u, nof = i < gn ? ofc : 0u;
+        const uint32_t T = nOF + nML + nLL + nll + nml + nof;
+        const uint32_t incl = wave_incl_scan(T, lane);
+        const uint32_t gbits = rdlane(incl, 63);
+        const uint32_t base = bitpos & ~31u;
+        uint32_t p = bitpos + (gbits - incl) - base;          // window-relative start of sequence i
+        const int nd = (int)((bitpos - base + gbits + 31) >> 5) + 1;
+        for (int d = lane; d < nd; d += 64) L.stage[d] = d == 0 ? cw : 0u;
+        wave_lds_fence();
+        auto put = [&](uint32_t v, uint32_t n) {
+            if (n) {
+                v &= n >= 32 ? ~0u : ((1u << n) - 1u);
+                const uint64_t x = (uint64_t)v << (p & 31u);
+                atomicOr((uint32_t*)&L.stage[p >> 5], (uint32_t)x);
+                if ((uint32_t)(x >> 32)) atomicOr((uint32_t*)&L.stage[(p >> 5) + 1], (uint32_t)(x >> 32));
+            }
+            p += n;
+        };
+        put(wOF & 0xffffu, nOF);
+        put(wML & 0xffffu, nML);
+        put(wLL & 0xffffu, nLL);
+        put(ll, nll);
+        put(ml - 3, nml);
+        put(off, nof);
+        wave_lds_fence();
+        const uint32_t end = bitpos + gbits;
+        const int full = (int)((end - base) >> 5);            // complete dwords of the window
+        for (int d = lane; d < full; d += 64) st_b32(tmp.r, (int)(base >> 3) + 4 * d, L.stage[d]);
+        cw = L.stage[full];
+        bitpos = end;
+        wave_lds_fence();
     }
+    // FSE_flushCState x 3 (ML, OF, LL), BIT_closeCStream (the end mark), into the open dword
     int res = 0;
-    if (lane == 0) {
-        b.add(sML, L.fse[2].tlog);
-        b.add(sOF, L.fse[1].tlog);
-        b.add(sLL, L.fse[0].tlog);
-        const int end = b.close();
-        const int bs = end - op;
-        res = (lastCount && lastCount + bs < 4) ? 0 : end - pos;
+    {
+        const uint32_t sML = (uint32_t)__builtin_amdgcn_readlane((int)state, 1), sOF = (uint32_t)__builtin_amdgcn_readlane((int)state, 0),
+                       sLL = (uint32_t)__builtin_amdgcn_readlane((int)state, 2);
+        uint64_t acc = cw;
+        uint32_t nb = bitpos & 31u;
+        const uint32_t base = bitpos & ~31u;
+        const uint32_t tl2 = L.fse[2].tlog, tl1 = L.fse[1].tlog, tl0 = L.fse[0].tlog;
+        // (at most 31 + 3 x 9 + 1 = 59 bits: one u64)
+        acc |= (uint64_t)(sML & ((1u << tl2) - 1u)) << nb; nb += tl2;
+        acc |= (uint64_t)(sOF & ((1u << tl1) - 1u)) << nb; nb += tl1;
+        acc |= (uint64_t)(sLL & ((1u << tl0) - 1u)) << nb; nb += tl0;
+        acc |= 1ull << nb; nb += 1;
+        if (lane == 0) {
+            st_b32(tmp.r, (int)(base >> 3), (uint32_t)acc);
+            if (nb > 32) st_b32(tmp.r, (int)(base >> 3) + 4, (uint32_t)(acc >> 32));
+        }
+        const int bs = (int)((base + nb + 7) >> 3);          // stream bytes
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        copy_span(tmp, 0, att, op, bs, lane, 64);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        res = (lastCount && lastCount + bs < 4) ? 0 : op + bs - pos;
     }
-    return (int)rdlane((uint32_t)res, 0);
+    return res;
 }
 
 }  // namespace ze
@@ -1882,7 +1949,7 @@ lzh_zstd_entropy_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readabl
         }
         o += ns < 128 ? 1 : (ns < 0x7F00 ? 2 : 3);
         if (ns) {
-            const int sz = ze::encode_sequences(L, att, o, make_rsrc(fs + seq_off, (uint32_t)(lit_off - seq_off)), ns, lane);
+            const int sz = ze::encode_sequences(L, att, tmp, o, make_rsrc(fs + seq_off, (uint32_t)(lit_off - seq_off)), ns, lane);
             csize = sz ? o + sz : 0;
         } else {
             csize = o;
