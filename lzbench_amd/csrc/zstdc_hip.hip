@@ -111,6 +111,10 @@ __device__ __forceinline__ uint32_t zhash(uint64_t v, uint32_t hlog, uint32_t ml
     }
 }
 
+// the hash with the minimum match length fixed at compile time (kMls 4..7) or read from P (kMls 0)
+template <int kMls>
+__device__ __forceinline__ uint32_t zh(uint64_t v, uint32_t hlog, uint32_t mls) { return zhash(v, hlog, kMls ? (uint32_t)kMls : mls); }
+
 // 8 bytes at pos (little endian) from aligned dwords
 __device__ __forceinline__ uint64_t ld64(const Bytes& b, int pos) {
     const int X = pos + b.sh, a = X & ~3;
@@ -236,15 +240,15 @@ __device__ __forceinline__ void pair_step(int& A, int& D, int& s, int& nx) {
     if (A + s >= nx) { s++; nx += 128; }
 }
 
-template <class Tab>
+template <int kMls = 0, class Tab>
 __device__ void tab_put_pos(const Tab& T, const Bytes& in, int pos, const ZParams& P) {
-    const uint32_t h = zhash(ld64(in, pos), P.hlog, P.mls);
+    const uint32_t h = zh<kMls>(ld64(in, pos), P.hlog, P.mls);
     T.put(h, (uint32_t)pos + 1);
 }
 
 // The parse of one block [bs, be) of a frame (positions relative to the frame start; table
 // entries hold position + 1, 0 = empty).  Mirrors zstd_fast.c:92-315.
-template <class Tab>
+template <int kMls = 0, class Tab>
 __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int bs, int be, uint32_t rep[2],
                            SeqOut& O, int lane) {
     const int W = 1 << P.wlog;
@@ -296,7 +300,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 w8 = ld64(in, q);
                 if (!half && r1 > 0) { rv = in.w32(Aj + Dj); rm = in.w32(Aj + Dj - (int)r1); }
             }
-            const uint32_t h = zhash(w8, P.hlog, P.mls);
+            const uint32_t h = zh<kMls>(w8, P.hlog, P.mls);
             // ---- table read, claim, read back
             uint32_t old = 0, back = 0;
             if (valid) old = T.get(h);
@@ -412,10 +416,10 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             const uint64_t h1 = ld64(in, ip1), h2 = ld64(in, cur0 + 2), h3 = ld64(in, ip - 2);
             const uint32_t c0 = in.w32(ip), c1 = in.w32(ip - (int)r2);
             if (lane == 0) {
-                if (ip1 < ip) T.put(zhash(h1, P.hlog, P.mls), (uint32_t)ip1 + 1);
+                if (ip1 < ip) T.put(zh<kMls>(h1, P.hlog, P.mls), (uint32_t)ip1 + 1);
                 if (ip <= ilimit) {
-                    T.put(zhash(h2, P.hlog, P.mls), (uint32_t)cur0 + 3);
-                    T.put(zhash(h3, P.hlog, P.mls), (uint32_t)ip - 1);
+                    T.put(zh<kMls>(h2, P.hlog, P.mls), (uint32_t)cur0 + 3);
+                    T.put(zh<kMls>(h3, P.hlog, P.mls), (uint32_t)ip - 1);
                 }
             }
             T.fence();
@@ -423,7 +427,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             while (more) {
                 const int rl = 4 + count_fwd(in, ip + 4, ip + 4 - (int)r2, be - (ip + 4), lane);
                 const uint32_t t = r2; r2 = r1; r1 = t;
-                if (lane == 0) tab_put_pos(T, in, ip, P);
+                if (lane == 0) tab_put_pos<kMls>(T, in, ip, P);
                 T.fence();
                 O.put(lane, 0, 1, (uint32_t)rl);
                 ip += rl;
@@ -911,6 +915,8 @@ lzh_zstd_match_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable,
         for (uint32_t i = lane; i < (2u * nent + bmb) / 4u; i += 64) ((volatile LDSA uint32_t*)zlds)[i] = 0u;
         T.fence();
         if (LZH_ZSTD_RING && ring) fast_block2(T, Rg, in_b, P, bs, be, rep, O, lane);
+        else if (P.mls == 6) fast_block<6>(T, in_b, P, bs, be, rep, O, lane);   // (hash fixed at compile time)
+        else if (P.mls == 5) fast_block<5>(T, in_b, P, bs, be, rep, O, lane);
         else fast_block(T, in_b, P, bs, be, rep, O, lane);
     } else if (chunk_size < (16u << 20) && 3u * nent <= lds_table_bytes) {
         LdsTab24 T{(LDSA uint16_t*)zlds, (LDSA uint8_t*)zlds + 2 * nent};
