@@ -111,6 +111,11 @@ __device__ __forceinline__ uint32_t zhash(uint64_t v, uint32_t hlog, uint32_t ml
     }
 }
 
+#ifdef LZH_ISA_MARKS
+#define ZMK(i) asm volatile("; ZMK " #i ::: "memory")
+#else
+#define ZMK(i) ((void)0)
+#endif
 // the hash with the minimum match length fixed at compile time (kMls 4..7) or read from P (kMls 0)
 template <int kMls>
 __device__ __forceinline__ uint32_t zh(uint64_t v, uint32_t hlog, uint32_t mls) { return zhash(v, hlog, kMls ? (uint32_t)kMls : mls); }
@@ -248,6 +253,23 @@ __device__ void tab_put_pos(const Tab& T, const Bytes& in, int pos, const ZParam
 
 // The parse of one block [bs, be) of a frame (positions relative to the frame start; table
 // entries hold position + 1, 0 = empty).  Mirrors zstd_fast.c:92-315.
+// dst[d0, d0+len) = src[s0, s0+len) for one wave: runs of up to 256 bytes load everything first
+// (head bytes, one dword per lane, tail bytes; positions clamped, nothing predicated) and store after
+// one wait; longer runs take copy_span
+__device__ __forceinline__ void lit_copy(const Bytes& src, int s0, const Bytes& dst, int d0, int len, int lane) {
+    if (len <= 0) return;
+    if (len > 4 * LZH_WAVE) { copy_span(src, s0, dst, d0, len, lane, LZH_WAVE); return; }
+    const int head = min(len, (4 - ((d0 + dst.sh) & 3)) & 3);
+    const int nd = (len - head) >> 2, t0 = head + 4 * nd;
+    const bool hl = lane < head, dl = lane < nd, tl = lane < len - t0;
+    const uint32_t hb = src.b(s0 + (hl ? lane : 0));
+    const uint32_t w = src.w32(s0 + (dl ? head + 4 * lane : 0));
+    const uint32_t tb = src.b(s0 + (tl ? t0 + lane : 0));
+    if (hl) dst.st8(d0 + lane, hb);
+    if (dl) dst.st32_aligned(d0 + head + 4 * lane, w);
+    if (tl) dst.st8(d0 + t0 + lane, tb);
+}
+
 template <int kMls = 0, class Tab>
 __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int bs, int be, uint32_t rep[2],
                            SeqOut& O, int lane) {
@@ -273,6 +295,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
         int eA = 0, eD = 0;
         bool ended = false;
         for (;;) {
+            ZMK(0);
             // ---- probe schedule of the batch: pair j of lane (A_j, D_j), and the state after 32 pairs
             int Aj, Dj;
             int A32, D32, s32, n32;
@@ -293,6 +316,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             const bool valid = j == 0 || Aj + 1 + Dj < ilimit;
             const uint64_t vmask = ballot(valid);
             const int q = Aj + half;
+            ZMK(1);
             // ---- P side, rep side
             uint64_t w8 = 0;
             uint32_t rv = 0, rm = 1;
@@ -301,6 +325,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 if (!half && r1 > 0) { rv = in.w32(Aj + Dj); rm = in.w32(Aj + Dj - (int)r1); }
             }
             const uint32_t h = zh<kMls>(w8, P.hlog, P.mls);
+            ZMK(2);
             // ---- table read, claim, read back
             uint32_t old = 0, back = 0;
             if (valid) old = T.get(h);
@@ -331,11 +356,13 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             }
             const int qprev = lane_gather((uint32_t)q, prev < 0 ? lane : prev);
             const uint32_t cand = prev >= 0 ? (uint32_t)qprev + 1 : old;
+            ZMK(3);
             // ---- candidate compare
             bool hit = false;
             if (valid && cand > (uint32_t)pstart) hit = in.w32((int)cand - 1) == (uint32_t)w8;
             const bool rhit = valid && !half && r1 > 0 && rv == rm;
             const uint64_t R = ballot(rhit), H = ballot(hit), E = R | H;
+            ZMK(4);
             const uint64_t committed = E ? (vmask & (ffs64(E) == 63 ? ~0ull : ((2ull << ffs64(E)) - 1ull))) : vmask;
             // ---- slots: the value the sequential order leaves
             if (valid) {
@@ -359,6 +386,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             A = A32; D = D32; s = s32; nx = n32;
         }
         if (ended) break;
+        ZMK(5);
         // ---- the match.  m0 / p0: its start and source before the backward extension; the bytes
         // of the backward and forward compares and the literal run [anchor, m0) are loaded in one
         // round trip (the forward count from m0 + 4 does not depend on the backward extension; the
@@ -385,10 +413,12 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
         }
         const int fmax = be - (m0 + 4);
         const bool bl = lane < bmax, fl = 4 * lane < fmax;
-        const uint32_t ba = bl ? in.b(m0 - 1 - lane) : 0u, bb = bl ? in.b(p0 - 1 - lane) : 0u;
-        const uint32_t fa = fl ? ld_u32(in.r, m0 + 4 + 4 * lane + in.sh) : 0u,
-                       fb = fl ? ld_u32(in.r, p0 + 4 + 4 * lane + in.sh) : 0u;
-        copy_span(in, anchor, O.lits, O.nl, m0 - anchor, lane, LZH_WAVE);
+        // (every load unconditional at a clamped position, literal loads included: one wait for all --
+        // loads under lane-divergent branches each got their own wait inside the branch)
+        const uint32_t ba = in.b(bl ? m0 - 1 - lane : m0), bb = in.b(bl ? p0 - 1 - lane : m0);
+        const uint32_t fa = ld_u32(in.r, (fl ? m0 + 4 + 4 * lane : m0) + in.sh),
+                       fb = ld_u32(in.r, (fl ? p0 + 4 + 4 * lane : m0) + in.sh);
+        lit_copy(in, anchor, O.lits, O.nl, m0 - anchor, lane);
         int bk;
         {
             const uint64_t m = ballot(!bl || ba != bb);
@@ -406,6 +436,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             if (m) fw = 4 * ffs64(m) + (int)rdlane((uint32_t)eq, ffs64(m));
             else fw = fmax <= 256 ? max(fmax, 0) : 256 + count_fwd(in, m0 + 4 + 256, p0 + 4 + 256, fmax - 256, lane);
         }
+        ZMK(6);
         const int mstart = m0 - bk;
         const int len = 4 + bk + fw;
         O.nl += mstart - anchor;
