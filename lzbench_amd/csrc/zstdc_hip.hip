@@ -318,12 +318,9 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             const int q = Aj + half;
             ZMK(1);
             // ---- P side, rep side
-            uint64_t w8 = 0;
-            uint32_t rv = 0, rm = 1;
-            if (valid) {
-                w8 = ld64(in, q);
-                if (!half && r1 > 0) { rv = in.w32(Aj + Dj); rm = in.w32(Aj + Dj - (int)r1); }
-            }
+            const bool rok = valid && !half && r1 > 0;
+            const uint64_t w8 = ld64(in, valid ? q : A);                  // (branch-free: clamped positions)
+            const uint32_t rv = in.w32(rok ? Aj + Dj : A), rm = in.w32(rok ? Aj + Dj - (int)r1 : A);
             const uint32_t h = zh<kMls>(w8, P.hlog, P.mls);
             ZMK(2);
             // ---- table read, claim, read back
@@ -358,9 +355,9 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             const uint32_t cand = prev >= 0 ? (uint32_t)qprev + 1 : old;
             ZMK(3);
             // ---- candidate compare
-            bool hit = false;
-            if (valid && cand > (uint32_t)pstart) hit = in.w32((int)cand - 1) == (uint32_t)w8;
-            const bool rhit = valid && !half && r1 > 0 && rv == rm;
+            const bool cok = valid && cand > (uint32_t)pstart;
+            const bool hit = cok && in.w32(cok ? (int)cand - 1 : A) == (uint32_t)w8;
+            const bool rhit = rok && rv == rm;
             const uint64_t R = ballot(rhit), H = ballot(hit), E = R | H;
             ZMK(4);
             const uint64_t committed = E ? (vmask & (ffs64(E) == 63 ? ~0ull : ((2ull << ffs64(E)) - 1ull))) : vmask;
