@@ -513,20 +513,11 @@ struct ZRing {
     __device__ __forceinline__ uint32_t byte(int p) const {
         return ((volatile const LDSA uint8_t*)w)[(p + sh) & (kZRing - 1)];
     }
-    // LDS-DMA through inline asm: with the builtin the compiler orders every later LDS access after
-    // the DMA's LDS write (an s_waitcnt vmcnt(0) before the next ds_write / ds_read: a full memory
-    // round trip per refill).  Ring bytes are only read below `ready`, set after an explicit vmcnt(0).
-    __device__ __forceinline__ static void dma(rsrc_t r, LDSA uint32_t* dst, int voff) {
-        const uint32_t a = (uint32_t)(uintptr_t)dst;
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
-                     :: "s"(a), "v"(voff), "s"(r) : "memory", "m0");
-#pragma clang diagnostic pop
-    }
     __device__ __forceinline__ void refill(rsrc_t r, int lane) {
-        dma(r, w + ((fill & (kZRing - 1)) >> 2), fill + 4 * lane);
-        if ((fill & (kZRing - 1)) == 0 && lane < 8) dma(r, w + kZRing / 4, fill + 4 * lane);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (zlds_ptr_t)(w + ((fill & (kZRing - 1)) >> 2)), 4, fill + 4 * lane,
+                                                 0, 0, 0);
+        if ((fill & (kZRing - 1)) == 0 && lane < 8)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (zlds_ptr_t)(w + kZRing / 4), 4, fill + 4 * lane, 0, 0, 0);
         fill += 256;
     }
     // keep [front - 64, front + kZAhead) coming (landed at the next vmcnt wait); a front past the
@@ -618,11 +609,16 @@ __device__ __forceinline__ uint64_t rg64(const ZRing& R, const Bytes& in, int po
 #endif
 #if LZH_ZSTDC_STATS
 __device__ unsigned long long lzh_zstdc_stats_buf[24];
+// entropy-kernel phase clocks (indices 16..23): lane 0 adds the clocks since its previous mark
+#define ZEM(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); if (threadIdx.x == 0) atomicAdd(&lzh_zstdc_stats_buf[16 + (i)], (unsigned long long)(t_ - ze_last)); ze_last = t_; } while (0)
+#define ZEM_DECL uint64_t ze_last = __builtin_amdgcn_s_memtime()
 #define ZS(i, v) (zst[i] += (uint64_t)(v))
 #define ZT(i) do { asm volatile("; ZMARK " #i ::: "memory"); const uint64_t t_ = __builtin_amdgcn_s_memtime(); zst[i] += t_ - zlast; zlast = t_; } while (0)
 #else
 #define ZS(i, v) ((void)0)
 #define ZT(i) ((void)0)
+#define ZEM(i) ((void)0)
+#define ZEM_DECL ((void)0)
 #endif
 
 template <class Tab>
@@ -1628,6 +1624,7 @@ __device__ int lit_raw(const Bytes& att, const Bytes& lits, int n, int lane) {
 __device__ int compress_literals(LDSA Lds& L, const Bytes& att, const Bytes& tmp, const Bytes& lits, int n, int ns,
                                  const zc::ZParams& P, int prevRepeat, int& newTable, int lane) {
     newTable = 0;
+    ZEM_DECL;
     if (P.lit_off || n <= 63) return lit_raw(att, lits, n, lane);
     const int lh = 3 + (n >= 1024) + (n >= 16384);
     const int four = n >= 256;
@@ -1643,6 +1640,7 @@ __device__ int compress_literals(LDSA Lds& L, const Bytes& att, const Bytes& tmp
     }
     histo256(L.cnt, lits, 0, n, lane);
     histo_stats(L.cnt, lane, largest, maxs);
+    ZEM(0);   // literal histogram
     if (largest == (uint32_t)n) {                        // RLE literals
         const int fl = 1 + (n > 31) + (n > 4095);
         if (lane == 0) {
@@ -1675,6 +1673,7 @@ __device__ int compress_literals(LDSA Lds& L, const Bytes& att, const Bytes& tmp
         }
         wave_lds_fence();
         const int h = (int)uni(L.misc[0]);
+        ZEM(1);   // Huffman tree + table description
         if (h < 0) return lit_raw(att, lits, n, lane);
         bool useOld = false;
         if (repeat) {
@@ -1698,6 +1697,7 @@ __device__ int compress_literals(LDSA Lds& L, const Bytes& att, const Bytes& tmp
             htype = 2;
         }
     }
+    ZEM(2);   // Huffman streams
     if (c >= n - minGain) return lit_raw(att, lits, n, lane);
     newTable = htype == 2;
     if (lane == 0) {
@@ -1726,6 +1726,7 @@ __device__ __forceinline__ void seq_unpack(uint32_t lo, uint32_t hi, uint32_t& l
 // sequences section after the nbSeq header (zstd_compress.c:2645-2689, ZSTD_buildSequencesStatistics,
 // zstd_compress_sequences.c:157-382); att[pos..); returns its size, 0 = emit the block raw
 __device__ int encode_sequences(LDSA Lds& L, const Bytes& att, const Bytes& tmp, int pos, rsrc_t seq, int ns, int lane) {
+    ZEM_DECL;
     for (int i = lane; i < 3 * 64; i += 64) (&L.cnt3[0][0])[i] = 0;
     wave_lds_fence();
     for (int i = lane; i < ns; i += 64) {
@@ -1736,6 +1737,7 @@ __device__ int encode_sequences(LDSA Lds& L, const Bytes& att, const Bytes& tmp,
         atomicAdd((uint32_t*)&L.cnt3[2][ml_code(ml - 3)], 1u);
     }
     wave_lds_fence();
+    ZEM(3);   // sequence histograms
     // codes of the first and the last sequence (RLE tables, FSE count trick)
     uint32_t c0[3], cl[3];
     {
@@ -1799,6 +1801,7 @@ __device__ int encode_sequences(LDSA Lds& L, const Bytes& att, const Bytes& tmp,
     // OF / ML / LL state bits, LL / ML / OF extra bits, in the reference's order -- at bit offsets from
     // a wave suffix sum, OR-ed into an LDS window of dwords that leaves for the aligned scratch `tmp`.
     // The stream is copied behind the table descriptions at the end.
+    ZEM(4);   // FSE tables
     const int tb = lane == 0 ? 1 : (lane == 1 ? 2 : 0);     // chain lane -> table (OF, ML, LL)
     uint32_t state = 0;
     uint32_t bitpos = 0;          // stream bits written so far
@@ -1809,35 +1812,47 @@ __device__ int encode_sequences(LDSA Lds& L, const Bytes& att, const Bytes& tmp,
         uint32_t ll = 0, ml = 3, off = 0;
         if (i < gn) seq_unpack(ld_b32(seq, 8 * (g0 + i)), ld_b32(seq, 8 * (g0 + i) + 4), ll, ml, off);
         const uint32_t llc = ll_code(ll), ofc = hb32(max(off, 1u)), mlc = ml_code(ml - 3);
-        const uint32_t dOF = L.fse[1].dnb[ofc], dML = L.fse[2].dnb[mlc], dLL = L.fse[0].dnb[llc];
-        const int32_t fOF = L.fse[1].dfs[ofc], fML = L.fse[2].dfs[mlc], fLL = L.fse[0].dfs[llc];
-        // ---- state chains (lanes 0..2), sequences gn-1 .. 0 of the group.  Every lane runs the loop
-        // (the others on a copy of lane 2's table, results dropped): inside a lane-divergent branch the
-        // compiler may sink the per-sequence operands of the readlanes into it, leaving the inactive
-        // lanes' values undefined.
+        // per table and sequence (deltaNbBits, deltaFindState) into LDS (the Huffman sort stack, free
+        // by now): the chain lanes read them ahead of the state-dependent lookups
         {
-            const LDSA uint16_t* st = L.fse[tb].st;
-            for (int k = gn - 1; k >= 0; k--) {
-                const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)dOF, k), a1 = (uint32_t)__builtin_amdgcn_readlane((int)dML, k),
-                               a2 = (uint32_t)__builtin_amdgcn_readlane((int)dLL, k);
-                const int32_t b0 = __builtin_amdgcn_readlane(fOF, k), b1 = __builtin_amdgcn_readlane(fML, k),
-                              b2 = __builtin_amdgcn_readlane(fLL, k);
-                const uint32_t dn = lane == 0 ? a0 : (lane == 1 ? a1 : a2);
-                const int32_t df = lane == 0 ? b0 : (lane == 1 ? b1 : b2);
-                uint32_t outw = 0;
-                if (g0 + k == ns - 1) {                       // FSE_initCState2
-                    const uint32_t nbo = (dn + (1u << 15)) >> 16;
-                    const uint32_t v = (nbo << 16) - dn;
-                    state = st[(int32_t)(v >> nbo) + df];
-                } else {                                      // FSE_encodeSymbol
-                    const uint32_t nbo = (state + dn) >> 16;
-                    outw = (nbo << 16) | (state & ((1u << nbo) - 1u));
-                    state = st[(int32_t)(state >> nbo) + df];
-                }
-                if (lane < 3) L.sq[3 * k + lane] = outw;
-            }
+            LDSA uint32_t* cd = (LDSA uint32_t*)L.qs;
+            cd[2 * i] = L.fse[1].dnb[ofc];             cd[2 * i + 1] = (uint32_t)L.fse[1].dfs[ofc];
+            cd[128 + 2 * i] = L.fse[2].dnb[mlc];       cd[128 + 2 * i + 1] = (uint32_t)L.fse[2].dfs[mlc];
+            cd[256 + 2 * i] = L.fse[0].dnb[llc];       cd[256 + 2 * i + 1] = (uint32_t)L.fse[0].dfs[llc];
         }
         wave_lds_fence();
+        // ---- state chains (lanes 0..2: OF, ML, LL; the other lanes repeat lane 2's), sequences gn-1 .. 0
+        {
+            const LDSA uint16_t* st = L.fse[tb].st;
+            const LDSA uint32_t* cdt = (const LDSA uint32_t*)L.qs + 128 * (lane < 3 ? lane : 2);
+            int k = gn - 1;
+            if (g0 + k == ns - 1) {                           // FSE_initCState2 (no bits)
+                const uint32_t dn = cdt[2 * k];
+                const int32_t df = (int32_t)cdt[2 * k + 1];
+                const uint32_t nbo = (dn + (1u << 15)) >> 16;
+                const uint32_t v = (nbo << 16) - dn;
+                state = st[(int32_t)(v >> nbo) + df];
+                if (lane < 3) L.sq[3 * k + lane] = 0u;
+                k--;
+            }
+            auto step = [&](uint32_t dn, int32_t df, int kk) {   // FSE_encodeSymbol
+                const uint32_t nbo = (state + dn) >> 16;
+                const uint32_t outw = (nbo << 16) | (state & ((1u << nbo) - 1u));
+                state = st[(int32_t)(state >> nbo) + df];
+                if (lane < 3) L.sq[3 * kk + lane] = outw;
+            };
+            for (; k >= 3; k -= 4) {                          // (the table deltas of 4 steps read up front)
+                const uint32_t d0 = cdt[2 * k], f0 = cdt[2 * k + 1], d1 = cdt[2 * k - 2], f1 = cdt[2 * k - 1],
+                               d2 = cdt[2 * k - 4], f2 = cdt[2 * k - 3], d3 = cdt[2 * k - 6], f3 = cdt[2 * k - 5];
+                step(d0, (int32_t)f0, k);
+                step(d1, (int32_t)f1, k - 1);
+                step(d2, (int32_t)f2, k - 2);
+                step(d3, (int32_t)f3, k - 3);
+            }
+            for (; k >= 0; k--) step(cdt[2 * k], (int32_t)cdt[2 * k + 1], k);
+        }
+        wave_lds_fence();
+        ZEM(5);   // state chains
         // ---- fields of sequence i, its bit offset (the group is written from its last sequence down)
         const uint32_t wOF = i < gn ? L.sq[3 * i] : 0u, wML = i < gn ? L.sq[3 * i + 1] : 0u, wLL = i < gn ? L.sq[3 * i + 2] : 0u;
         const uint32_t nOF = wOF >> 16, nML = wML >> 16, nLL = wLL >> 16;
@@ -1872,6 +1887,7 @@ __device__ int encode_sequences(LDSA Lds& L, const Bytes& att, const Bytes& tmp,
         cw = L.stage[full];
         bitpos = end;
         wave_lds_fence();
+        ZEM(6);   // field packing
     }
     // FSE_flushCState x 3 (ML, OF, LL), BIT_closeCStream (the end mark), into the open dword
     int res = 0;
