@@ -1471,20 +1471,30 @@ __device__ int huf_write_table(LDSA Lds& L, uint32_t maxs, uint32_t tl) {
 }
 
 // ---- wave helpers
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
-    return v;
-}
+// wave-wide scans through DPP row shifts + row broadcasts (no LDS round trip per step)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
+    (void)lane;
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return (uint32_t)x;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    return __builtin_amdgcn_readlane(wave_incl_scan(v, 0), 63);
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {   // (unsigned: 0 is the identity of a shifted-out lane)
+    uint32_t x = v;
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(x, 63);
 }
 
 // histogram of bytes [a, a+n) of src (4-aligned buffer) into cnt (256 bins), all lanes: 16 bytes
