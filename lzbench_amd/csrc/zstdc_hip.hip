@@ -1543,10 +1543,15 @@ __device__ int huf_streams(LDSA Lds& L, const LDSA uint8_t* nb, const LDSA uint1
     const int seg = four ? (n + 3) / 4 : n;
     int sizes[4] = {0, 0, 0, 0};
     uint32_t tbits[4] = {0, 0, 0, 0};
+    // (4 symbols per lane: one unaligned dword of literals, bytes past the stream's end masked)
     for (int sidx = 0; sidx < nstreams; sidx++) {
         const int a = sidx * seg, e = (sidx == nstreams - 1) ? n : a + seg;
         uint32_t bits = 0;
-        for (int i = a + lane; i < e; i += 64) bits += nb[lits.b(i)];
+        for (int i = a + 4 * lane; i < e; i += 256) {
+            const uint32_t w = lits.w32(i);
+#pragma unroll
+            for (int k = 0; k < 4; k++) bits += i + k < e ? (uint32_t)nb[(w >> (8 * k)) & 0xffu] : 0u;
+        }
         bits = wave_sum(bits);
         tbits[sidx] = bits;
         sizes[sidx] = (int)((bits + 8) >> 3);
@@ -1564,12 +1569,18 @@ __device__ int huf_streams(LDSA Lds& L, const LDSA uint8_t* nb, const LDSA uint1
         uint32_t carry = 0;            // bits of symbols before this group
         uint32_t cw = 0;               // pending partial dword (index cd), low part still open
         int cd = -1;
-        for (int g = a; g < e; g += 64) {
-            const int i = g + lane;
-            const uint32_t sym = i < e ? lits.b(i) : 0u;
-            const uint32_t len = i < e ? nb[sym] : 0u;
-            const uint32_t code = i < e ? val[sym] : 0u;
-            const uint32_t incl = wave_incl_scan(len, lane);
+        for (int g = a; g < e; g += 256) {
+            const int i = g + 4 * lane;
+            const uint32_t w = i < e ? lits.w32(i) : 0u;
+            uint32_t len[4], code[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t sym = (w >> (8 * k)) & 0xffu;
+                len[k] = i + k < e ? (uint32_t)nb[sym] : 0u;
+                code[k] = val[sym];
+            }
+            const uint32_t L4 = len[0] + len[1] + len[2] + len[3];
+            const uint32_t incl = wave_incl_scan(L4, lane);
             const uint32_t gsum = rdlane(incl, 63);
             const uint32_t hiBit = total - carry;              // group occupies [hiBit - gsum, hiBit)
             const uint32_t loBit = hiBit - gsum;
@@ -1577,11 +1588,17 @@ __device__ int huf_streams(LDSA Lds& L, const LDSA uint8_t* nb, const LDSA uint1
             const int d1 = (int)(((g == a ? hiBit + 1 : hiBit) + 31) >> 5);   // (+1: the end mark)
             for (int d = lane; d < d1 - d0; d += 64) L.stage[d] = 0;
             wave_lds_fence();
-            if (len) {
-                const uint32_t bp = hiBit - incl - loBit + (loBit & 31u);   // bit offset in the window
-                const uint64_t v = (uint64_t)code << (bp & 31u);
-                atomicOr((uint32_t*)&L.stage[bp >> 5], (uint32_t)v);
-                if ((uint32_t)(v >> 32)) atomicOr((uint32_t*)&L.stage[(bp >> 5) + 1], (uint32_t)(v >> 32));
+            // symbol i + k sits below the bits of every symbol before it in the group
+            uint32_t S = incl - L4;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                S += len[k];
+                if (len[k]) {
+                    const uint32_t bp = hiBit - S - loBit + (loBit & 31u);   // bit offset in the window
+                    const uint64_t v = (uint64_t)code[k] << (bp & 31u);
+                    atomicOr((uint32_t*)&L.stage[bp >> 5], (uint32_t)v);
+                    if ((uint32_t)(v >> 32)) atomicOr((uint32_t*)&L.stage[(bp >> 5) + 1], (uint32_t)(v >> 32));
+                }
             }
             if (g == a && lane == 0) {
                 const uint32_t bp = total - loBit + (loBit & 31u);
@@ -1591,7 +1608,7 @@ __device__ int huf_streams(LDSA Lds& L, const LDSA uint8_t* nb, const LDSA uint1
             if (cd >= 0 && lane == 0) atomicOr((uint32_t*)&L.stage[cd - d0], cw);
             wave_lds_fence();
             // store every window dword but the lowest unless the window ends on a dword boundary
-            const bool last_group = g + 64 >= e;
+            const bool last_group = g + 256 >= e;
             const int dstart = ((loBit & 31u) == 0 || last_group) ? d0 : d0 + 1;
             for (int d = dstart + lane; d < d1; d += 64) st_b32(tmp.r, 4 * d, L.stage[d - d0]);
             if (dstart != d0) { cw = L.stage[0]; cd = d0; } else { cd = -1; }
