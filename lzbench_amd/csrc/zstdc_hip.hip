@@ -326,6 +326,10 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             // ---- table read, claim, read back
             uint32_t old = 0, back = 0;
             if (valid) old = T.get(h);
+            // the compare load for the slot's old value goes out before the claim round trip (a lane
+            // whose slot an earlier lane of the batch claimed compares against that lane's bytes)
+            const bool ook = valid && old > (uint32_t)pstart;
+            const uint32_t cwo = in.w32(ook ? (int)old - 1 : A);
             T.fence();
             if (valid) T.claim(h, (uint32_t)q + 1);
             T.fence();
@@ -351,12 +355,13 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 const uint64_t eb = grp & below;
                 prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
             }
-            const int qprev = lane_gather((uint32_t)q, prev < 0 ? lane : prev);
+            const int src = prev < 0 ? lane : prev;
+            const int qprev = lane_gather((uint32_t)q, src);
+            const uint32_t wprev = lane_gather((uint32_t)w8, src);
             const uint32_t cand = prev >= 0 ? (uint32_t)qprev + 1 : old;
             ZMK(3);
-            // ---- candidate compare
-            const bool cok = valid && cand > (uint32_t)pstart;
-            const bool hit = cok && in.w32(cok ? (int)cand - 1 : A) == (uint32_t)w8;
+            // ---- candidate compare (an in-batch candidate is past the prefix start)
+            const bool hit = prev >= 0 ? (valid && wprev == (uint32_t)w8) : (ook && cwo == (uint32_t)w8);
             const bool rhit = rok && rv == rm;
             const uint64_t R = ballot(rhit), H = ballot(hit), E = R | H;
             ZMK(4);
