@@ -366,8 +366,11 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             const uint64_t R = ballot(rhit), H = ballot(hit), E = R | H;
             ZMK(4);
             const uint64_t committed = E ? (vmask & (ffs64(E) == 63 ? ~0ull : ((2ull << ffs64(E)) - 1ull))) : vmask;
-            // ---- slots: the value the sequential order leaves
-            if (valid) {
+            // ---- slots: the value the sequential order leaves (no collision in the batch: each lane
+            // owns its slot, and the lanes past the first event put the old value back)
+            if (!losers) {
+                if (valid && !lane_on(committed)) T.put(h, old);
+            } else if (valid) {
                 const uint64_t gc = grp & committed;
                 bool writer;
                 uint32_t val;
