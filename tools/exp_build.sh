@@ -10,6 +10,7 @@ cd $root/lzbench_amd/csrc
 objs=""
 for f in lz4c_hip snappyc_hip decode_hip pack_hip zstdc_hip frame_hip; do
   sf=""; { [ $f = lz4c_hip ] || [ $f = snappyc_hip ]; } && sf="${SCHED_LZ4C--mllvm -amdgpu-sched-strategy=max-memory-clause}"
+  [ $f = zstdc_hip ] && sf="-mllvm -amdgpu-atomic-optimizer-strategy=None"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $sf $flags -c $f.hip -o $out/$f.o &
   objs="$objs $out/$f.o"
 done
