@@ -31,6 +31,7 @@ __device__ __forceinline__ uint32_t ld_u8(rsrc_t r, int off) { return __builtin_
 __device__ __forceinline__ void st_u8(rsrc_t r, int off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0); }
 __device__ __forceinline__ void st_b32(rsrc_t r, int off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0); }
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_b64(rsrc_t r, int off, uint32_t lo, uint32_t hi) {
     const u32x2 v = {lo, hi};
     __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 0);

@@ -48,7 +48,24 @@ lzh_pack_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint6
     Bytes src, dst;
     src.init(sp, sread);
     dst.init(packed + doff, cs);
-    copy_span(src, 0, dst, 0, (int)cs, threadIdx.x, blockDim.x);
+    // 16 bytes per thread and step: destination-aligned 16-byte stores, each from five aligned source
+    // dwords shifted by v_alignbyte; bytewise head (to the destination's 16-byte boundary) and tail
+    const int t = threadIdx.x, nt = blockDim.x, n = (int)cs;
+    const int head = min(n, (int)((16u - ((uint32_t)(uint64_t)(packed + doff) & 15u)) & 15u));
+    if (t < head) dst.st8(t, src.b(t));
+    const int nb = (n - head) >> 4;
+    for (int k = t; k < nb; k += nt) {
+        const int p = head + 16 * k;                       // source / destination position
+        const int Y = p + src.sh, Y0 = Y & ~3;
+        const uint32_t sft = (uint32_t)Y & 3u;
+        const uint32_t d0 = ld_b32(src.r, Y0), d1 = ld_b32(src.r, Y0 + 4), d2 = ld_b32(src.r, Y0 + 8),
+                       d3 = ld_b32(src.r, Y0 + 12), d4 = ld_b32(src.r, Y0 + 16);
+        const u32x4 v = {__builtin_amdgcn_alignbyte(d1, d0, sft), __builtin_amdgcn_alignbyte(d2, d1, sft),
+                         __builtin_amdgcn_alignbyte(d3, d2, sft), __builtin_amdgcn_alignbyte(d4, d3, sft)};
+        __builtin_amdgcn_raw_buffer_store_b128(v, dst.r, p + dst.sh, 0, 0);
+    }
+    const int t0 = head + 16 * nb;
+    if (t < n - t0) dst.st8(t0 + t, src.b(t0 + t));
 }
 
 // plain device copy, 16 B per lane (plumbing row: device memcpy of the whole input)
