@@ -1317,7 +1317,7 @@ __device__ void huf_qsort(LDSA HNode* a, int lo0, int hi0, LDSA int32_t* stk) {
         }
     }
 }
-__device__ uint32_t huf_limit(LDSA HNode* node, uint32_t last, uint32_t maxNb) {
+__device__ uint32_t huf_limit(LDSA HNode* node, uint32_t last, uint32_t maxNb, LDSA uint32_t* rankLast) {
     const uint32_t largest = node[last].nb;
     if (largest <= maxNb) return largest;
     int cost = 0;
@@ -1331,7 +1331,6 @@ __device__ uint32_t huf_limit(LDSA HNode* node, uint32_t last, uint32_t maxNb) {
     while (node[n].nb == maxNb) n--;
     cost >>= (largest - maxNb);
     const uint32_t NONE = 0xF0F0F0F0u;
-    uint32_t rankLast[14];
     for (int i = 0; i < 14; i++) rankLast[i] = NONE;
     uint32_t curNb = maxNb;
     for (int p = n; p >= 0; p--) {
@@ -1377,7 +1376,10 @@ __device__ uint32_t huf_build(LDSA Lds& L, uint32_t maxs, uint32_t maxNb) {
     for (int i = 0; i < 514; i++) { all[i].count = 0; all[i].parent = 0; all[i].byte = 0; all[i].nb = 0; }
     LDSA HNode* node = all + 1;
     {   // HUF_sort: buckets, then quick sort of the log2 buckets
-        uint16_t base[192], cur[192];
+        // (bucket bounds in LDS, the sequence-code histograms' space: a private array indexed by
+        // data would live in scratch memory)
+        LDSA uint16_t* base = (LDSA uint16_t*)&L.cnt3[0][0];
+        LDSA uint16_t* cur = base + 192;
         for (int b = 0; b < 192; b++) base[b] = 0;
         for (uint32_t s = 0; s <= maxs; s++) base[huf_bucket(L.cnt[s])]++;
         for (int b = 191; b > 0; b--) { base[b - 1] += base[b]; cur[b - 1] = base[b - 1]; }
@@ -1416,8 +1418,9 @@ __device__ uint32_t huf_build(LDSA Lds& L, uint32_t maxs, uint32_t maxNb) {
     node[root].nb = 0;
     for (int i = root - 1; i >= 256; i--) node[i].nb = node[node[i].parent].nb + 1;
     for (int i = 0; i <= nonNull; i++) node[i].nb = node[node[i].parent].nb + 1;
-    maxNb = huf_limit(node, (uint32_t)nonNull, maxNb);
-    uint16_t nbPer[13], valPer[13];
+    maxNb = huf_limit(node, (uint32_t)nonNull, maxNb, &L.cnt3[1][0]);
+    LDSA uint16_t* nbPer = (LDSA uint16_t*)&L.cnt3[0][0];
+    LDSA uint16_t* valPer = nbPer + 16;
     for (int i = 0; i < 13; i++) { nbPer[i] = 0; valPer[i] = 0; }
     for (int i = 0; i <= nonNull; i++) nbPer[node[i].nb]++;
     uint16_t mn = 0;
@@ -1513,14 +1516,16 @@ __device__ void histo256(LDSA uint32_t* cnt, const Bytes& src, int a, int n, int
     const int e = a + n;
     for (int base = a & ~3; base < e; base += 64 * 16) {
         const int p0 = base + 16 * lane;
+        uint32_t w[4];   // (loads unconditional at clamped positions: one wait for the four)
+#pragma unroll
+        for (int d = 0; d < 4; d++) w[d] = ld_b32(src.r, (p0 + 4 * d < e ? p0 + 4 * d : (a & ~3)) + src.sh);
 #pragma unroll
         for (int d = 0; d < 4; d++) {
             const int p = p0 + 4 * d;
             if (p < e) {
-                const uint32_t w = ld_b32(src.r, p + src.sh);
 #pragma unroll
                 for (int b = 0; b < 4; b++)
-                    if (p + b >= a && p + b < e) atomicAdd((uint32_t*)&cnt[(w >> (8 * b)) & 0xffu], 1u);
+                    if (p + b >= a && p + b < e) atomicAdd((uint32_t*)&cnt[(w[d] >> (8 * b)) & 0xffu], 1u);
             }
         }
     }
@@ -1555,10 +1560,14 @@ __device__ int huf_streams(LDSA Lds& L, const LDSA uint8_t* nb, const LDSA uint1
     for (int sidx = 0; sidx < nstreams; sidx++) {
         const int a = sidx * seg, e = (sidx == nstreams - 1) ? n : a + seg;
         uint32_t bits = 0;
-        for (int i = a + 4 * lane; i < e; i += 256) {
-            const uint32_t w = lits.w32(i);
+        for (int i0 = a + 4 * lane; i0 < e; i0 += 1024) {   // (four dwords' loads in flight at once)
+            uint32_t w[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) bits += i + k < e ? (uint32_t)nb[(w >> (8 * k)) & 0xffu] : 0u;
+            for (int u = 0; u < 4; u++) w[u] = lits.w32(i0 + 256 * u < e ? i0 + 256 * u : a);
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+#pragma unroll
+                for (int k = 0; k < 4; k++) bits += i0 + 256 * u + k < e ? (uint32_t)nb[(w[u] >> (8 * k)) & 0xffu] : 0u;
         }
         bits = wave_sum(bits);
         tbits[sidx] = bits;
@@ -1577,9 +1586,11 @@ __device__ int huf_streams(LDSA Lds& L, const LDSA uint8_t* nb, const LDSA uint1
         uint32_t carry = 0;            // bits of symbols before this group
         uint32_t cw = 0;               // pending partial dword (index cd), low part still open
         int cd = -1;
+        uint32_t wn = lits.w32(a + 4 * lane < e ? a + 4 * lane : a);   // (the next group's dword, loaded a group ahead)
         for (int g = a; g < e; g += 256) {
             const int i = g + 4 * lane;
-            const uint32_t w = i < e ? lits.w32(i) : 0u;
+            const uint32_t w = wn;
+            wn = lits.w32(i + 256 < e ? i + 256 : a);
             uint32_t len[4], code[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -1841,11 +1852,20 @@ __device__ int encode_sequences(LDSA Lds& L, const Bytes& att, const Bytes& tmp,
     uint32_t state = 0;
     uint32_t bitpos = 0;          // stream bits written so far
     uint32_t cw = 0;              // the open (partial) dword at bitpos >> 5
+    uint32_t q0, q1;              // the group's sequence, loaded a group ahead
+    {
+        const int x = min(max(ns - 64, 0) + lane, ns - 1);
+        q0 = ld_b32(seq, 8 * x); q1 = ld_b32(seq, 8 * x + 4);
+    }
     for (int g = ns; g > 0; g -= 64) {
         const int g0 = g >= 64 ? g - 64 : 0, gn = g - g0;
         const int i = lane;
         uint32_t ll = 0, ml = 3, off = 0;
-        if (i < gn) seq_unpack(ld_b32(seq, 8 * (g0 + i)), ld_b32(seq, 8 * (g0 + i) + 4), ll, ml, off);
+        if (i < gn) seq_unpack(q0, q1, ll, ml, off);
+        {
+            const int x = min((g0 >= 64 ? g0 - 64 : 0) + lane, max(g0 - 1, 0));
+            q0 = ld_b32(seq, 8 * x); q1 = ld_b32(seq, 8 * x + 4);
+        }
         const uint32_t llc = ll_code(ll), ofc = hb32(max(off, 1u)), mlc = ml_code(ml - 3);
         // per table and sequence (deltaNbBits, deltaFindState) into LDS (the Huffman sort stack, free
         // by now): the chain lanes read them ahead of the state-dependent lookups
