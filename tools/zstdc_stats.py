@@ -28,9 +28,6 @@ names = {9: "batches", 10: "pside_global", 11: "fwd_slow", 12: "bwd_slow", 13: "
 print(corpus, chunk >> 10, "KiB per block:", {k: round(v[i] / blocks, 1) for i, k in names.items()})
 ze = {16: "lit_histo", 17: "huf_tree", 18: "huf_streams", 19: "seq_histo", 20: "fse_tables", 21: "seq_chains", 22: "seq_packing"}
 zt = sum(v[i] for i in ze) or 1
-print("  sequence chains per block with sequences: longest part %.1f steps, parts (3 tables) %.1f (%d blocks)"
-      % (v[23] / blocks, v[14] / blocks, v[15]))
-print("  sequences %d; with a count-1 code: LL %.2f%%, OF %.2f%%, ML %.2f%%" % (v[12], *(100 * v[9 + t] / max(v[12], 1) for t in range(3))))
 print("  entropy clocks/block %.0f:" % (zt / blocks), {k: "%.1f%%" % (100 * v[i] / zt) for i, k in ze.items()})
 ph = {0: "schedule", 1: "pside+hash", 2: "table+groups", 3: "window_wait", 4: "eval+restore", 5: "match_finish",
       6: "literals+record", 7: "fills", 8: "loop/other", 14: "rep_loop", 16: "fills_loads", 17: "fills_puts", 18: "lit_copy"}
