@@ -270,6 +270,12 @@ __device__ __forceinline__ void lit_copy(const Bytes& src, int s0, const Bytes& 
     if (tl) dst.st8(d0 + t0 + lane, tb);
 }
 
+#ifndef LZH_ZSTD_FWD
+#define LZH_ZSTD_FWD 16   // lanes of the forward compare in the match's round trip (4 bytes each; longer: count_fwd)
+#endif
+#ifndef LZH_ZSTD_BWD
+#define LZH_ZSTD_BWD 16   // lanes of the backward compare in the match's round trip (1 byte each; longer: count_bwd)
+#endif
 template <int kMls = 0, class Tab>
 __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int bs, int be, uint32_t rep[2],
                            SeqOut& O, int lane) {
@@ -417,7 +423,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             bmax = max(0, min(m0 - anchor, p0 - pstart));
         }
         const int fmax = be - (m0 + 4);
-        const bool bl = lane < bmax, fl = 4 * lane < fmax;
+        const bool bl = lane < bmax && lane < LZH_ZSTD_BWD, fl = lane < LZH_ZSTD_FWD && 4 * lane < fmax;
         // (every load unconditional at a clamped position, literal loads included: one wait for all --
         // loads under lane-divergent branches each got their own wait inside the branch)
         const uint32_t ba = in.b(bl ? m0 - 1 - lane : m0), bb = in.b(bl ? p0 - 1 - lane : m0);
@@ -426,9 +432,10 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
         lit_copy(in, anchor, O.lits, O.nl, m0 - anchor, lane);
         int bk;
         {
+            constexpr int kB = LZH_ZSTD_BWD;
             const uint64_t m = ballot(!bl || ba != bb);
-            bk = m ? ffs64(m) : LZH_WAVE;
-            if (!m && bmax > LZH_WAVE) bk = LZH_WAVE + count_bwd(in, m0 - LZH_WAVE, p0 - LZH_WAVE, bmax - LZH_WAVE, lane);
+            bk = ffs64(m);
+            if (bk >= kB && bmax > kB) bk = kB + count_bwd(in, m0 - kB, p0 - kB, bmax - kB, lane);
             bk = min(bk, bmax);
         }
         int fw;
@@ -438,8 +445,9 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             if (4 * lane + eq > fmax) eq = fmax - 4 * lane;
             const bool st = fl && eq < 4;
             const uint64_t m = ballot(st);
+            constexpr int kF = 4 * LZH_ZSTD_FWD;
             if (m) fw = 4 * ffs64(m) + (int)rdlane((uint32_t)eq, ffs64(m));
-            else fw = fmax <= 256 ? max(fmax, 0) : 256 + count_fwd(in, m0 + 4 + 256, p0 + 4 + 256, fmax - 256, lane);
+            else fw = fmax <= kF ? max(fmax, 0) : kF + count_fwd(in, m0 + 4 + kF, p0 + 4 + kF, fmax - kF, lane);
         }
         ZMK(6);
         const int mstart = m0 - bk;
