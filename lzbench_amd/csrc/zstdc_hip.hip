@@ -256,8 +256,17 @@ __device__ void tab_put_pos(const Tab& T, const Bytes& in, int pos, const ZParam
 // dst[d0, d0+len) = src[s0, s0+len) for one wave: runs of up to 256 bytes load everything first
 // (head bytes, one dword per lane, tail bytes; positions clamped, nothing predicated) and store after
 // one wait; longer runs take copy_span
+#ifndef LZH_ZSTD_LITB
+#define LZH_ZSTD_LITB 64   // literal runs up to this many bytes: one byte per lane (no head / dword / tail split)
+#endif
 __device__ __forceinline__ void lit_copy(const Bytes& src, int s0, const Bytes& dst, int d0, int len, int lane) {
     if (len <= 0) return;
+    if (len <= LZH_ZSTD_LITB) {
+        const bool on = lane < len;
+        const uint32_t v = src.b(s0 + (on ? lane : 0));
+        if (on) dst.st8(d0 + lane, v);
+        return;
+    }
     if (len > 4 * LZH_WAVE) { copy_span(src, s0, dst, d0, len, lane, LZH_WAVE); return; }
     const int head = min(len, (4 - ((d0 + dst.sh) & 3)) & 3);
     const int nd = (len - head) >> 2, t0 = head + 4 * nd;
