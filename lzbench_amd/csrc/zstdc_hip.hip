@@ -1027,22 +1027,33 @@ struct Fse {                    // FSE compression table (FSE_buildCTable_wksp l
 };
 
 struct Lds {
-    uint32_t cnt[256];
     uint32_t cnt3[3][64];       // LL / OF / ML code histograms
-    HNode node[514];
+    // the Huffman tree while the literals' table is built (huf_build), the FSE tables after it: the
+    // weights' table (fse[0], huf_compress_weights) and the sequences' tables
+    union {
+        HNode node[514];
+        Fse fse[3];
+    };
     uint8_t nb[256];            // fresh Huffman table
     uint16_t val[256];
     uint8_t pnb[256];           // previous block's Huffman table (frame scratch)
     uint16_t pval[256];
-    Fse fse[3];
-    Fse wfse;                   // weights table (tableLog <= 6)
     s16 norm[64];
-    uint8_t w[256];             // Huffman weights
-    uint8_t hdr[264];           // Huffman table header
-    uint8_t symAt[512];         // FSE spread workspace
-    uint32_t cumul[64];
-    uint32_t sq[64 * 3];        // a group's (nbBits << 16 | bits) per state chain
-    int32_t qs[2 * 300];        // quick-sort task stack
+    // the literals section's workspace, then the sequences section's (the two unions: 13 waves per CU
+    // instead of 8)
+    union {
+        struct {
+            uint32_t cnt[256];  // literal histogram
+            uint8_t w[256];     // Huffman weights
+            uint8_t hdr[264];   // Huffman table header
+            int32_t qs[2 * 300];   // quick-sort task stack (the sequence encoder's table deltas later)
+        };
+        struct {
+            uint8_t symAt[512];    // FSE spread workspace
+            uint32_t cumul[64];
+            uint32_t sq[64 * 3];   // a group's (nbBits << 16 | bits) per state chain
+        };
+    };
     uint32_t stage[192];        // bit staging window (64 sequences of <= 90 bits)
     uint32_t misc[16];
 };
@@ -1471,25 +1482,25 @@ __device__ int huf_compress_weights(LDSA Lds& L, const LdsSink& o, int pos, uint
     const uint32_t tl = fse_opt_log(6, wn, maxs, 2);
     if (fse_normalize(L.norm, tl, cnt, wn, maxs, 0)) return 0;
     const int h = fse_write_ncount(o, pos, L.norm, maxs, tl);
-    fse_build(L.wfse, L.norm, maxs, tl, (LDSA uint8_t*)L.cnt3[1], L.cnt3[2]);
+    fse_build(L.fse[0], L.norm, maxs, tl, (LDSA uint8_t*)L.cnt3[1], L.cnt3[2]);
     if (wn <= 2) return 0;
     BitW<LdsSink> b{o, pos + h, 0, 0};
     uint32_t s1, s2;
     int i = (int)wn;
     if (wn & 1) {
-        s1 = fse_init_state(L.wfse, L.w[--i]);
-        s2 = fse_init_state(L.wfse, L.w[--i]);
-        fse_encode(b, L.wfse, s1, L.w[--i]);
+        s1 = fse_init_state(L.fse[0], L.w[--i]);
+        s2 = fse_init_state(L.fse[0], L.w[--i]);
+        fse_encode(b, L.fse[0], s1, L.w[--i]);
     } else {
-        s2 = fse_init_state(L.wfse, L.w[--i]);
-        s1 = fse_init_state(L.wfse, L.w[--i]);
+        s2 = fse_init_state(L.fse[0], L.w[--i]);
+        s1 = fse_init_state(L.fse[0], L.w[--i]);
     }
     while (i > 0) {
-        fse_encode(b, L.wfse, s2, L.w[--i]);
-        fse_encode(b, L.wfse, s1, L.w[--i]);
+        fse_encode(b, L.fse[0], s2, L.w[--i]);
+        fse_encode(b, L.fse[0], s1, L.w[--i]);
     }
-    b.add(s2, L.wfse.tlog);
-    b.add(s1, L.wfse.tlog);
+    b.add(s2, L.fse[0].tlog);
+    b.add(s1, L.fse[0].tlog);
     return b.close() - pos;
 }
 // HUF_writeCTable_wksp into L.hdr; returns its size, -1 = not representable
