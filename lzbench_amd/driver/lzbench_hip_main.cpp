@@ -399,7 +399,10 @@ static void bench_list(params_t* P, std::vector<size_t>& fs, const char* list, u
         const compressor_desc_t* d = find_row(parts[0].c_str());
         if (!d || ((d == &comp_desc[1] || d == &comp_desc[2]) && !sys_lz4_compress_fast) ||
             (!g_gpu && d->init)) {
-            printf("%s NOT FOUND\n", parts[0].c_str());
+            // (lzbench.cpp:507-528: one line per requested level, "(null)" -- glibc's rendering of the
+            // NULL level argument -- when none is given; memcpy, index 0, is never found by name)
+            for (size_t k = 1; k == 1 || k < parts.size(); k++)
+                printf("NOT FOUND: %s %s\n", parts[0].c_str(), k < parts.size() ? parts[k].c_str() : "(null)");
             continue;
         }
         if (parts.size() == 1) {

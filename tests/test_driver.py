@@ -56,6 +56,53 @@ def test_cpu_rows_chunk_loop(sample):
     assert "ERROR" not in out
 
 
+@pytest.fixture(scope="module")
+def random16(tmp_path_factory):
+    """BASELINE.json configs[0]'s input: a 16 MiB random file."""
+    d = L.datagen("random", 16 << 20, seed=31)
+    p = tmp_path_factory.mktemp("cfg1") / "random16.bin"
+    p.write_bytes(d.tobytes())
+    return str(p), d
+
+
+def test_config1_memcpy_chunk_loop_cpu(random16):
+    """Config 1 (`-ememcpy -b64` on 16 MiB random, CPU path only): the implicit memcpy row runs the chunk
+    loop and verifies; memcpy named in -e is not found, as in the reference (lzbench.cpp:507-528 search
+    from index 1); an lz4 row on the same incompressible chunks (each one larger than its chunk, so not
+    raw-stored: lzbench.cpp:284-288 stores only clen <= 0 or clen == part) equals the reference loop."""
+    path, data = random16
+    out = run(["-ememcpy/lz4", "-b64", "-t0,0", "-i1,1", "-o3", path])
+    assert "ERROR" not in out, out
+    assert "NOT FOUND: memcpy (null)" in out, out
+    r = rows(out)
+    mc = [k for k in r if k.startswith("memcpy")]
+    assert mc and int(r[mc[0]][4]) == int(r[mc[0]][5]) == len(data), out   # Orig. size == Compr. size
+    packed, cs = O.compress_chunks(data, "lz4", 65536)
+    lz4 = [k for k in r if k.startswith("lz4 ")]
+    assert lz4 and int(r[lz4[0]][5]) == len(packed) > len(data), out
+    assert (cs == 65536 + 258).all()          # token + 257 literal-length bytes + 65 536 literals
+
+
+@pytest.mark.gpu
+def test_config1_gpu_rows_raw_store(random16, tmp_path):
+    """The same 16 MiB random file through the GPU rows (`hipMemcpy`, `hip_lz4`, `hip_snappy`): every
+    incompressible chunk is handled exactly as the reference loop handles it (bytes and sizes compared
+    through the LZH_DUMP_DIR hook), and every row verifies."""
+    path, data = random16
+    env = dict(os.environ, LZH_DUMP_DIR=str(tmp_path))
+    out = run(["-ehipMemcpy/hip_lz4/hip_snappy", "-b64", "-t0,0", "-i1,1", path], env=env)
+    assert "ERROR" not in out, out
+    r = rows(out)
+    assert any(k.startswith("hipMemcpy") for k in r), out
+    for name, codec in (("hip_lz4", "lz4"), ("hip_snappy", "snappy")):
+        packed, cs = O.compress_chunks(data, codec, 65536)
+        key = [k for k in r if k.startswith(name + " ")]
+        assert key and int(r[key[0]][4]) == len(packed), (name, out)
+        got = np.fromfile(tmp_path / f"{name}_0.bin", np.uint8)
+        gcs = np.fromfile(tmp_path / f"{name}_0.sizes", np.uint64)
+        assert (got == packed).all() and (gcs == cs).all(), name
+
+
 def test_csv_format(sample):
     path, _ = sample
     out = run(["-elz4", "-b64", "-t0,0", "-o4", path])
