@@ -194,7 +194,9 @@ def e2e_rows(L, host, codec, chunk, level, ngpus, iters, dig=None):
             best_d = min(best_d, time.perf_counter() - t)
     ok = tot > 0 and r == n and bool((back[:n] == host).all())
     exact = None
-    if dig is not None and tot > 0:
+    # (each copy's slab lines up with whole chunks only when the per-copy size is a multiple of the
+    # chunk size; otherwise a copy's chunks straddle two copies and no per-copy digest applies)
+    if dig is not None and tot > 0 and dig["size"] % chunk == 0:
         reps, per = n // dig["size"], len(cs) // (n // dig["size"])
         c64 = comp.astype("<u8")
         offs = np.concatenate([[0], np.cumsum(comp.astype(np.int64))])
@@ -354,6 +356,8 @@ def main():
     result_extra["host_cpu"] = cpuinfo
     if not args.no_e2e:
         # the in-process product path over all N devices, by rank 0 while the other ranks wait
+        # (host memory on rank 0: the N-copy input plus its packed output and the decode buffer, about
+        # 3N GiB at the default 1 GiB per GPU -- 24 GiB at N = 8, well inside a node's RAM)
         del d_in, codec
         torch.cuda.empty_cache()
         if dist:

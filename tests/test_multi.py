@@ -20,10 +20,12 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, codec, chunk, n, q, hip=False):
+def _worker(rank, world, port, codec, chunk, n, q, hip=False, gather_mode=None):
     import torch.distributed as dist
     import lzbench_amd as L
     from lzbench_amd.shard import sharded_compress
+    if gather_mode:
+        os.environ["LZH_GATHER"] = gather_mode
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -45,14 +47,17 @@ def _worker(rank, world, port, codec, chunk, n, q, hip=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("codec,chunk", [("lz4", 65536), ("snappy", 262144)])
-def test_two_rank_shard_gather_equals_single(codec, chunk):
+@pytest.mark.parametrize("codec,chunk,mode", [("lz4", 65536, None), ("snappy", 262144, None),
+                                              ("lz4", 65536, "collective")])
+def test_two_rank_shard_gather_equals_single(codec, chunk, mode):
+    """mode None: the shared /dev/shm buffer; "collective": the dist.gather fallback that ranks on
+    several hosts (or a /dev/shm too small for the buffer) take -- forced here by LZH_GATHER."""
     import lzbench_amd as L
     n = 3 * chunk + 12345                       # ragged tail, uneven split across ranks
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, codec, chunk, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, codec, chunk, n, q, False, mode)) for r in range(2)]
     for p in procs:
         p.start()
     packed, cs, tmax = q.get(timeout=120)
@@ -91,6 +96,41 @@ def test_two_rank_shard_gather_hip_codec(codec, chunk):
     ep, ec = O.compress_chunks(data, oc, chunk, 0 if codec == "lz4frame" else 1)
     assert np.frombuffer(packed, np.uint8).tobytes() == ep.tobytes()
     assert cs == ec.tolist()
+
+
+def _gather_path_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from lzbench_amd import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    host = socket.gethostname
+    if rank == 1:   # rank 1 pretends to live on another host: the shared buffer is not an option
+        socket.gethostname = lambda: "elsewhere"
+    info, res = shard.gather_slabs(np.full(10 + rank, rank + 1, np.uint8), np.array([10 + rank]), rank, world)
+    socket.gethostname = host
+    if rank == 0:
+        q.put((info["path"], info.get("why", ""), res[0].tolist(), res[1].tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_falls_back_across_hosts():
+    """with ranks on two hosts the /dev/shm gather cannot work (the other host's ranks
+    cannot open the file), so every rank takes the dist.gather path, chosen on rank 0 and broadcast."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_path_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    path, why, packed, cs = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert path == "collective" and "2 hosts" in why
+    assert packed == [1] * 10 + [2] * 11 and cs == [10, 11]
 
 
 def test_shard_ranges_cover_all_chunks():
