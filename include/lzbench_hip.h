@@ -124,6 +124,11 @@ int lzh_level_supported(int codec, int level, size_t chunk_size);
  * sub-batches, shards, compress input / packed / temp bytes per sub-batch slot, then the sub-batch
  * slots of shard 0 .. shards-1.  Host arithmetic only (no device call).  Returns the count written. */
 int lzh_debug_plan(size_t ngpus, size_t n, size_t chunk_size, int codec, uint64_t* out, int nout);
+/* The batched rows' host gather order (api.cpp GatherOrder): sub-batches 0 .. nsb-1 complete in
+ * `order` (a permutation) with packed sizes sizes[j]; placed[3i .. 3i+2] = (sub-batch, output offset,
+ * index into `order` of the completion that made it placeable) for the i-th placement.  Host
+ * arithmetic only.  Returns the number of placements (nsb). */
+int lzh_debug_gather_order(size_t nsb, const uint64_t* order, const uint64_t* sizes, uint64_t* placed);
 
 /* d_csizes: nchunks u32 (out); d_offsets: nchunks+1 u64 (out; [nchunks] = packed total).
  * level: lz4 acceleration (<=1 -> LZ4_compress_default); zstd level; ignored by snappy. */

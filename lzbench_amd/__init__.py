@@ -90,6 +90,7 @@ SIGNATURES = {
     "lzh_num_chunks": (_SZ, [_SZ, _SZ]),
     "lzh_level_supported": (C.c_int, [C.c_int, C.c_int, _SZ]),
     "lzh_debug_plan": (C.c_int, [_SZ, _SZ, _SZ, C.c_int, _P, C.c_int]),
+    "lzh_debug_gather_order": (C.c_int, [_SZ, _P, _P, _P]),
     "lzh_compress_async": (C.c_int, [C.c_int, C.c_int, _P, _SZ, _SZ, _SZ, _P, _SZ, _P, _P, _P, _SZ, _P]),
     "lzh_decompress_async": (C.c_int, [C.c_int, _P, _SZ, _P, _P, _SZ, _SZ, _P, _P, _P, _SZ, _P]),
     "lzh_compress_kernel_only": (C.c_int, [C.c_int, C.c_int, _P, _SZ, _SZ, _SZ, _P, _P, _P]),

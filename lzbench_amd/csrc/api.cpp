@@ -5,8 +5,10 @@
 // Host layer: lzbench rows and batched rows.  A row's workmem is an LzhCtx holding, per GPU,
 // a stream and device buffers sized at init for the chunk size (grown on demand).  A batch
 // is cut into runs of uniform chunking (lzbench's chunk list is uniform per input file,
-// lzbench.cpp:366-373); each run is sharded over the GPUs by contiguous chunk ranges, every
-// GPU compresses its slab, and the host gathers the packed slabs in chunk order.
+// lzbench.cpp:366-373); each run is cut into ~128 MiB sub-batches dealt round-robin to the GPUs
+// (make_plan), every GPU pipelines its sub-batches (copy in | kernels | copy out), and the host
+// places each sub-batch's packed bytes at its chunk-order offset as soon as the sizes before it
+// are known.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -14,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -502,6 +505,32 @@ struct Plan {
     size_t slots(size_t g) const { return nsb > g ? (nsb - g + G - 1) / G : 0; }
 };
 
+// Host gather bookkeeping (pure host code, tested on the CPU through lzh_debug_gather_order):
+// sub-batches finish in any order across the shards; sub-batch j's packed bytes go to the
+// output at the sum of the packed sizes before it (lzbench.cpp:266-298), so j is placed as soon
+// as its own sizes and every earlier sub-batch's are known -- the earliest moment its offset
+// exists -- and the copies leave in chunk order.
+struct GatherOrder {
+    std::vector<uint8_t> done;
+    std::vector<size_t> tot;
+    size_t next = 0, base = 0;
+    explicit GatherOrder(size_t n) : done(n, 0), tot(n, 0) {}
+    bool finished() const { return next == done.size(); }
+    // j's sizes are known (packed total t): place(j', offset) for every sub-batch that became placeable
+    template <class F>
+    int complete(size_t j, size_t t, F&& place) {
+        done[j] = 1;
+        tot[j] = t;
+        while (next < done.size() && done[next]) {
+            const int rc = place(next, base);
+            if (rc) return rc;
+            base += tot[next];
+            next++;
+        }
+        return 0;
+    }
+};
+
 // (a chunk size above the input is one chunk of the input's size: buffers are sized from the bytes
 // present, not from lzbench's 1.79 GB default chunk)
 size_t row_chunk(size_t n, size_t chunk) { return std::max<size_t>(std::min(chunk, n), 1); }
@@ -562,21 +591,41 @@ int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t c
         LZH_CHECK(hipMemcpyAsync(d.h_cs + l * P.sbk, dcs, ck * 4, hipMemcpyDeviceToHost, ks));
         LZH_CHECK(hipEventRecord(e_k, ks));
     }
-    size_t base = 0;
+    // host-side gather: poll every pending sub-batch (any shard, any order); each one's sizes are
+    // read when its kernels are done, and copies leave as soon as their chunk-order offset is known
     bool fits = true;
-    for (size_t j = 0; j < P.nsb; j++) {     // host-side gather in chunk order
+    GatherOrder go(P.nsb);
+    auto place = [&](size_t j, size_t base) -> int {
         Dev& d = c->devs[P.shard(j)];
-        const size_t l = P.slot(j), ck = P.c_count(j), c0 = P.c_begin(j);
+        const size_t l = P.slot(j), tot = go.tot[j];
+        if (!fits || base + tot > outcap) { fits = false; return 0; }   // lzbench: cannot store
         if (hipSetDevice(d.id) != hipSuccess) return LZH_EHIP;
-        LZH_CHECK(hipEventSynchronize(evk.get(j)));
-        size_t tot = 0;
-        const uint32_t* hs = d.h_cs + l * P.sbk;
-        for (size_t i = 0; i < ck; i++) { compr_sizes[c0 + i] = hs[i]; tot += hs[i]; }
-        if (!fits || base + tot > outcap) { fits = false; continue; }   // lzbench: cannot store
         LZH_CHECK(hipStreamWaitEvent(d.sout, evk.get(j), 0));
         LZH_CHECK(hipMemcpyAsync(out + base, (uint8_t*)d.packed.p + l * sb_packed, tot, hipMemcpyDeviceToHost, d.sout));
-        base += tot;
+        return 0;
+    };
+    for (unsigned spin = 0; !go.finished(); spin++) {
+        bool progress = false;
+        for (size_t j = go.next; j < P.nsb; j++) {
+            if (go.done[j]) continue;
+            const hipError_t q = hipEventQuery(evk.get(j));
+            if (q == hipErrorNotReady) continue;
+            if (q != hipSuccess) {
+                fprintf(stderr, "lzbench_hip: sub-batch %zu failed: %s\n", j, hipGetErrorString(q));
+                return LZH_EHIP;
+            }
+            Dev& d = c->devs[P.shard(j)];
+            const size_t l = P.slot(j), ck = P.c_count(j), c0 = P.c_begin(j);
+            size_t tot = 0;
+            const uint32_t* hs = d.h_cs + l * P.sbk;
+            for (size_t i = 0; i < ck; i++) { compr_sizes[c0 + i] = hs[i]; tot += hs[i]; }
+            const int rc = go.complete(j, tot, place);
+            if (rc) return rc;
+            progress = true;
+        }
+        if (!progress && (spin & 63) == 63) std::this_thread::yield();
     }
+    const size_t base = go.base;
     for (size_t g = 0; g < P.G; g++) {
         if (hipSetDevice(c->devs[g].id) != hipSuccess || hipStreamSynchronize(c->devs[g].sout) != hipSuccess ||
             hipStreamSynchronize(c->devs[g].s) != hipSuccess || hipStreamSynchronize(c->devs[g].s2) != hipSuccess)
@@ -663,6 +712,24 @@ int64_t run_decompress(LzhCtx* c, const uint8_t* in, const size_t* compr_sizes, 
 }
 
 }  // namespace
+
+// debug (CPU): the gather's placement order for sub-batches completing in `order` with packed
+// sizes `sizes`: placed[i] = (sub-batch, offset, index into `order` of the completion that placed it)
+extern "C" int lzh_debug_gather_order(size_t nsb, const uint64_t* order, const uint64_t* sizes, uint64_t* placed) {
+    GatherOrder go(nsb);
+    size_t np = 0, at = 0;
+    for (size_t i = 0; i < nsb; i++) {
+        at = i;
+        go.complete((size_t)order[i], (size_t)sizes[order[i]], [&](size_t j, size_t base) {
+            placed[3 * np] = j;
+            placed[3 * np + 1] = base;
+            placed[3 * np + 2] = at;
+            np++;
+            return 0;
+        });
+    }
+    return (int)np;
+}
 
 extern "C" int lzh_debug_plan(size_t ngpus, size_t n, size_t chunk_size, int codec, uint64_t* out, int nout) {
     if (!out || nout <= 0 || chunk_size == 0) return 0;

@@ -504,424 +504,22 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
     O.nl += be - anchor;
 }
 
-// ------------------------------------------------------------------ ring parse (v2)
-// The same parse with fewer dependent global round trips per sequence (one sequence costs one
-// batch; with one or two waves per SIMD every round trip is exposed):
-//   * the probes' P side (hash input, the 4-byte compare, the forward / backward compare bytes)
-//     and the literal copy read an LDS input ring filled ahead of the front by LDS-DMA;
-//   * the candidate compare loads a 32-byte window [c-4, c+28) per lane and the repcode check a
-//     window at ip2 - rep, so the event lane's backward extension (<= 4 bytes) and forward count
-//     (<= 20 bytes) come out of the same round trip as the compare (zstd_fast.c:196-283);
-//   * the table fills and the immediate repcode check after a match (zstd_fast.c:296-311) share a
-//     round trip with the ring's refill for the new front.
 #ifndef LZH_ZSTD_TAB17
 #define LZH_ZSTD_TAB17 1   // 17-bit hash-table entries (LdsTab17) for chunks <= 128 KiB
 #endif
-#ifndef LZH_ZSTD_RING
-#define LZH_ZSTD_RING 0   // (measured slower: 1 GiB mixed -b128 compress 100.7 -> 108.7 ms, text 209 -> 222 ms, profiles/r03_z)
-#endif
-constexpr int kZRing = 1024;               // bytes of LDS input ring
-constexpr int kZAhead = 640;               // keep the ring filled this far past the front
-constexpr int kZRingLds = kZRing + 32;     // + a mirror of the ring's first 32 bytes (reads never wrap)
-
-typedef __attribute__((address_space(3))) void* zlds_ptr_t;
-
-// s_waitcnt vmcnt(0) the compiler sees (an asm wait is opaque to its counter model: it would keep
-// the loads pending and later wait with counts that miss the asm LDS-DMA refills, stalling on them)
-__device__ __forceinline__ void wait_vm_known() { __builtin_amdgcn_s_waitcnt(0x0F70); }
-
-// LDS ring over descriptor offsets X = p + sh: holds [max(lo, fill - kZRing), ready)
-struct ZRing {
-    LDSA uint32_t* w;
-    int sh, lo, fill, ready;
-    __device__ __forceinline__ bool has(int p0, int p1) const {
-        return p0 + sh >= max(lo, fill - kZRing) && p1 + sh <= ready;
-    }
-    __device__ __forceinline__ uint32_t dword(int a) const {
-        return ((volatile const LDSA uint32_t*)w)[(a >> 2) & (kZRing / 4 - 1)];
-    }
-    __device__ __forceinline__ uint32_t u32(int p) const {
-        const int X = p + sh, a = X & ~3;
-        return __builtin_amdgcn_alignbyte(dword(a + 4), dword(a), (uint32_t)X & 3u);
-    }
-    __device__ __forceinline__ uint32_t byte(int p) const {
-        return ((volatile const LDSA uint8_t*)w)[(p + sh) & (kZRing - 1)];
-    }
-    __device__ __forceinline__ void refill(rsrc_t r, int lane) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (zlds_ptr_t)(w + ((fill & (kZRing - 1)) >> 2)), 4, fill + 4 * lane,
-                                                 0, 0, 0);
-        if ((fill & (kZRing - 1)) == 0 && lane < 8)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (zlds_ptr_t)(w + kZRing / 4), 4, fill + 4 * lane, 0, 0, 0);
-        fill += 256;
-    }
-    // keep [front - 64, front + kZAhead) coming (landed at the next vmcnt wait); a front past the
-    // ring restarts it
-    __device__ __forceinline__ void advance(rsrc_t r, int front, int endX, int lane) {
-        const int want = (front + sh - 64) & ~255;
-        if (fill < want) { fill = want; lo = want; }
-        const int target = min(front + sh + kZAhead, endX);
-        for (int k = 0; k < 4 && fill < target; k++) refill(r, lane);
-    }
-    __device__ __forceinline__ void landed() {
-        ready = fill;
-        wave_lds_fence();
-    }
-};
-
-struct PW {   // words at p-4, p, p+4, .., p+20 of a probe position
-    uint32_t m4, w, q0, q1, q2, q3, q4;
-};
-__device__ __forceinline__ PW pw_ring(const ZRing& R, int p) {   // one base, immediate offsets (mirror)
-    const int X = p - 4 + R.sh;
-    const uint32_t s = (uint32_t)X & 3u;
-    const volatile LDSA uint32_t* q = (const volatile LDSA uint32_t*)R.w + ((X & (kZRing - 1)) >> 2);
-    const uint32_t a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3], a4 = q[4], a5 = q[5], a6 = q[6], a7 = q[7];
-    PW v;
-    v.m4 = __builtin_amdgcn_alignbyte(a1, a0, s);
-    v.w = __builtin_amdgcn_alignbyte(a2, a1, s);
-    v.q0 = __builtin_amdgcn_alignbyte(a3, a2, s);
-    v.q1 = __builtin_amdgcn_alignbyte(a4, a3, s);
-    v.q2 = __builtin_amdgcn_alignbyte(a5, a4, s);
-    v.q3 = __builtin_amdgcn_alignbyte(a6, a5, s);
-    v.q4 = __builtin_amdgcn_alignbyte(a7, a6, s);
-    return v;
-}
-// a 32-byte window [c-4, c+28) from global memory (8 aligned dwords; bytes before 0 are garbage and
-// never counted: the backward extension is bounded by the block's prefix start)
-struct ZWin {
-    uint32_t d0, d1, d2, d3, d4, d5, d6, d7, sm;
-    __device__ __forceinline__ void load(const Bytes& in, int c) {
-        const int X = c + in.sh;
-        const int A = (X & ~3) - 4;
-        sm = (uint32_t)X & 3u;
-        d0 = ld_b32(in.r, max(A, 0)); d1 = ld_b32(in.r, A + 4); d2 = ld_b32(in.r, A + 8); d3 = ld_b32(in.r, A + 12);
-        d4 = ld_b32(in.r, A + 16); d5 = ld_b32(in.r, A + 20); d6 = ld_b32(in.r, A + 24); d7 = ld_b32(in.r, A + 28);
-    }
-    __device__ __forceinline__ PW words() const {
-        PW v;
-        v.m4 = __builtin_amdgcn_alignbyte(d1, d0, sm);
-        v.w = __builtin_amdgcn_alignbyte(d2, d1, sm);
-        v.q0 = __builtin_amdgcn_alignbyte(d3, d2, sm);
-        v.q1 = __builtin_amdgcn_alignbyte(d4, d3, sm);
-        v.q2 = __builtin_amdgcn_alignbyte(d5, d4, sm);
-        v.q3 = __builtin_amdgcn_alignbyte(d6, d5, sm);
-        v.q4 = __builtin_amdgcn_alignbyte(d7, d6, sm);
-        return v;
-    }
-};
-// 4-byte equality at (p, c); bkr = equal bytes going backwards from p-1 / c-1 (<= 4), len = equal
-// bytes forwards from p+4 / c+4 (<= 20)
-__device__ __forceinline__ bool zeval(const PW& P, const PW& M, int& bkr, int& len) {
-    len = first_diff20(P.q0 ^ M.q0, P.q1 ^ M.q1, P.q2 ^ M.q2, P.q3 ^ M.q3, P.q4 ^ M.q4);
-    const uint32_t y = P.m4 ^ M.m4;
-    bkr = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
-    return P.w == M.w;
-}
-
-// dst[d0, d0+len) = ring bytes [s0, s0+len): destination-aligned dword stores, bytewise head / tail
-__device__ __forceinline__ void ring_copy(const ZRing& R, int s0, const Bytes& dst, int d0, int len, int lane) {
-    if (len <= 0) return;
-    const int head = min(len, (4 - ((d0 + dst.sh) & 3)) & 3);
-    if (lane < head) dst.st8(d0 + lane, R.byte(s0 + lane));
-    const int nd = (len - head) >> 2;
-    for (int d = lane; d < nd; d += LZH_WAVE) {
-        const int o = head + 4 * d;
-        dst.st32_aligned(d0 + o, R.u32(s0 + o));
-    }
-    const int tail0 = head + 4 * nd;
-    if (lane < len - tail0) dst.st8(d0 + tail0 + lane, R.byte(s0 + tail0 + lane));
-}
-
-// 8 bytes at a wave-uniform position: from the ring when it holds them, else global memory
-__device__ __forceinline__ uint64_t rg64(const ZRing& R, const Bytes& in, int pos) {
-    if (R.has(pos, pos + 12)) return (uint64_t)R.u32(pos) | ((uint64_t)R.u32(pos + 4) << 32);
-    return ld64(in, pos);
-}
 
 #ifndef LZH_ZSTDC_STATS
-#define LZH_ZSTDC_STATS 0   // event counters and phase clocks of fast_block2 (tools/zstdc_stats.py)
+#define LZH_ZSTDC_STATS 0   // entropy-kernel phase clocks (tools/zstdc_stats.py)
 #endif
 #if LZH_ZSTDC_STATS
 __device__ unsigned long long lzh_zstdc_stats_buf[24];
 // entropy-kernel phase clocks (indices 16..23): lane 0 adds the clocks since its previous mark
 #define ZEM(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); if (threadIdx.x == 0) atomicAdd(&lzh_zstdc_stats_buf[16 + (i)], (unsigned long long)(t_ - ze_last)); ze_last = t_; } while (0)
 #define ZEM_DECL uint64_t ze_last = __builtin_amdgcn_s_memtime()
-#define ZS(i, v) (zst[i] += (uint64_t)(v))
-#define ZT(i) do { asm volatile("; ZMARK " #i ::: "memory"); const uint64_t t_ = __builtin_amdgcn_s_memtime(); zst[i] += t_ - zlast; zlast = t_; } while (0)
 #else
-#define ZS(i, v) ((void)0)
-#define ZT(i) ((void)0)
 #define ZEM(i) ((void)0)
 #define ZEM_DECL ((void)0)
 #endif
-
-template <class Tab>
-__device__ void fast_block2(const Tab& T, ZRing& Rg, const Bytes& in, const ZParams& P, int bs, int be, uint32_t rep[2],
-                            SeqOut& O, int lane) {
-    const int W = 1 << P.wlog;
-    const int dl = bs > W ? bs - W : 0;                     // ZSTD_window_enforceMaxDist at the block start
-    const int pstart = (be - dl > W) ? be - W : dl;        // ZSTD_getLowestPrefixIndex(blockEnd)
-    const int ilimit = be - 8;
-    const int endX = be + Rg.sh + 64;                       // (ring fills stop a little past the block)
-    int ip = bs + (bs == pstart);
-    int anchor = bs;
-    uint32_t r1 = rep[0], r2 = rep[1], saved = 0;
-    {
-        const int wlow = (ip - dl > W) ? ip - W : dl;
-        const uint32_t maxRep = (uint32_t)(ip - wlow);
-        if (r2 > maxRep) { saved = r2; r2 = 0; }
-        if (r1 > maxRep) { saved = r1; r1 = 0; }
-    }
-    const int j = lane >> 1, half = lane & 1;
-    const uint64_t below = (1ull << lane) - 1ull;
-#if LZH_ZSTDC_STATS
-    uint64_t zst[24] = {};
-    uint64_t zlast = __builtin_amdgcn_s_memtime();
-#endif
-    Rg.fill = Rg.lo = max((bs + Rg.sh - 64) & ~255, 0);
-    Rg.advance(in.r, bs, endX, lane);
-    wait_vm_known();
-    Rg.landed();
-    // the immediate repcode loop (zstd_fast.c:301-311) from ip, its first check known to hold
-    auto rep_loop = [&]() {
-        bool more = true;
-        while (more) {
-            const int rl = 4 + count_fwd(in, ip + 4, ip + 4 - (int)r2, be - (ip + 4), lane);
-            const uint32_t t = r2; r2 = r1; r1 = t;
-            if (lane == 0) tab_put_pos(T, in, ip, P);
-            T.fence();
-            O.put(lane, 0, 1, (uint32_t)rl);
-            ip += rl;
-            anchor = ip;
-            more = ip <= ilimit && r2 > 0 && in.w32(ip) == in.w32(ip - (int)r2);
-        }
-    };
-    // pend: a match ended at ip and its immediate repcode check is still to be done; the check's
-    // loads ride on the next batch's window round trip (the batch is dropped when it holds)
-    bool pend = false;
-    for (;;) {
-        ip = unii(ip); anchor = unii(anchor);
-        Rg.fill = unii(Rg.fill); Rg.lo = unii(Rg.lo); Rg.ready = unii(Rg.ready);
-        pend = unii((int)pend) != 0;
-        ZT(8);
-        if (ip + (int)P.step + 1 >= ilimit) {
-            if (pend) {   // no search follows: the check on its own
-                pend = false;
-                if (in.w32(ip) == in.w32(ip - (int)r2)) rep_loop();
-                continue;
-            }
-            break;
-        }
-        int A = ip, D = (int)P.step, s = (int)P.step, nx = ip + 128;
-        int kind = 0, ev = 0, ecand = 0, ebk = 0, elen = 0;
-        int eA = 0, eD = 0;
-        bool ended = false;
-        for (;;) {
-            // ---- probe schedule of the batch: pair j of lane (A_j, D_j), and the state after 32 pairs
-            int Aj, Dj;
-            int A32, D32, s32, n32;
-            if (D == 2 && s == 2 && A + 62 < nx) {
-                Aj = A + 2 * j;
-                Dj = 2;
-                A32 = A + 60; D32 = 2; s32 = 2; n32 = nx;
-                pair_step(A32, D32, s32, n32);
-                pair_step(A32, D32, s32, n32);
-            } else {
-                int a = A, d = D, ss = s, nn = nx;
-                for (int i = 0; i < j; i++) pair_step(a, d, ss, nn);
-                Aj = a;
-                Dj = d;
-                pair_step(a, d, ss, nn);
-                A32 = rdlanei(a, 63); D32 = rdlanei(d, 63); s32 = rdlanei(ss, 63); n32 = rdlanei(nn, 63);
-            }
-            const bool valid = j == 0 || Aj + 1 + Dj < ilimit;
-            const uint64_t vmask = ballot(valid);
-            const int q = valid ? Aj + half : A;
-            const int ap = valid ? Aj + Dj : A;                   // the pair's repcode position (ip2)
-            const int pmax = rdlanei(Aj + Dj, 63 - __builtin_clzll(vmask));
-            ZT(0);
-            ZS(9, 1);
-            // ---- P side (ring, else global), hash, table read / claim / read back
-            PW pq, pr;
-            if (Rg.has(A - 4, pmax + 32)) {
-                pq = pw_ring(Rg, q);
-                pr = pw_ring(Rg, ap);
-            } else {
-                ZS(10, 1);
-                ZWin t;
-                t.load(in, q);
-                pq = t.words();
-                t.load(in, ap);
-                pr = t.words();
-            }
-            const uint64_t w8 = (uint64_t)pq.w | ((uint64_t)pq.q0 << 32);
-            const uint32_t h = zhash(w8, P.hlog, P.mls);
-            ZT(1);
-            uint32_t old = 0, back = 0;
-            if (valid) old = T.get(h);
-            T.fence();
-            if (valid) T.claim(h, (uint32_t)q + 1);
-            T.fence();
-            if (valid) back = T.back(h);
-            const uint64_t losers = ballot(valid && back != (((uint32_t)q + 1) & Tab::kBackMask));
-            uint64_t grp = 1ull << lane;
-            int prev = -1;
-            if (losers) {
-                // lanes of one slot read back the same winner: group by equal winner (bit-sliced over
-                // the winner's offset from the batch's first position)
-                const int A0 = rdlanei(Aj, 0);
-                const int span = rdlanei(Aj, 62) + 2 - A0;
-                int nbits = 1;
-                while ((1 << nbits) < span) nbits++;
-                const uint32_t wr = (back - 1u - (uint32_t)A0) & Tab::kBackMask;
-                uint64_t eq = vmask;
-                for (int b = 0; b < nbits; b++) {
-                    const bool wb = (wr >> b) & 1u;
-                    const uint64_t bm = ballot(valid && wb);
-                    eq &= wb ? bm : ~bm;
-                }
-                grp = valid ? eq : grp;
-                const uint64_t eb = grp & below;
-                prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
-            }
-            const int qprev = lane_gather((uint32_t)q, prev < 0 ? lane : prev);
-            const uint32_t cand = prev >= 0 ? (uint32_t)qprev + 1 : old;
-            const bool cok = valid && cand > (uint32_t)pstart;
-            const bool rok = valid && !half && r1 > 0;
-            ZT(2);
-            // ---- candidate and repcode windows: one round trip (the ring's refill lands with it)
-            ZWin wc, wr;
-            wc.d0 = wc.d1 = wc.d2 = wc.d3 = wc.d4 = wc.d5 = wc.d6 = wc.d7 = wc.sm = 0;
-            wr.d0 = wr.d1 = wr.d2 = wr.d3 = wr.d4 = wr.d5 = wr.d6 = wr.d7 = wr.sm = 0;
-            if (cok) wc.load(in, (int)cand - 1);      // (only the lanes that compare: fewer requests)
-            if (rok) wr.load(in, ap - (int)r1);
-            uint32_t pc0 = 0, pc1 = 1;
-            if (pend) { pc0 = in.w32(ip); pc1 = in.w32(ip - (int)r2); }
-            wait_vm_known();
-            Rg.landed();
-            ZT(3);
-            Rg.advance(in.r, A, endX, lane);
-            if (pend) {
-                pend = false;
-                if (pc0 == pc1) {   // the repcode loop runs first: drop the batch, its claims undone
-                    if (valid) T.put(h, old);
-                    T.fence();
-                    kind = -1;
-                    break;
-                }
-            }
-            int bkr, len, rbk, rlen;
-            const bool hit = zeval(pq, wc.words(), bkr, len) && cok;
-            const bool rhit = zeval(pr, wr.words(), rbk, rlen) && rok;
-            const uint64_t R = ballot(rhit), H = ballot(hit), E = R | H;
-            const uint64_t committed = E ? (vmask & (ffs64(E) == 63 ? ~0ull : ((2ull << ffs64(E)) - 1ull))) : vmask;
-            // ---- slots: the value the sequential order leaves
-            if (valid) {
-                const uint64_t gc = grp & committed;
-                bool writer;
-                uint32_t val;
-                if (gc) { writer = lane == 63 - __builtin_clzll(gc); val = (uint32_t)q + 1; }
-                else { writer = lane == ffs64(grp); val = old; }
-                if (writer && (losers || !gc)) T.put(h, val);
-            }
-            T.fence();
-            ZT(4);
-            if (E) {
-                ev = ffs64(E);
-                const bool isr = (R >> ev) & 1ull;
-                kind = (ev & 1) ? 3 : (isr ? 1 : 2);
-                eA = rdlanei(Aj, ev);
-                eD = rdlanei(Dj, ev);
-                ecand = (int)rdlane(cand, ev);
-                ebk = isr ? rdlanei(rbk, ev) : rdlanei(bkr, ev);
-                elen = isr ? rdlanei(rlen, ev) : rdlanei(len, ev);
-                break;
-            }
-            if (vmask != ~0ull || A32 + 1 + D32 >= ilimit) { ended = true; break; }
-            A = A32; D = D32; s = s32; nx = n32;
-        }
-        if (ended) break;
-        if (kind < 0) {
-            rep_loop();
-            ZT(14);
-            continue;
-        }
-        // ---- the match: m0 / p0 its start and source before the backward extension
-        int m0, p0, bmax, cur0, ip1;
-        uint32_t offBase;
-        if (kind == 1) {
-            m0 = eA + eD;
-            p0 = m0 - (int)r1;
-            bmax = 1;                                     // ip0[-1] == match0[-1], zstd_fast.c:178-185
-            offBase = 1;
-            cur0 = eA;
-            ip1 = eA + 1;
-        } else {
-            m0 = kind == 2 ? eA : eA + 1;
-            p0 = ecand - 1;
-            r2 = r1;
-            r1 = (uint32_t)(m0 - p0);
-            offBase = r1 + 3;
-            cur0 = m0;
-            ip1 = kind == 2 ? eA + 1 : eA + eD;
-            bmax = max(0, min(m0 - anchor, p0 - pstart));  // zstd_fast.c:273-278
-        }
-        int bk = min(ebk, bmax);
-        if (ebk == 4 && bmax > 4) { ZS(12, 1); bk = 4 + count_bwd(in, m0 - 4, p0 - 4, bmax - 4, lane); }
-        const int fmax = be - (m0 + 4);                   // ZSTD_count up to iend (zstd_fast.c:283)
-        int fw;
-        if (elen < 20) fw = min(elen, fmax);
-        else { ZS(11, 1); fw = fmax <= 20 ? fmax : 20 + count_fwd(in, m0 + 24, p0 + 24, fmax - 20, lane); }
-        ZT(5);
-        const int mstart = m0 - bk;
-        const int mlen = 4 + bk + fw;
-        if (Rg.has(anchor, mstart + 4)) ring_copy(Rg, anchor, O.lits, O.nl, mstart - anchor, lane);
-        else copy_span(in, anchor, O.lits, O.nl, mstart - anchor, lane, LZH_WAVE);
-        ZT(18);
-        O.nl += mstart - anchor;
-        O.put(lane, (uint32_t)(mstart - anchor), offBase, (uint32_t)mlen);
-        ZT(6);
-        ZS(13, 1);
-        ip = mstart + mlen;
-        anchor = ip;
-        // table fills (zstd_fast.c:291-300) from the ring when it holds the three positions; the
-        // ring's refill for the new front lands at the next batch's wait
-        {
-            const int flo = min(ip1, cur0 + 2), fhi = max(ip1, ip - 2) + 12;
-            uint64_t h1, h2, h3;
-            if (Rg.has(flo, fhi)) {
-                h1 = (uint64_t)Rg.u32(ip1) | ((uint64_t)Rg.u32(ip1 + 4) << 32);
-                h2 = (uint64_t)Rg.u32(cur0 + 2) | ((uint64_t)Rg.u32(cur0 + 6) << 32);
-                h3 = (uint64_t)Rg.u32(ip - 2) | ((uint64_t)Rg.u32(ip + 2) << 32);
-            } else {
-                h1 = ld64(in, ip1); h2 = ld64(in, cur0 + 2); h3 = ld64(in, ip - 2);
-            }
-            ZT(16);
-            if (lane == 0) {
-                if (ip1 < ip) T.put(zhash(h1, P.hlog, P.mls), (uint32_t)ip1 + 1);
-                if (ip <= ilimit) {
-                    T.put(zhash(h2, P.hlog, P.mls), (uint32_t)cur0 + 3);
-                    T.put(zhash(h3, P.hlog, P.mls), (uint32_t)ip - 1);
-                }
-            }
-            T.fence();
-            ZT(17);
-            Rg.advance(in.r, ip, endX, lane);   // (after the fills: no compiler wait then sees the DMA)
-            pend = ip <= ilimit && r2 > 0;
-        }
-        ZT(7);
-    }
-    rep[0] = r1 ? r1 : saved;
-    rep[1] = r2 ? r2 : saved;
-    if (Rg.has(anchor, be + 4)) ring_copy(Rg, anchor, O.lits, O.nl, be - anchor, lane);   // last literals
-    else copy_span(in, anchor, O.lits, O.nl, be - anchor, lane, LZH_WAVE);
-    O.nl += be - anchor;
-#if LZH_ZSTDC_STATS
-    zst[15] += 1;
-    if (lane == 0)
-        for (int i = 0; i < 24; i++) atomicAdd(&lzh_zstdc_stats_buf[i], (unsigned long long)zst[i]);
-#endif
-}
 
 }  // namespace zc
 
@@ -961,19 +559,14 @@ lzh_zstd_match_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable,
     if (k > 0) { rep[0] = uni(ld_b32(hdr, 16)); rep[1] = uni(ld_b32(hdr, 20)); }
     const uint32_t tbytes = 4u << P.hlog;
     const uint32_t nent = 1u << P.hlog;
-    // lds_arg: table bytes in LDS, bit 31 = an input ring follows them (the launch sizes the
-    // dynamic LDS for both)
-    const uint32_t lds_table_bytes = lds_arg & 0x7fffffffu;
-    const bool ring = (lds_arg >> 31) != 0;
-    ZRing Rg{(LDSA uint32_t*)((LDSA uint8_t*)zlds + ((lds_table_bytes + 15u) & ~15u)), in_b.sh, 0, 0, 0};
+    const uint32_t lds_table_bytes = lds_arg;          // the table's bytes in dynamic LDS (0: global)
     const uint32_t bmb = max(nent / 8u, 4u);            // LdsTab17 bitmap bytes
     if (LZH_ZSTD_TAB17 && chunk_size <= 131072u && nblocks == 1 && 2u * nent + bmb <= lds_table_bytes) {
         // (single-block frames: the table starts empty and is not saved)
         LdsTab17 T{(LDSA uint16_t*)zlds, (LDSA uint32_t*)((LDSA uint8_t*)zlds + 2 * nent)};
         for (uint32_t i = lane; i < (2u * nent + bmb) / 4u; i += 64) ((volatile LDSA uint32_t*)zlds)[i] = 0u;
         T.fence();
-        if (LZH_ZSTD_RING && ring) fast_block2(T, Rg, in_b, P, bs, be, rep, O, lane);
-        else if (P.mls == 6) fast_block<6>(T, in_b, P, bs, be, rep, O, lane);   // (hash fixed at compile time)
+        if (P.mls == 6) fast_block<6>(T, in_b, P, bs, be, rep, O, lane);   // (hash fixed at compile time)
         else if (P.mls == 5) fast_block<5>(T, in_b, P, bs, be, rep, O, lane);
         else fast_block(T, in_b, P, bs, be, rep, O, lane);
     } else if (chunk_size < (16u << 20) && 3u * nent <= lds_table_bytes) {
@@ -981,8 +574,7 @@ lzh_zstd_match_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable,
         rsrc_t save = make_rsrc(fs + tab_off, tbytes);
         for (uint32_t i = lane; i < nent; i += 64) T.put(i, k == 0 ? 0u : ld_b32(save, (int)(i * 4)));
         T.fence();
-        if (LZH_ZSTD_RING && ring) fast_block2(T, Rg, in_b, P, bs, be, rep, O, lane);
-        else fast_block(T, in_b, P, bs, be, rep, O, lane);
+        fast_block(T, in_b, P, bs, be, rep, O, lane);
         if ((uint64_t)k + 1 < nblocks)
             for (uint32_t i = lane; i < nent; i += 64) st_b32(save, (int)(i * 4), T.get(i));
     } else if (tbytes <= lds_table_bytes) {
@@ -990,8 +582,7 @@ lzh_zstd_match_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable,
         rsrc_t save = make_rsrc(fs + tab_off, tbytes);
         for (uint32_t i = lane; i < tbytes / 4; i += 64) T.put(i, k == 0 ? 0u : ld_b32(save, (int)(i * 4)));
         T.fence();
-        if (LZH_ZSTD_RING && ring) fast_block2(T, Rg, in_b, P, bs, be, rep, O, lane);
-        else fast_block(T, in_b, P, bs, be, rep, O, lane);
+        fast_block(T, in_b, P, bs, be, rep, O, lane);
         if ((uint64_t)k + 1 < nblocks)
             for (uint32_t i = lane; i < tbytes / 4; i += 64) st_b32(save, (int)(i * 4), T.get(i));
     } else {
@@ -1000,8 +591,7 @@ lzh_zstd_match_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable,
             for (uint32_t i = lane; i < tbytes / 4; i += 64) T.put(i, 0u);
             T.fence();
         }
-        if (LZH_ZSTD_RING && ring) fast_block2(T, Rg, in_b, P, bs, be, rep, O, lane);
-        else fast_block(T, in_b, P, bs, be, rep, O, lane);
+        fast_block(T, in_b, P, bs, be, rep, O, lane);
     }
     if (lane == 0) {
         st_b32(hdr, 0, (uint32_t)O.ns);
@@ -2193,13 +1783,10 @@ hipError_t lzh_launch_zstd_compress(const uint8_t* in, uint64_t n_total, uint64_
     const uint32_t t17 = (2u << PF.hlog) + std::max((1u << PF.hlog) / 8u, 4u);
     const uint32_t lds_tab = (4u << PF.hlog) > (uint32_t)LZH_ZSTD_LDS_MAX ? 0u
                              : (LZH_ZSTD_TAB17 && chunk_size <= 131072u) ? ((t17 + 15u) & ~15u) : (ebytes << PF.hlog);
-    // (the ring only where table + ring fit the 64 KiB a launch gets without an attribute)
-    const bool ring = LZH_ZSTD_RING && ((lds_tab + 15u) & ~15u) + (uint32_t)zc::kZRingLds <= 65536u;
-    const uint32_t lds_all = ring ? ((lds_tab + 15u) & ~15u) + (uint32_t)zc::kZRingLds : lds_tab;
     for (uint32_t k = 0; k < std::max(nblocks, 1u); k++) {
-        hipLaunchKernelGGL(lzh_zstd_match_kernel, dim3(nchunks), dim3(64), lds_all, s, in, n_total, in_readable,
+        hipLaunchKernelGGL(lzh_zstd_match_kernel, dim3(nchunks), dim3(64), lds_tab, s, in, n_total, in_readable,
                            chunk_size, level, (int)k, scratch, (uint64_t)fstride, Lo.seq_off, Lo.lit_off, Lo.tab_off,
-                           lds_tab | (ring ? 0x80000000u : 0u));
+                           lds_tab);
         hipLaunchKernelGGL(lzh_zstd_entropy_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable,
                            chunk_size, level, (int)k, scratch, (uint64_t)fstride, Lo.seq_off, Lo.lit_off, Lo.att_off,
                            Lo.tmp_off, stage, stride, csizes);

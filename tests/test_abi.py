@@ -126,6 +126,27 @@ def test_batched_row_plan_arithmetic(ngpus, n, chunk):
         assert p["sb_temp"] < (256 << 20)
 
 
+@pytest.mark.parametrize("nsb,seed", [(1, 0), (2, 1), (7, 2), (16, 3), (64, 4)])
+def test_gather_places_each_sub_batch_as_soon_as_its_offset_is_known(nsb, seed):
+    """api.cpp GatherOrder (the batched rows' host gather, polled over every shard's sub-batches):
+    whatever order the sub-batches finish in, each is copied out at the exclusive prefix sum of the
+    packed sizes (lzbench.cpp:266-298 packing), in chunk order, and at the first completion after
+    which it and everything before it are known -- never later."""
+    rng = np.random.default_rng(seed)
+    order = rng.permutation(nsb).astype(np.uint64)
+    sizes = rng.integers(0, 1 << 27, nsb).astype(np.uint64)
+    placed = np.zeros(3 * nsb, np.uint64)
+    lib = L.lib()
+    m = lib.lzh_debug_gather_order(nsb, order.ctypes.data, sizes.ctypes.data, placed.ctypes.data)
+    assert m == nsb
+    pl = placed.reshape(-1, 3)
+    assert pl[:, 0].tolist() == list(range(nsb))
+    assert pl[:, 1].tolist() == np.concatenate([[0], np.cumsum(sizes)[:-1]]).tolist()
+    pos = np.empty(nsb, np.int64)
+    pos[order.astype(np.int64)] = np.arange(nsb)
+    assert pl[:, 2].tolist() == np.maximum.accumulate(pos).tolist()
+
+
 def test_level_supported():
     lib = L.lib()
     assert lib.lzh_level_supported(3, 1, 1 << 20) == 1          # zstd 1: fast strategy at every size

@@ -1,4 +1,4 @@
-"""tools/zstdc_stats.py -- event counters and phase clocks of the zstd match finder (fast_block2).
+"""tools/zstdc_stats.py -- phase clocks of the zstd entropy kernel (lane 0 of every frame, stamps 16..22).
 Needs a -DLZH_ZSTDC_STATS=1 build: tools/exp_build.sh zst "-DLZH_ZSTDC_STATS=1", then
 LZH_LIB=build/exp/zst/liblzbench_hip.so python tools/zstdc_stats.py [corpus] [chunk_kib] [mib]"""
 import ctypes as C, os, sys
@@ -23,14 +23,7 @@ dc.compress_kernel_only(d_in)
 torch.cuda.synchronize()
 assert f(buf, 0) == 0
 v = list(buf)
-blocks = max(v[15], 1)
-names = {9: "batches", 10: "pside_global", 11: "fwd_slow", 12: "bwd_slow", 13: "sequences"}   # (ring parse only)
-print(corpus, chunk >> 10, "KiB per block:", {k: round(v[i] / blocks, 1) for i, k in names.items()})
+blocks = max(n // chunk, 1)
 ze = {16: "lit_histo", 17: "huf_tree", 18: "huf_streams", 19: "seq_histo", 20: "fse_tables", 21: "seq_chains", 22: "seq_packing"}
 zt = sum(v[i] for i in ze) or 1
-print("  entropy clocks/block %.0f:" % (zt / blocks), {k: "%.1f%%" % (100 * v[i] / zt) for i, k in ze.items()})
-ph = {0: "schedule", 1: "pside+hash", 2: "table+groups", 3: "window_wait", 4: "eval+restore", 5: "match_finish",
-      6: "literals+record", 7: "fills", 8: "loop/other", 14: "rep_loop", 16: "fills_loads", 17: "fills_puts", 18: "lit_copy"}
-tot = sum(v[i] for i in ph) or 1
-print("  clocks/block %.0f, per sequence %.0f:" % (tot / blocks, tot / max(v[13], 1)),
-      {k: "%.1f%%" % (100 * v[i] / tot) for i, k in ph.items()})
+print(corpus, chunk >> 10, "KiB:", "entropy clocks/block %.0f:" % (zt / blocks), {k: "%.1f%%" % (100 * v[i] / zt) for i, k in ze.items()})
