@@ -1,7 +1,7 @@
 /*
  * oracle/frame_oracle.c -- the framed LZ4 formats restated in C.  TEST INFRASTRUCTURE ONLY.
  *
- * 1. LZ4 frame (lz4frame.c 1.9.3) as LZ4F_compressFrame writes it with independent blocks:
+ * 1. LZ4 frame (lz4frame.c 1.9.3) as LZ4F_compressFrame writes it, blocks independent or linked:
  *      LZ4F_compressFrame_usingCDict  /root/reference/lz4/lz4frame.c:373-419 (optimal block size,
  *                                     autoFlush, single-block frames independent)
  *      LZ4F_optimalBSID               lz4frame.c:304-316
@@ -17,7 +17,19 @@
  *    sequence layout, because the parse does not: the notLimited block is produced and its tokens
  *    are walked with the same conditions (the match-length check at every sequence implies the
  *    literal check, so it and the last-literals check decide).
- *    Decoding restates LZ4F_decompress (lz4frame.c:1384-1899) for one whole frame.
+ *    Linked blocks (LZ4F_blockLinked, the LZ4F default; params flag 0x80): LZ4F_compressBegin resets
+ *    the stream once per frame (lz4frame.c:651-655, LZ4F_initStream -> LZ4_resetStream_fast), and every
+ *    block goes through LZ4F_compressBlock_continue -> LZ4_compress_fast_continue (lz4frame.c:777-782,
+ *    lz4.c:1565-1628).  The blocks lie back to back in the caller's buffer (stableSrc), so each one is
+ *    compressed in prefix mode: LZ4_compress_generic with byU32 / hash5, withPrefix64k, noDictIssue and
+ *    limitedOutput (lz4.c:851-1240): positions are frame indices (base = the frame start, the table
+ *    persists from block to block), candidates reach up to 65535 bytes back into earlier blocks, the
+ *    catch-up stops at the frame start (lowLimit = source - dictSize), and a block that does not fit
+ *    size - 1 bytes returns 0 where the first check fails (lz4.c:1024-1027, :1097-1121, :1207-1216),
+ *    leaving the table as it stands there for the next block (restated inline: lz4f_linked_block).
+ *    Decoding restates LZ4F_decompress (lz4frame.c:1384-1899) for one whole frame; a linked block
+ *    decodes with everything decoded before it in the frame as its prefix (LZ4F_updateDict's prefix
+ *    mode, lz4frame.c:1290-1306, and LZ4_decompress_safe_usingDict, lz4.c:2404-2416).
  * 2. The nvcomp LZ4 container (nvcomp 1.2.2, the reference's nvcomp_lz4 row): 8-byte fields
  *      [LZ4_FLAG = 4, metadata bytes M = (4 + k + 1) * 8, uncompressed size, chunk size,
  *       offsets[0..k]] (nvcomp/LZ4Metadata.h:39-60, MutableLZ4MetadataOnGPU.cpp copyToGPU,
@@ -96,6 +108,97 @@ static int limited_fails(const uint8_t* blk, int bs, int cap) {
     return 0;
 }
 
+static uint32_t lz4f_h5(const uint8_t* p) {   /* LZ4_hash5 for byU32 (lz4.c:706-722) */
+    const uint64_t v = (uint64_t)rd32(p) | (uint64_t)rd32(p + 4) << 32;
+    return (uint32_t)(((v << 24) * 889523592379ull) >> 52);
+}
+
+static int lz4f_put_len(uint8_t* dst, int op, int len) {
+    while (len >= 255) { dst[op++] = 255; len -= 255; }
+    dst[op++] = (uint8_t)len;
+    return op;
+}
+
+/* One block of a linked frame: f = the frame, the block = [b0, b0 + n), t = the frame's table
+ * (4096 u32 indices, zeroed at the frame start).  LZ4_compress_generic's prefix-mode parse with the
+ * limitedOutput checks at their places (olimit = cap = n - 1); returns the block size or 0. */
+static int lz4f_linked_block(uint32_t* t, const uint8_t* f, int b0, int n, uint8_t* dst, int acc) {
+    const int cap = n - 1, iend = b0 + n, mfl1 = iend - 12 + 1, mlimit = iend - 5;
+    int ip = b0, anchor = b0, op = 0;
+    uint32_t fh;
+    if (n < 13) goto last_literals;                       /* lz4.c:921 */
+    t[lz4f_h5(f + b0)] = (uint32_t)b0;                    /* first byte (lz4.c:924-925) */
+    ip = b0 + 1;
+    fh = lz4f_h5(f + ip);
+    for (;;) {
+        int match, tok;
+        {   /* probe loop (lz4.c:954-1014) */
+            int fwd = ip, step = 1, nb = acc << 6;
+            for (;;) {
+                const uint32_t h = fh;
+                const int cur = fwd;
+                const uint32_t cand = t[h];
+                ip = fwd;
+                fwd += step;
+                step = nb++ >> 6;
+                if (fwd > mfl1) goto last_literals;
+                fh = lz4f_h5(f + fwd);
+                t[h] = (uint32_t)cur;
+                if (cand + 65535u < (uint32_t)cur) continue;             /* too far (lz4.c:1003) */
+                if (rd32(f + cand) == rd32(f + ip)) { match = (int)cand; break; }
+            }
+        }
+        /* catch up, down to the frame start (lowLimit = source - dictSize, lz4.c:1019) */
+        while (ip > anchor && match > 0 && f[ip - 1] == f[match - 1]) { ip--; match--; }
+        {   /* literals, with the limitedOutput check (lz4.c:1024-1027) */
+            const int lit = ip - anchor;
+            tok = op++;
+            if (op + lit + 8 + lit / 255 > cap) return 0;
+            if (lit >= 15) { dst[tok] = 15 << 4; op = lz4f_put_len(dst, op, lit - 15); }
+            else dst[tok] = (uint8_t)(lit << 4);
+            memcpy(dst + op, f + anchor, (size_t)lit);
+            op += lit;
+        }
+    next_match:
+        {
+            const int off = ip - match;
+            dst[op++] = (uint8_t)(off & 0xff);
+            dst[op++] = (uint8_t)(off >> 8);
+            int ml = 0;                                                  /* LZ4_count to matchlimit */
+            while (ip + 4 + ml < mlimit && f[ip + 4 + ml] == f[match + 4 + ml]) ml++;
+            ip += ml + 4;
+            if (op + 6 + (ml + 240) / 255 > cap) return 0;              /* lz4.c:1097-1121 */
+            if (ml >= 15) { dst[tok] = (uint8_t)(dst[tok] + 15); op = lz4f_put_len(dst, op, ml - 15); }
+            else dst[tok] = (uint8_t)(dst[tok] + ml);
+        }
+        anchor = ip;
+        if (ip >= mfl1) break;                                           /* lz4.c:1142 */
+        t[lz4f_h5(f + ip - 2)] = (uint32_t)(ip - 2);                     /* lz4.c:1146 */
+        {   /* immediate re-test (lz4.c:1159-1196): no literal check on this path */
+            const uint32_t h = lz4f_h5(f + ip), cand = t[h];
+            t[h] = (uint32_t)ip;
+            if (cand + 65535u >= (uint32_t)ip && rd32(f + cand) == rd32(f + ip)) {
+                match = (int)cand;
+                tok = op++;
+                dst[tok] = 0;
+                goto next_match;
+            }
+        }
+        ip++;
+        fh = lz4f_h5(f + ip);
+    }
+last_literals:
+    {   /* lz4.c:1204-1231 */
+        const int run = iend - anchor;
+        if (op + run + 1 + (run + 240) / 255 > cap) return 0;
+        if (run >= 15) { dst[op++] = 15 << 4; op = lz4f_put_len(dst, op, run - 15); }
+        else dst[op++] = (uint8_t)(run << 4);
+        memcpy(dst + op, f + anchor, (size_t)run);
+        op += run;
+    }
+    return op;
+}
+
 size_t oracle_lz4f_bound(size_t n, int params) {
     const size_t B = bsid_size(optimal_bsid(params & 7, n));
     const size_t nb = (n + B - 1) / B;
@@ -107,21 +210,31 @@ int64_t oracle_lz4f_compress(const uint8_t* src, size_t n, uint8_t* dst, int par
     const int bcrc = (params & 0x10) != 0, ccrc = (params & 0x20) != 0, csz = (params & 0x40) && n > 0;
     const int acc = (params >> 8) & 0xff;
     const size_t B = bsid_size(bsid);
+    /* a frame of one block is independent whatever was asked (lz4frame.c:394-395) */
+    const int linked = (params & 0x80) && n > B;
     uint8_t* o = dst;
     wr32(o, 0x184D2204u);
     o += 4;
     uint8_t* hs = o;
-    *o++ = (uint8_t)((1 << 6) | (1 << 5) | (bcrc << 4) | (csz << 3) | (ccrc << 2));
+    *o++ = (uint8_t)((1 << 6) | ((!linked) << 5) | (bcrc << 4) | (csz << 3) | (ccrc << 2));
     *o++ = (uint8_t)((bsid & 7) << 4);
     if (csz) { wr64(o, (uint64_t)n); o += 8; }
     *o = (uint8_t)((oracle_xxh32(hs, (size_t)(o - hs), 0) >> 8) & 0xff);
     o++;
     uint8_t* tmp = (uint8_t*)malloc((size_t)oracle_lz4_bound((int)B) + 64);
+    uint32_t* tab = linked ? (uint32_t*)calloc(4096, sizeof(uint32_t)) : NULL;
     for (size_t p = 0; p < n; p += B) {
         const int bs = (int)(n - p < B ? n - p : B);
-        const int c = oracle_lz4_compress(src + p, bs, tmp, acc < 1 ? 1 : acc);
+        int c, raw;
+        if (linked) {
+            c = lz4f_linked_block(tab, src, (int)p, bs, tmp, acc < 1 ? 1 : acc);
+            raw = c == 0;
+        } else {
+            c = oracle_lz4_compress(src + p, bs, tmp, acc < 1 ? 1 : acc);
+            raw = limited_fails(tmp, c, bs - 1);
+        }
         uint32_t cs;
-        if (limited_fails(tmp, c, bs - 1)) {
+        if (raw) {
             cs = (uint32_t)bs;
             wr32(o, cs | 0x80000000u);
             memcpy(o + 4, src + p, (size_t)bs);
@@ -134,6 +247,7 @@ int64_t oracle_lz4f_compress(const uint8_t* src, size_t n, uint8_t* dst, int par
         o += 4 + cs + 4 * bcrc;
     }
     free(tmp);
+    free(tab);
     wr32(o, 0);
     o += 4;
     if (ccrc) { wr32(o, oracle_xxh32(src, n, 0)); o += 4; }
@@ -142,7 +256,8 @@ int64_t oracle_lz4f_compress(const uint8_t* src, size_t n, uint8_t* dst, int par
 
 /* LZ4F_decompress over one whole frame (lz4frame.c:1384-1899: header decode :1150-1260 with its
  * checks, block loop, block / content checksums); returns the decoded size, -1 on malformed input,
- * -2 for a dictionary id or a second linked block (not restated; the GPU decoder refuses them too) */
+ * -2 for a dictionary id (not restated; the GPU decoder refuses it too).  A linked frame's blocks
+ * decode with the frame's output so far as their prefix. */
 int64_t oracle_lz4f_decompress(const uint8_t* src, size_t cs, uint8_t* dst, size_t cap) {
     if (cs < 7 || rd32(src) != 0x184D2204u) return -1;
     const uint32_t flg = src[4], bd = src[5];
@@ -162,7 +277,6 @@ int64_t oracle_lz4f_decompress(const uint8_t* src, size_t cs, uint8_t* dst, size
         const uint32_t w = rd32(src + ip);
         ip += 4;
         if (w == 0) break;
-        if (nb > 0 && !(flg & 0x20)) return -2;   /* linked blocks past the first: not restated */
         const uint32_t sz = w & 0x7fffffffu;
         if (sz > B || ip + sz + 4u * (uint32_t)bcrc > cs) return -1;
         if (bcrc && rd32(src + ip + sz) != oracle_xxh32(src + ip, sz, 0)) return -1;
@@ -172,7 +286,10 @@ int64_t oracle_lz4f_decompress(const uint8_t* src, size_t cs, uint8_t* dst, size
             op += sz;
         } else {
             const size_t room = cap - op < B ? cap - op : B;
-            const int d = oracle_lz4_decompress_safe(src + ip, (int)sz, dst + op, (int)room);
+            /* linked: LZ4_decompress_safe_usingDict with the prefix dst[0, op) (withPrefix64k from the
+             * second block on, every earlier block being full: no offset reaches past it) */
+            const int d = (flg & 0x20) ? oracle_lz4_decompress_safe(src + ip, (int)sz, dst + op, (int)room)
+                                       : oracle_lz4_decompress_prefix(src + ip, (int)sz, dst + op, (int)room, (int64_t)op);
             if (d < 0) return -1;
             op += (size_t)d;
         }

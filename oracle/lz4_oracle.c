@@ -149,6 +149,13 @@ last_literals:
 /* ---------------------------------------------------------------- decoder */
 
 int oracle_lz4_decompress_safe(const uint8_t* src, int csize, uint8_t* dst, int cap) {
+    return oracle_lz4_decompress_prefix(src, csize, dst, cap, 0);
+}
+
+/* the same with `prefix` bytes of earlier output before dst that matches may reach into
+ * (LZ4_decompress_safe_usingDict in prefix mode, lz4.c:2404-2416; the offset check of
+ * LZ4_decompress_generic then fails only below dst - prefix, :1915-1917) */
+int oracle_lz4_decompress_prefix(const uint8_t* src, int csize, uint8_t* dst, int cap, int64_t prefix) {
     int64_t ip = 0, op = 0;
     const int64_t iend = csize, oend = cap;
     if (cap == 0) return (csize == 1 && src[0] == 0) ? 0 : -1;
@@ -191,7 +198,7 @@ int oracle_lz4_decompress_safe(const uint8_t* src, int csize, uint8_t* dst, int 
             } while (s == 255);
         }
         ml += LZ4O_MINMATCH;
-        if (off > op) return (int)(-ip - 1);                 /* offset before block start */
+        if (off > op + prefix) return (int)(-ip - 1);        /* offset before block (or prefix) start */
         if (op + ml > oend - LZ4O_LASTLITERALS) return (int)(-ip - 1);  /* last 5 bytes are literals */
         if (off == 0) { memset(dst + op, 0, (size_t)ml); op += ml; continue; }
         /* forward byte copy reproduces overlapping-match (offset < length) semantics */

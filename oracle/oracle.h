@@ -28,6 +28,7 @@ int oracle_lz4_bound(int n);
 /* LZ4_decompress_safe semantics (reference lz4/lz4.c:1737-2165 safe loop, :2170-2176).
  * Returns decoded size, or a negative value on malformed input. */
 int oracle_lz4_decompress_safe(const uint8_t* src, int csize, uint8_t* dst, int cap);
+int oracle_lz4_decompress_prefix(const uint8_t* src, int csize, uint8_t* dst, int cap, int64_t prefix);
 
 /* snappy::RawCompress (reference snappy/snappy.cc:1043-1111, :510-681). Returns bytes written. */
 size_t oracle_snappy_compress(const uint8_t* src, size_t n, uint8_t* dst);

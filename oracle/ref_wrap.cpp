@@ -14,7 +14,8 @@
  *   zstd adapters      /root/reference/_lzbench/compressors.cpp:1745-1778 (codec 2: ZSTD_getParams(level,
  *                      part, 0), contentSizeFlag = 1, ZSTD_compress_advanced; ZSTD_decompressDCtx)
  *   codec 3            one LZ4 frame per chunk: LZ4F_compressFrame (lz4/lz4frame.c:429-470) with
- *                      independent blocks and the requested block size / checksums / content size;
+ *                      independent or linked blocks and the requested block size / checksums /
+ *                      content size;
  *                      LZ4F_decompress (lz4frame.c:1384) over the whole frame
  *   codec 4            one nvcomp LZ4 container per chunk (nvcomp/LZ4Metadata.h layout, restated as in
  *                      oracle/frame_oracle.c: nvcomp itself cannot be built) around reference
@@ -76,12 +77,13 @@ int64_t ref_zstd_decompress(const char* in, size_t csize, char* out, size_t cap)
 int ref_zstd_version(void) { return (int)ZSTD_versionNumber(); }
 
 /* params as oracle_lz4f_compress: bits 0-2 blockSizeID (0 default), 0x10 block checksum, 0x20 content
- * checksum, 0x40 content size, bits 8-15 acceleration (compressionLevel = -(acc - 1)) */
+ * checksum, 0x40 content size, 0x80 linked blocks (LZ4F_blockLinked, the LZ4F default), bits 8-15
+ * acceleration (compressionLevel = -(acc - 1)) */
 static LZ4F_preferences_t lz4f_prefs(size_t n, int params) {
     LZ4F_preferences_t p;
     memset(&p, 0, sizeof(p));
     p.frameInfo.blockSizeID = (LZ4F_blockSizeID_t)(params & 7);
-    p.frameInfo.blockMode = LZ4F_blockIndependent;
+    p.frameInfo.blockMode = (params & 0x80) ? LZ4F_blockLinked : LZ4F_blockIndependent;
     p.frameInfo.blockChecksumFlag = (params & 0x10) ? LZ4F_blockChecksumEnabled : LZ4F_noBlockChecksum;
     p.frameInfo.contentChecksumFlag = (params & 0x20) ? LZ4F_contentChecksumEnabled : LZ4F_noContentChecksum;
     p.frameInfo.contentSize = (params & 0x40) ? (unsigned long long)n : 0;

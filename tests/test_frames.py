@@ -9,7 +9,8 @@ import oracle_lib as O
 import lzbench_amd as L
 
 SIZES = [0, 1, 5, 12, 13, 100, 4095, 4096, 65535, 65536, 65537, 65547, 200000, 262145, (1 << 20) + 17]
-PARAMS = [0, 4, 5, 6, 7, 0x10, 0x20, 0x40, 0x74, 0x300, 0x1104, 0x77]
+PARAMS = [0, 4, 5, 6, 7, 0x10, 0x20, 0x40, 0x74, 0x300, 0x1104, 0x77,
+          0x80, 0x84, 0x85, 0xF4, 0x380, 0x1184]          # 0x80: linked blocks (the LZ4F default)
 
 
 def _frame(fn, data, params, cap):
@@ -61,6 +62,54 @@ def test_lz4f_raw_block_boundary():
         assert a == b
 
 
+def _near_limit_blocks(rng, nblocks, bs=65536):
+    """Blocks whose LZ4 size lands near the raw limit (bs - 1): random bytes with copies of earlier
+    bytes spliced in at a per-block density, some copies reaching back into the previous block."""
+    d = rng.integers(0, 256, nblocks * bs + int(rng.integers(0, 5000)), dtype=np.uint8)
+    for b in range(nblocks):
+        for _ in range(int(rng.integers(150, 330))):
+            dst = b * bs + int(rng.integers(8, bs - 8))
+            src = dst - int(rng.integers(4, 65535 if rng.random() < 0.2 else 4000))
+            if src >= 0:
+                ln = int(rng.integers(8, 17))
+                d[dst:dst + ln] = d[src:src + ln].copy()
+    return d
+
+
+def test_lz4f_linked_raw_decisions_vs_reference():
+    """Linked frames whose blocks barely do or do not fit size - 1 bytes: a block that fails is stored
+    raw and the parse stopped where the first limitedOutput check failed -- the next block starts from
+    the table as it stood there (lz4.c:1024-1027, :1097-1121, :1207-1216), so the following blocks'
+    bytes pin the abort point."""
+    if not O.have_ref():
+        pytest.skip("reference build not present")
+    R, orc = O.ref(), O.oracle()
+    rng = np.random.default_rng(17)
+    raw = comp = 0
+    for t in range(60):
+        d = _near_limit_blocks(rng, int(rng.integers(2, 6)))
+        for p in (0x80, 0x90):
+            cap = int(R.ref_lz4f_bound(len(d), p)) + 64
+            a = _frame(R.ref_lz4f_compress, d, p, cap)
+            b = _frame(orc.oracle_lz4f_compress, d, p, max(cap, int(orc.oracle_lz4f_bound(len(d), p))) + 64)
+            assert a == b, (t, hex(p))
+            o = np.zeros(len(d) + 64, np.uint8)
+            ab = np.frombuffer(a, np.uint8).copy()
+            assert orc.oracle_lz4f_decompress(ab.ctypes.data, len(a), o.ctypes.data, len(d) + 64) == len(d)
+            assert (o[:len(d)] == d).all()
+            # count raw / compressed blocks (both must occur for the test to mean something)
+            ip = 7
+            while True:
+                w = int.from_bytes(a[ip:ip + 4], "little")
+                ip += 4
+                if w == 0:
+                    break
+                raw += w >> 31
+                comp += 1 - (w >> 31)
+                ip += (w & 0x7fffffff) + (4 if p & 0x10 else 0)
+    assert raw > 20 and comp > 20, (raw, comp)
+
+
 def test_nvlz4_oracle_vs_reference():
     if not O.have_ref():
         pytest.skip("reference build not present")
@@ -91,8 +140,8 @@ def test_lz4f_decode_verdicts_vs_reference():
     n = 70000
     data = L.datagen("text", n, seed=9)
     checked = 0
-    for t in range(600):
-        p = int(rng.choice([0, 0x10, 0x20, 0x40, 0x70, 5]))
+    for t in range(900):
+        p = int(rng.choice([0, 0x10, 0x20, 0x40, 0x70, 5, 0x80, 0xB0]))
         good = _frame(R.ref_lz4f_compress, data, p, int(R.ref_lz4f_bound(n, p)) + 64)
         bad = np.frombuffer(F.corrupt(rng, good), np.uint8).copy()
         o1, o2 = np.zeros(n + 64, np.uint8), np.zeros(n + 64, np.uint8)
@@ -104,4 +153,4 @@ def test_lz4f_decode_verdicts_vs_reference():
         assert (x >= 0) == (y >= 0), (t, x, y)
         if x >= 0:
             assert x == y and (o1[:x] == o2[:y]).all()
-    assert checked > 500
+    assert checked > 800
