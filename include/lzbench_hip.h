@@ -64,6 +64,7 @@ enum { LZH_CODEC_LZ4 = 0, LZH_CODEC_SNAPPY = 1, LZH_CODEC_MEMCPY = 2, LZH_CODEC_
 #define LZH_LZ4F_BLOCK_CHECKSUM   0x10   /* LZ4F_blockChecksumEnabled */
 #define LZH_LZ4F_CONTENT_CHECKSUM 0x20   /* LZ4F_contentChecksumEnabled */
 #define LZH_LZ4F_CONTENT_SIZE     0x40   /* frameInfo.contentSize = chunk size */
+#define LZH_LZ4F_LINKED           0x80   /* LZ4F_blockLinked (the LZ4F default; frames of one block stay independent) */
 #define LZH_LZ4F_PARAMS(bsid, flags, acc) ((bsid) | (flags) | ((acc) << 8))
 enum { LZH_OK = 0, LZH_EARG = -1, LZH_EHIP = -2, LZH_ESPACE = -3, LZH_ECORRUPT = -4 };
 

@@ -24,7 +24,8 @@ __all__ = [
     "ExtensionMissing", "lib", "CODECS", "COMP_DESC", "CompressorDesc", "find_compressor",
     "compress_chunks", "decompress_chunks", "chunk_sizes_for", "datagen", "DeviceCodec",
     "LZH_CODEC_LZ4", "LZH_CODEC_SNAPPY", "LZH_CODEC_MEMCPY", "LZH_CODEC_ZSTD", "LZH_CODEC_LZ4F", "LZH_CODEC_NVLZ4",
-    "LZ4F_BLOCK_CHECKSUM", "LZ4F_CONTENT_CHECKSUM", "LZ4F_CONTENT_SIZE", "PAD_SIZE", "get_compress_bound",
+    "LZ4F_BLOCK_CHECKSUM", "LZ4F_CONTENT_CHECKSUM", "LZ4F_CONTENT_SIZE", "LZ4F_LINKED", "PAD_SIZE",
+    "get_compress_bound",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -37,7 +38,7 @@ CODECS = {"lz4": LZH_CODEC_LZ4, "lz4fast": LZH_CODEC_LZ4, "snappy": LZH_CODEC_SN
           "zstd": LZH_CODEC_ZSTD, "zstd_fast": LZH_CODEC_ZSTD, "lz4frame": LZH_CODEC_LZ4F,
           "nvcomp_lz4": LZH_CODEC_NVLZ4}
 # LZ4 frame parameters (include/lzbench_hip.h LZH_LZ4F_*): level = bsid | flags | acceleration << 8
-LZ4F_BLOCK_CHECKSUM, LZ4F_CONTENT_CHECKSUM, LZ4F_CONTENT_SIZE = 0x10, 0x20, 0x40
+LZ4F_BLOCK_CHECKSUM, LZ4F_CONTENT_CHECKSUM, LZ4F_CONTENT_SIZE, LZ4F_LINKED = 0x10, 0x20, 0x40, 0x80
 # codecs whose level is passed through as is (the others: 1 for lz4 = LZ4_compress_default, 0)
 _LEVELED = ("lz4fast", "zstd", "zstd_fast", "lz4frame", "nvcomp_lz4")
 PAD_SIZE = 16 * 1024          # lzbench.h:14

@@ -92,7 +92,7 @@ static size_t frame_block_bytes(int codec, int level) {
 }
 
 static bool frame_level_ok(int codec, int level) {
-    if (codec == LZH_CODEC_LZ4F) { const int id = level & 7; return level >= 0 && level < (1 << 16) && (id == 0 || id >= 4) && !(level & 0x88); }
+    if (codec == LZH_CODEC_LZ4F) { const int id = level & 7; return level >= 0 && level < (1 << 16) && (id == 0 || id >= 4) && !(level & 0x08); }
     return level >= 0 && level <= 5;
 }
 
@@ -208,8 +208,17 @@ int lzh_compress_kernel_stage(int codec, int level, int stage_mask, const void* 
         uint8_t* base = (uint8_t*)d_stage;
         uint32_t* bcs = (uint32_t*)(base + t.bcs);
         const int acc = codec == LZH_CODEC_LZ4F ? std::max(1, (level >> 8) & 0xff) : 1;
-        LZH_CHECK(lzh_launch_lz4_split((const uint8_t*)d_in, n, in_readable, g.bs, acc, base + t.stage, t.stride, bcs,
-                                       (uint32_t)g.nblocks, base + t.recs, stage_mask, s, g.F, g.bpf));
+        if (codec == LZH_CODEC_LZ4F && (level & LZH_LZ4F_LINKED)) {
+            // linked blocks: one wave per frame walks its blocks in order (the records area holds the
+            // per-frame table snapshots: 16 KiB per frame)
+            if (stage_mask & 1)
+                LZH_CHECK(lzh_launch_lz4f_linked((const uint8_t*)d_in, n, in_readable, g.F, g.bs, g.bpf, acc,
+                                                 base + t.stage, t.stride, bcs, (uint32_t*)(base + t.recs),
+                                                 (uint32_t)g.nframes, s));
+        } else {
+            LZH_CHECK(lzh_launch_lz4_split((const uint8_t*)d_in, n, in_readable, g.bs, acc, base + t.stage, t.stride, bcs,
+                                           (uint32_t)g.nblocks, base + t.recs, stage_mask, s, g.F, g.bpf));
+        }
         if (stage_mask & 2)
             LZH_CHECK(lzh_launch_frame_sizes(codec, level, n, g.F, g.bs, g.bpf, bcs, (uint32_t*)(base + t.rel), d_csizes,
                                              (uint32_t)g.nframes, s));

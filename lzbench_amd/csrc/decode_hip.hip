@@ -233,7 +233,7 @@ using owin::kW;
 
 template <class SinkType>
 __device__ __forceinline__ int lz4_one(const Bytes& in, int cs, SinkType& O, Win& w, int cap, int& ip, int& op,
-                                       int lane) {
+                                       int lane, int prefix = 0) {
     if (ip >= cs) return -ip - 1;
     w.ensure(ip, lane);
     const uint32_t tok = w.byte(ip++);
@@ -270,7 +270,7 @@ __device__ __forceinline__ int lz4_one(const Bytes& in, int cs, SinkType& O, Win
         }
     }
     ml += 4;
-    if (off > op) return -ip - 1;
+    if (off > op + prefix) return -ip - 1;   // (prefix: earlier output of a linked frame, lz4.c:2404-2416)
     if (op + ml > cap - 5) return -ip - 1;
     if (off == 0) {
         for (int base = 0; base < ml; base += LZH_WAVE) {
@@ -602,7 +602,7 @@ __device__ __forceinline__ uint64_t chain_members(int link, int lane) {
 
 template <class SinkType>
 __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* mark, LDSA uint8_t* ring, int cap,
-                          int lane) {
+                          int lane, int prefix = 0) {
     if (cap == 0) return (cs == 1 && in.b(0) == 0) ? 0 : -1;
     if (cs <= 0) return -1;
     Win w;
@@ -642,12 +642,12 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
         const int excl = incl - L;
         const int opm = op + excl + lit;
         const bool bad = mem && (x >= cs || (ln == 15 && x + 1 >= cs - 15) || opm > cap - 12 || p1 + lit > cs - 8 ||
-                                 (mc == 15 && po + 3 >= cs - 4) || off == 0 || off > opm || opm + ml > cap - 5);
+                                 (mc == 15 && po + 3 >= cs - 4) || off == 0 || off > opm + prefix || opm + ml > cap - 5);
         const uint64_t badm = ballot(bad);
         const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
         finish_tail(O, tl, lane);   // (the previous group's last pass: its far reads ran under this parse)
         if (!keep) {
-            const int r = checked::lz4_one(in, cs, O, w, cap, ip, op, lane);
+            const int r = checked::lz4_one(in, cs, O, w, cap, ip, op, lane, prefix);
             DST(6, 1);
 #if LZH_DEC_STATS
             DST(10, __builtin_amdgcn_s_memtime() - t0);
@@ -819,13 +819,17 @@ __device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, c
     uint64_t ooff, ioff;
     int part, cs;
     bool raw;
+    uint32_t nlink = 1;      // blocks this wave decodes (a linked frame's, in order)
     if (desc) {   // framed layouts: one 32-byte block descriptor each (frame_hip.hip FrameDesc)
         const uint32_t* d = desc + 8 * chunk;
         ioff = (uint64_t)uni(d[1]) << 32 | uni(d[0]);
         ooff = (uint64_t)uni(d[3]) << 32 | uni(d[2]);
         cs = (int)uni(d[4]);
         part = (int)uni(d[5]);
-        raw = (uni(d[6]) & 1u) != 0;
+        const uint32_t fl = uni(d[6]);
+        raw = (fl & 1u) != 0;
+        if (fl & 4u) return;                    // a linked frame's later block: its first block's wave decodes it
+        if (fl & 2u) nlink = uni(d[7]);
         if (part == 0) { if (lane == 0) status[chunk] = 0; return; }   // unused slot
     } else {
         ooff = chunk * chunk_size;
@@ -839,23 +843,41 @@ __device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, c
     if (lane < 16) g_dst[lane] = 0;
     DCLK(tk0);
 #endif
-    const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
-    Bytes rin, rout;
-    rin.init(packed + ioff, readable);
-    rout.init(out + ooff, (uint64_t)part);
-    int r;
-    if (raw) {
-        copy_raw(rin, rout, part, lane);
-        r = part;
-    } else {
-        owin::SinkT<KW> O{win, rout, 0, 0};
-        LDSA uint8_t* mark = win + KW;
-        LDSA uint8_t* ring = mark + 3 * LZH_WAVE;
-        r = codec == 0 ? groups::lz4_decode(rin, cs, O, mark, ring, part, lane)
-                       : groups::snappy_decode(rin, cs, O, mark, ring, part, lane);
-        if (r > 0) O.flush(r, lane);
+    const uint64_t foff = ooff;              // (linked: the frame's output start)
+    for (uint32_t bi = 0; bi < nlink; bi++) {
+        if (bi > 0) {   // next block of a linked frame: its matches may reach into the blocks before it
+            const uint32_t* d = desc + 8 * (chunk + bi);
+            ioff = (uint64_t)uni(d[1]) << 32 | uni(d[0]);
+            ooff = (uint64_t)uni(d[3]) << 32 | uni(d[2]);
+            cs = (int)uni(d[4]);
+            part = (int)uni(d[5]);
+            raw = (uni(d[6]) & 1u) != 0;
+            wait_vm();   // (the previous block's output stores are done before its bytes are read back)
+        }
+        const int prefix = (int)(ooff - foff);
+        const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+        Bytes rin, rout;
+        rin.init(packed + ioff, readable);
+        rout.init(out + foff, (uint64_t)prefix + part);
+        rout.sh += prefix;                    // (block positions; earlier output at negative ones)
+        int r;
+        if (raw) {
+            copy_raw(rin, rout, part, lane);
+            r = part;
+        } else {
+            owin::SinkT<KW> O{win, rout, 0, 0};
+            LDSA uint8_t* mark = win + KW;
+            LDSA uint8_t* ring = mark + 3 * LZH_WAVE;
+            r = codec == 0 ? groups::lz4_decode(rin, cs, O, mark, ring, part, lane, prefix)
+                           : groups::snappy_decode(rin, cs, O, mark, ring, part, lane);
+            if (r > 0) O.flush(r, lane);
+        }
+        if (lane == 0) status[chunk + bi] = r;
+        if (r < 0) {   // the frame is bad: its remaining blocks are not decoded
+            for (uint32_t bj = bi + 1 + (uint32_t)lane; bj < nlink; bj += LZH_WAVE) status[chunk + bj] = -1;
+            break;
+        }
     }
-    if (lane == 0) status[chunk] = r;
 #if LZH_DEC_STATS
     DST(11, 1);
     DST(12, __builtin_amdgcn_s_memtime() - tk0);

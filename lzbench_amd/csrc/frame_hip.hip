@@ -186,7 +186,8 @@ lzh_frame_pack_kernel(int codec, int params, const uint8_t* in, uint64_t n_total
         const int bsid = frm::optimal_bsid(params & 7, s);
         // header (lz4frame.c:669-696): magic, FLG (version 01, independent blocks, flags), BD, content
         // size, HC = second byte of XXH32 of FLG..content size
-        const uint32_t flg = (1u << 6) | (1u << 5) | ((uint32_t)bcrc << 4) | ((uint32_t)csz << 3) | ((uint32_t)ccrc << 2);
+        const uint32_t indep = (params & 0x80) && s > bs ? 0u : 1u;   // linked blocks (frames of one block: independent)
+        const uint32_t flg = (1u << 6) | (indep << 5) | ((uint32_t)bcrc << 4) | ((uint32_t)csz << 3) | ((uint32_t)ccrc << 2);
         const uint32_t bd = (uint32_t)(bsid & 7) << 4;
         uint32_t hw[3] = {flg | (bd << 8), 0, 0};   // descriptor bytes as little-endian words
         int hl = 2;
@@ -232,8 +233,9 @@ struct FrameDesc { uint64_t src, dst; uint32_t cs, ds, flags, pad; };
 // one wave per frame: header checks and block walk (lz4frame.c:1150-1260 LZ4F_decodeHeader,
 // :1384-1899 LZ4F_decompress; nvcomp: LZ4Metadata.cpp:60-110), descriptors for every block
 // (maxbpf slots per frame, unused slots decode nothing), fstat[f] = 0 or a negative status:
-// -1 malformed, -2 a feature outside the supported set (dictionary id, linked blocks past the
-// first, blocks that are not all full but the last)
+// -1 malformed, -2 a feature outside the supported set (dictionary id, blocks that are not all full
+// but the last).  A linked frame's blocks are marked so that one wave decodes them in order, each
+// with the frame's output before it as its prefix (LZ4F_updateDict, lz4frame.c:1290-1306).
 extern "C" __global__ void __launch_bounds__(64)
 lzh_frame_parse_kernel(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                        const uint32_t* csizes, uint64_t n_total, uint64_t fs, uint32_t maxbpf, FrameDesc* desc,
@@ -289,7 +291,6 @@ lzh_frame_parse_kernel(int codec, const uint8_t* packed, uint64_t packed_readabl
             const uint32_t sz = w & 0x7fffffffu;
             if (sz > B || ip + sz + 4u * (uint32_t)bcrc > cs) { st = -1; break; }
             if (b >= nbe) { st = -2; break; }
-            if (b > 0 && !(flg & 0x20)) { st = -2; break; }
             const uint32_t ds = (uint32_t)min<uint64_t>(B, s - b * B);
             const bool raw = (w >> 31) != 0;
             if (raw && sz != ds) { st = sz > ds ? -1 : -2; break; }
@@ -299,11 +300,15 @@ lzh_frame_parse_kernel(int codec, const uint8_t* packed, uint64_t packed_readabl
                 const uint32_t h = frm::xxh32_wave(bb, sz, lane);
                 if (h != rd(ip + sz)) { st = -1; break; }
             }
-            if (lane == 0) D[b] = FrameDesc{ioff + ip, foff + b * B, sz, ds, raw ? 1u : 0u, 0};
+            // flags: 1 = stored raw, 2 = a linked frame's first block (pad = the frame's block count),
+            // 4 = a linked frame's later block (decoded by the first block's wave, in order)
+            const uint32_t lk = (flg & 0x20) ? 0u : (b == 0 ? 2u : 4u);
+            if (lane == 0) D[b] = FrameDesc{ioff + ip, foff + b * B, sz, ds, (raw ? 1u : 0u) | lk, 0};
             ip += sz + 4u * (uint32_t)bcrc;
             b++;
         }
         if (!st && b != nbe) st = -2;
+        if (!st && !(flg & 0x20) && lane == 0) D[0].pad = b;
         if (!st && ccrc) ip += 4;
         if (!st && ip != cs) st = -1;
     } else {

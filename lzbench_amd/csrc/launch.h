@@ -30,6 +30,9 @@ size_t lzh_zstd_scratch_stride(size_t chunk_size, int level);
 int lzh_zstd_level_ok(int level, size_t chunk_size);
 // frame_size / bpf: framed layouts (LZ4 frame, nvcomp container) -- block i is block i mod bpf of
 // frame i / bpf (frames of frame_size bytes cut into blocks of chunk_size); bpf <= 1: plain chunks
+hipError_t lzh_launch_lz4f_linked(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t fs, uint64_t bs,
+                                  uint32_t bpf, int acc, uint8_t* stage, uint64_t stride, uint32_t* bcs, uint32_t* snap,
+                                  uint32_t nframes, hipStream_t s);
 hipError_t lzh_launch_lz4_split(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                                 uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
                                 int stage_mask, hipStream_t s, uint64_t frame_size = 0, uint32_t bpf = 1);

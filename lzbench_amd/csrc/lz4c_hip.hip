@@ -256,7 +256,7 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 // output.  Emitted lane-parallel under the NEXT batch's candidate loads.  Plain locals (a
 // struct here ends up in scratch memory).
 #define RECS_DECL                                                                                  \
-    uint32_t rc_anc = 0, rc_lit = 0, rc_off = 0, rc_mlx = 0, rc_st = 0;                            \
+    uint32_t rc_anc = 0, rc_lit = 0, rc_off = 0, rc_mlx = 0, rc_st = 0, rc_p = 0;                  \
     uint64_t rc_m = 0;                                                                             \
     int rc_tot = 0
 #define RECS_EMIT() op = emit_recs(in, R, out, O, op, rc_anc, rc_lit, rc_off, rc_mlx, rc_st, rc_m, rc_tot, lane)
@@ -276,7 +276,24 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
                 nrec = unii(nrec + __builtin_popcountll(rm_));                                     \
             }                                                                                      \
         } else {                                                                                   \
+            RECS_CHECK();                                                                          \
             RECS_EMIT();                                                                           \
+        }                                                                                          \
+    } while (0)
+// (kLinked) limitedOutput: the first sequence whose match-length check fails (lz4.c:1097-1121: the
+// output after its offset + LASTLITERALS + 1 + its match-length bytes past cap) ends the block
+#define RECS_CHECK()                                                                               \
+    do {                                                                                           \
+        if (kLinked && rc_m) {                                                                     \
+            const int lt_ = (int)rc_lit, ml_ = (int)rc_mlx;                                        \
+            const bool f_ = lane_on(rc_m) &&                                                       \
+                            op + (int)rc_st + 9 + ext_len_bytes(lt_) + lt_ + (ml_ + 240) / 255 > lk->cap; \
+            const uint64_t fm_ = ballot(f_);                                                       \
+            if (fm_) {                                                                             \
+                aborted = true;                /* (ends the batch loop) */                        \
+                lk->abort = rdlanei((int)rc_p, __builtin_ctzll(fm_));                              \
+                rc_m = 0;                                                                          \
+            }                                                                                      \
         }                                                                                          \
     } while (0)
 
@@ -528,6 +545,45 @@ __device__ __forceinline__ uint64_t lane_bits(int lo, int hi) {   // bits lo..hi
     return ((2ull << hi) - 1ull) & (~0ull << lo);                 // 2 << 63 wraps to 0: all ones
 }
 
+// ---- 128-position run batches (kWide): lane l holds positions base+l (half 0) and base+64+l (half 1);
+// 128-bit position masks are pairs of 64-bit ballots (word 0 = half 0, word 1 = half 1).
+constexpr int kOut128 = 128;      // link code: the chain continues past the batch
+constexpr int kExh128 = 129;      // link code: the 65 step-1 probes of the segment end inside the batch, no hit
+constexpr int kSpc128 = 130;      // link code: long match (count past the window) or a match end past mflimit
+
+__device__ __forceinline__ int msb64(uint64_t m) { return 63 - __builtin_clzll(m); }   // (m != 0)
+
+// first hit of A0:A1 in the segment [e, e + 64] (the re-test at a match end e plus 64 step-1 search
+// probes, lz4.c:955-969) clipped to the batch; kExh128 when the segment lies inside the batch (e <= 63)
+// and has no hit, kOut128 when it runs past the batch
+__device__ __forceinline__ int next_hit128(uint64_t A0, uint64_t A1, int e) {
+    const int ec = min(e, 127);
+    const uint64_t m0 = ec < 64 ? A0 & (~0ull << ec) : 0ull;
+    const uint64_t m1 = ec < 64 ? A1 & ((2ull << ec) - 1ull) : A1 & (~0ull << (ec & 63));
+    const int r = m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : (e < 64 ? kExh128 : kOut128));
+    return e >= 128 ? kOut128 : r;
+}
+
+// candidate window taken from the input ring (a candidate inside the batch) compared with the P side:
+// ok = 4-byte seed (lz4.c:1005), len = LZ4_count bytes past +4 capped at 20
+__device__ __forceinline__ bool eval_ring(const PSide& P, const PSide& Q, bool valid, int& len) {
+    len = first_diff20(P.q0 ^ Q.q0, P.q1 ^ Q.q1, P.q2 ^ Q.q2, P.q3 ^ Q.q3, P.q4 ^ Q.q4);
+    return valid && P.w == Q.w;
+}
+
+// the same against a global candidate window (MWin) without the catch-up bytes
+__device__ __forceinline__ bool eval_fwd(const PSide& P, const MWin& W, bool valid, int& len) {
+    const uint32_t s = (uint32_t)W.sm;
+    const uint32_t mw = __builtin_amdgcn_alignbyte(W.d2, W.d1, s);
+    const uint32_t x0 = P.q0 ^ __builtin_amdgcn_alignbyte(W.d3, W.d2, s);
+    const uint32_t x1 = P.q1 ^ __builtin_amdgcn_alignbyte(W.d4, W.d3, s);
+    const uint32_t x2 = P.q2 ^ __builtin_amdgcn_alignbyte(W.d5, W.d4, s);
+    const uint32_t x3 = P.q3 ^ __builtin_amdgcn_alignbyte(W.d6, W.d5, s);
+    const uint32_t x4 = P.q4 ^ __builtin_amdgcn_alignbyte(W.d7, W.d6, s);
+    len = first_diff20(x0, x1, x2, x3, x4);
+    return valid && mw == P.w;
+}
+
 // Group lanes by table slot (one ballot per slot that has a collision): grp = lanes sharing
 // this lane's slot; prev = the closest earlier lane in it (-1 if none).
 __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t losers, uint64_t& grp, int& prev,
@@ -574,6 +630,7 @@ __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t los
             }                                                                                      \
             const int lit_ = p_ - bk_ - anc_, mlx_ = bk_ + pr_cn;                                  \
             rc_anc = (uint32_t)anc_;                                                               \
+            rc_p = (uint32_t)p_;                                                                   \
             rc_lit = kRec ? (uint32_t)p_ : (uint32_t)lit_;   /* kRec: the match start P */        \
             rc_off = (uint32_t)(p_ - (int)pr_ce);                                                  \
             rc_mlx = (uint32_t)mlx_;                                                               \
@@ -588,15 +645,295 @@ __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t los
         }                                                                                          \
     } while (0)
 
+// P side at p from the ring when the batch is in it, else from global memory
+__device__ __forceinline__ PSide p_side_at(bool rg, const Ring& R, const Bytes& in, int p) {
+    return rg ? p_side_ring_m<false>(R, p) : p_side_global(in, p);
+}
+
+#ifndef LZH_WIDE
+#define LZH_WIDE 0   // 128-position run batches in the parse kernel (acceleration 1, byU16): measured slower (text 15.9 -> 18.2 ms compress), kept off
+#endif
+
+// One 128-position run batch of the parse kernel (acceleration 1, byU16 table, records out):
+// positions base .. base+127, two per lane (base+l, base+64+l).  The same resolve as the 64-lane
+// run batch in compress_chunk -- hash, read the slot (the candidate), claim it, read it back; the
+// candidate windows of all 128 positions in one memory round trip; the chain of sequences from the
+// batch's search start by a scalar walk over per-position links; probed / inserted sets; colliders
+// re-resolved until consistent -- over twice the input per round trip, resolve and loop overhead.
+// Positions of one segment (a match end re-tested, then 64 step-1 search probes, lz4.c:955-969 and
+// :1148-1200) may now end inside the batch: the walk stops there and stride batches take over.
+// Records go out at the end of the batch.  Returns false when the parse has ended.
+__device__ __forceinline__ bool run_batch128(const Bytes& in, Ring& R, const Table<true>& T, rsrc_t recs, int lane,
+                                             int mfl1, int mlimit, int endX, int& base, int& q, int& qlim, int& pins,
+                                             int& s, int& k0, bool& runb, bool& retest, int& anchor, int& nrec,
+                                             uint32_t rc_lit, uint32_t rc_off, uint32_t rc_mlx, uint64_t& rc_m) {
+    constexpr int W = LZH_WAVE;
+    {   // a stride batch's pending record (its one sequence)
+        if (uni64(rc_m)) {
+            if (lane == 0) st_b64(recs, 8 * nrec, rc_lit | (rc_mlx << 24), (rc_mlx >> 8) | (rc_off << 16));
+            nrec = unii(nrec + 1);
+        }
+        rc_m = 0;
+    }
+    const int p0 = base + lane, p1 = p0 + W;
+    const bool v0 = p0 + 1 <= mfl1, v1 = p1 + 1 <= mfl1;   // forwardIp <= mflimitPlusOne (lz4.c:969)
+    const uint64_t vm0 = ballot(v0), vm1 = ballot(v1);
+    const int fv = __builtin_popcountll(vm0) + __builtin_popcountll(vm1);   // valid positions: [0, fv)
+    const bool rg = R.has(base - 4, base + 2 * W + 28);
+    const PSide s0 = p_side_at(rg, R, in, p0), s1 = p_side_at(rg, R, in, p1);
+    const uint32_t h0 = hash_of<true>(s0.w, 0), h1 = hash_of<true>(s1.w, 0);
+    const uint32_t old0 = T.get(h0), old1 = T.get(h1);
+    MWin W0, W1;
+    W0.load(in, old0, v0);                                    // (issued before the claim round trip)
+    W1.load(in, old1, v1);
+    // claims (the half-1 stores come second: a slot claimed in both halves holds a half-1 position)
+    if (vm0 == ~0ull) T.put(h0, (uint32_t)p0); else if (v0) T.put(h0, (uint32_t)p0);
+    if (vm1 == ~0ull) T.put(h1, (uint32_t)p1); else if (v1) T.put(h1, (uint32_t)p1);
+    wave_lds_fence();
+    const uint32_t bk0 = T.get(h0), bk1 = T.get(h1);
+    const uint64_t los = ballot(v0 && bk0 != (uint32_t)p0) | ballot(v1 && bk1 != (uint32_t)p1);
+    // slot groups (under the candidate loads): every position of a slot read back the same claim
+    // winner w (0..127), so equal w <=> same slot; equality bit-sliced over 7 ballots per half.
+    // g00 = half-0 members of x0's slot; g10 / g11 = half-0 / half-1 members of x1's slot.
+    const uint64_t self = 1ull << lane, below = self - 1ull;
+    uint64_t g00 = self, g10 = 0, g11 = self;
+    int prev0 = -1, prev1 = -1;                               // closest earlier position of the slot
+    if (los) {
+        const uint32_t w0 = bk0 - (uint32_t)base, w1 = bk1 - (uint32_t)base;
+        uint32_t a_lo = 0, a_hi = 0, b_lo = 0, b_hi = 0, c_lo = 0, c_hi = 0;
+#pragma unroll
+        for (int b = 0; b < 7; b++) {
+            const uint64_t m0 = ballot((w0 >> b) & 1u), m1 = ballot((w1 >> b) & 1u);
+            const uint32_t t0 = (uint32_t)__builtin_amdgcn_sbfe((int)w0, b, 1);
+            const uint32_t t1 = (uint32_t)__builtin_amdgcn_sbfe((int)w1, b, 1);
+            a_lo |= (uint32_t)m0 ^ t0; a_hi |= (uint32_t)(m0 >> 32) ^ t0;
+            b_lo |= (uint32_t)m0 ^ t1; b_hi |= (uint32_t)(m0 >> 32) ^ t1;
+            c_lo |= (uint32_t)m1 ^ t1; c_hi |= (uint32_t)(m1 >> 32) ^ t1;
+        }
+        g00 = v0 ? ~(((uint64_t)a_hi << 32) | a_lo) & vm0 : self;
+        g10 = v1 ? ~(((uint64_t)b_hi << 32) | b_lo) & vm0 : 0ull;
+        g11 = v1 ? ~(((uint64_t)c_hi << 32) | c_lo) & vm1 : self;
+        const uint64_t e0b = g00 & below, e1b = g11 & below;
+        prev0 = (v0 && e0b) ? msb64(e0b) : -1;
+        prev1 = v1 ? (e1b ? W + msb64(e1b) : (g10 ? msb64(g10) : -1)) : -1;
+    }
+    // colliders: the usual candidate is the closest earlier position of the slot; its window is in
+    // the ring (the batch's own bytes): pre-evaluated under the candidate loads
+    const uint64_t coll0 = ballot(prev0 >= 0), coll1 = ballot(prev1 >= 0);
+    bool okp0 = false, okp1 = false;
+    int lep0 = 0, lep1 = 0;
+    if (coll0 | coll1) {
+        const PSide Q0 = p_side_at(rg, R, in, base + max(prev0, 0)), Q1 = p_side_at(rg, R, in, base + max(prev1, 0));
+        okp0 = eval_ring(s0, Q0, v0, lep0);
+        okp1 = eval_ring(s1, Q1, v1, lep1);
+    }
+    wait_vm();
+    R.ready = R.fill;
+    wave_lds_fence();
+    {   // ring refill after the wait: it completes under the next batch
+        const int target = min(base + in.sh + kAhead, endX + 256);
+        for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
+    }
+    int len0, len1;
+    const bool ok0 = eval_fwd(s0, W0, v0, len0), ok1 = eval_fwd(s1, W1, v1, len1);
+
+    // ---- resolve (lz4.c:1142-1200: match end -> ip-2 fill -> re-test -> search from ip+1)
+    const int lo = q - base, hi0 = min(qlim - base, 2 * W - 1);   // the first segment's probes: lo..hi0
+    const uint64_t P0a = lo < W ? lane_bits(lo, min(hi0, W - 1)) : 0ull;
+    const uint64_t P0b = hi0 >= W ? lane_bits(max(lo, W) - W, hi0 - W) : 0ull;
+    const uint64_t I0 = pins >= 0 ? 1ull : 0ull;              // a pending ip-2 fill at base (lz4.c:1146)
+    int ak0 = prev0, ak1 = prev1;                             // assumed candidate (-1: the slot's old value)
+    bool oe0 = prev0 >= 0 ? okp0 : ok0, oe1 = prev1 >= 0 ? okp1 : ok1;
+    int le0 = prev0 >= 0 ? lep0 : len0, le1 = prev1 >= 0 ? lep1 : len1;
+    uint32_t ce0 = prev0 >= 0 ? (uint32_t)(base + prev0) : old0, ce1 = prev1 >= 0 ? (uint32_t)(base + prev1) : old1;
+    uint64_t Mm0 = 0, Mm1 = 0, Ia0 = 0, Ia1 = 0;
+    int cn0 = 0, cn1 = 0, e0 = 0, e1 = 0, eL = 0, fin = kOut128;
+    bool endip = false;
+    for (int round = 0; round <= 2 * W; round++) {
+        const uint64_t A0 = ballot(oe0), A1 = ballot(oe1);
+        // if position x starts a sequence: match count, end, next hit in the segment at the end
+        cn0 = min(le0, mlimit - (p0 + kMinMatch));
+        cn1 = min(le1, mlimit - (p1 + kMinMatch));
+        const bool lg0 = oe0 && le0 == 20 && p0 + kMinMatch + 20 < mlimit;
+        const bool lg1 = oe1 && le1 == 20 && p1 + kMinMatch + 20 < mlimit;
+        e0 = max(lane + kMinMatch + cn0, 0);
+        e1 = max(W + lane + kMinMatch + cn1, 0);
+        const int lk0 = (lg0 || p0 + kMinMatch + cn0 >= mfl1) ? kSpc128 : next_hit128(A0, A1, e0);
+        const int lk1 = (lg1 || p1 + kMinMatch + cn1 >= mfl1) ? kSpc128 : next_hit128(A0, A1, e1);
+        Mm0 = 0;
+        Mm1 = 0;
+        endip = false;
+        const uint64_t r0 = A0 & P0a, r1 = A1 & P0b;
+        uint64_t E0, E1;                                      // probed positions
+        if (!(r0 | r1)) {
+            E0 = P0a;
+            E1 = P0b;
+            fin = hi0 == qlim - base ? kExh128 : kOut128;
+            Ia0 = I0 | E0;
+            Ia1 = E1;
+        } else {
+            int sl = r0 ? __builtin_ctzll(r0) : W + __builtin_ctzll(r1);
+            int fs = kOut128;
+            for (;;) {                                        // (links strictly increase: the walk ends)
+                if (sl < W) {
+                    for (;;) {
+                        Mm0 |= 1ull << sl;
+                        fs = rdlanei(lk0, sl);
+                        if (fs >= W) break;
+                        sl = fs;
+                    }
+                    if (fs < kOut128) sl = fs;                // into half 1
+                }
+                if (sl >= W) {
+                    for (;;) {
+                        Mm1 |= 1ull << (sl - W);
+                        fs = rdlanei(lk1, sl - W);
+                        if (fs >= kOut128) break;
+                        sl = fs;
+                    }
+                }
+                if (fs != kSpc128) break;                     // the chain leaves the batch / the segment ends
+                const bool h1s = sl >= W;
+                const int sk = sl & (W - 1);
+                int es;
+                if (rdlane((uint32_t)(h1s ? lg1 : lg0), sk)) {   // match runs past the 20-byte window
+                    const int c = slow_count(in, base + sl, (int)rdlane(h1s ? ce1 : ce0, sk), mlimit, lane);
+                    es = sl + kMinMatch + c;
+                    if (h1s) { cn1 = lane == sk ? c : cn1; e1 = lane == sk ? es : e1; }
+                    else { cn0 = lane == sk ? c : cn0; e0 = lane == sk ? es : e0; }
+                    fs = next_hit128(A0, A1, es);
+                } else {
+                    es = rdlanei(h1s ? e1 : e0, sk);
+                }
+                if (base + es >= mfl1) { endip = true; break; }   // lz4.c:1142
+                if (fs >= kOut128) break;
+                sl = fs;
+            }
+            fin = fs;
+            eL = rdlanei(sl >= W ? e1 : e0, sl & (W - 1));
+            // j = the last member at or before each position: positions strictly inside its match are
+            // not probed, its segment [e, e + 64] is; ip-2 of each member is inserted (lz4.c:1146)
+            const uint64_t ml0 = Mm0 & (below | self), ml1 = Mm1 & (below | self);
+            const int j0 = ml0 ? msb64(ml0) : -1;
+            const int j1 = ml1 ? W + msb64(ml1) : (Mm0 ? msb64(Mm0) : -1);
+            const uint32_t epk = (uint32_t)min(e0, 0xffff) | ((uint32_t)min(e1, 0xffff) << 16);
+            const uint32_t g0 = lane_gather(epk, j0 & (W - 1)), g1 = lane_gather(epk, j1 & (W - 1));
+            const int ej0 = (int)(g0 & 0xffffu), ej1 = (int)(j1 >= W ? g1 >> 16 : g1 & 0xffffu);
+            const int x0 = lane, x1 = W + lane;
+            bool pr0 = j0 >= 0 ? (x0 == j0 || (x0 >= ej0 && x0 <= ej0 + 64)) : lane_on(P0a);
+            bool pr1 = j1 >= 0 ? (x1 == j1 || (x1 >= ej1 && x1 <= ej1 + 64)) : lane_on(P0b);
+            if (endip) { pr0 = pr0 && x0 < eL; pr1 = pr1 && x1 < eL; }
+            E0 = ballot(pr0);
+            E1 = ballot(pr1);
+            Ia0 = ballot(j0 >= 0 && x0 == ej0 - 2) | I0 | E0;
+            Ia1 = ballot(j1 >= 0 && x1 == ej1 - 2) | E1;
+        }
+        if (!((coll0 & E0) | (coll1 & E1))) break;
+        // each probed collider's real candidate: the latest earlier inserted position of its slot
+        const uint64_t k0m = g00 & below & Ia0, k1m = g11 & below & Ia1, k1z = g10 & Ia0;
+        const int kt0 = k0m ? msb64(k0m) : -1;
+        const int kt1 = k1m ? W + msb64(k1m) : (k1z ? msb64(k1z) : -1);
+        const bool fx0 = lane_on(E0) && kt0 != ak0, fx1 = lane_on(E1) && kt1 != ak1;
+        if (!(ballot(fx0) | ballot(fx1))) break;
+        const bool far0 = fx0 && kt0 >= 0 && kt0 != prev0, far1 = fx1 && kt1 >= 0 && kt1 != prev1;
+        if (fx0) {
+            ak0 = kt0;
+            oe0 = kt0 < 0 ? ok0 : okp0;
+            ce0 = kt0 < 0 ? old0 : (uint32_t)(base + kt0);
+            le0 = kt0 < 0 ? len0 : lep0;
+        }
+        if (fx1) {
+            ak1 = kt1;
+            oe1 = kt1 < 0 ? ok1 : okp1;
+            ce1 = kt1 < 0 ? old1 : (uint32_t)(base + kt1);
+            le1 = kt1 < 0 ? len1 : lep1;
+        }
+        if (ballot(far0) | ballot(far1)) {                    // an older position of the slot than prev
+            const PSide F0 = p_side_at(rg, R, in, base + (far0 ? kt0 : 0));
+            const PSide F1 = p_side_at(rg, R, in, base + (far1 ? kt1 : 0));
+            int l0, l1;
+            const bool o0 = eval_ring(s0, F0, v0, l0), o1 = eval_ring(s1, F1, v1, l1);
+            if (far0) { oe0 = o0; le0 = l0; }
+            if (far1) { oe1 = o1; le1 = l1; }
+        }
+    }
+    // ---- records: match start P | match length - 4 << 24 | offset << 48 (catch-up: the emission kernel)
+    const bool anym = (Mm0 | Mm1) != 0;
+    if (anym) {
+        const int n0 = __builtin_popcountll(Mm0);
+        if (lane_on(Mm0)) {
+            const int ri = nrec + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(Mm0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Mm0, 0u));
+            st_b64(recs, 8 * ri, (uint32_t)p0 | ((uint32_t)cn0 << 24), ((uint32_t)cn0 >> 8) | (((uint32_t)p0 - ce0) << 16));
+        }
+        if (lane_on(Mm1)) {
+            const int ri = nrec + n0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(Mm1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Mm1, 0u));
+            st_b64(recs, 8 * ri, (uint32_t)p1 | ((uint32_t)cn1 << 24), ((uint32_t)cn1 >> 8) | (((uint32_t)p1 - ce1) << 16));
+        }
+        nrec = unii(nrec + n0 + __builtin_popcountll(Mm1));
+    }
+    // the parse ends here: a match end past mflimit, or the search reaches the invalid positions
+    const bool endp = anym ? (endip || (eL < 2 * W && fv <= min(eL + 64, 2 * W - 1))) : hi0 >= fv;
+    if (endp) {
+        if (anym) anchor = base + eL;
+        return false;
+    }
+    {   // table: each slot ends with its last inserted position, else its old value (all members of a
+        // slot store the same value; a half-1 member's store comes last)
+        const uint64_t gi0 = g00 & Ia0, gi1 = g11 & Ia1, gz = g10 & Ia0;
+        const uint32_t val0 = gi0 ? (uint32_t)(base + msb64(gi0)) : old0;
+        const uint32_t val1 = gi1 ? (uint32_t)(base + W + msb64(gi1)) : (gz ? (uint32_t)(base + msb64(gz)) : old1);
+        if (vm0 == ~0ull) T.put(h0, val0); else if (v0) T.put(h0, val0);
+        if (vm1 == ~0ull) T.put(h1, val1); else if (v1) T.put(h1, val1);
+        wave_lds_fence();
+    }
+    if (anym) {
+        const int ip = base + eL;
+        anchor = ip;
+        if (fin == kExh128) {                                 // 65 step-1 probes done: stride batches
+            runb = false; s = ip + 1; k0 = W; retest = false;
+        } else if (eL < 2 * W) {                              // searched to the batch end
+            q = base + 2 * W; qlim = ip + 64; pins = -1;
+        } else {                                              // re-test in a later batch
+            q = ip; qlim = ip + 64; pins = eL - 2 >= 2 * W ? ip - 2 : -1;
+        }
+    } else if (fin == kExh128) {
+        runb = false; s = qlim - 64 + 1; k0 = W; retest = false;
+    } else {
+        q = base + 2 * W; pins = -1;
+    }
+    if (runb) base = pins >= 0 ? pins : q;
+    return true;
+}
+
+// One block of an LZ4 frame with linked blocks (kLinked; lzh_lz4f_linked_kernel): the parse of
+// LZ4_compress_fast_continue in prefix mode (lz4.c:1565-1628 -> LZ4_compress_generic with byU32,
+// withPrefix64k, noDictIssue, limitedOutput): positions are frame indices, the block is
+// [b0, b0 + n), the table persists from block to block, candidates reach back into earlier blocks
+// (at most 65535 bytes, the byU32 distance check), the catch-up stops at the frame start
+// (lowLimit = source - dictSize).  cap = the limitedOutput budget (block size - 1): the first
+// sequence whose match-length check fails (lz4.c:1097-1121; it implies the literal check,
+// :1024-1027) ends the parse with abort = its probe position, a failing last-literals check
+// (:1207-1216) with abort = -2; else -1.  stop >= 0: a table-only replay that ends right after
+// the probe at `stop` (the table as the reference leaves it at an abort: positions past stop are not
+// probed, a match ending past it ends the parse).  At every end of the parse the table is left as
+// the reference leaves it (the next block starts from it).
+struct LinkCtl {
+    int b0, cap, stop;
+    bool keep_tab;       // the table holds the frame's earlier blocks (else zeroed)
+    int abort;           // out: -1 fits, >= 0 probe position of the failing sequence, -2 last literals
+};
+
 // kFast (acceleration > 1, lz4.c:958-967): run batches probe a data-independent pattern.  A search
 // from a segment origin e (a match end, re-tested, or position 0 at the chunk start) probes
 // e+1, e+2, then steps of acc for 64 probes: offsets {0, 1, 2, 2+acc, 2+2acc, ..} from e.  Run
 // batches cover the first 64 search probes of each segment (as with acc 1); later probes and the
 // chunk tail (where a probe's forwardIp could pass mflimit) go through stride batches.
-template <bool kSmall, bool kStats, bool kRec = false, bool kFast = false>
+template <bool kSmall, bool kStats, bool kRec = false, bool kFast = false, bool kWide = false, bool kLinked = false>
 __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab,
                                LDSA uint32_t* ringw, LDSA uint8_t* outb, uint32_t* out_size,
-                               unsigned long long* stats, rsrc_t recs, uint32_t* rec_hdr) {
+                               unsigned long long* stats, rsrc_t recs, uint32_t* rec_hdr, LinkCtl* lk = nullptr) {
+    static_assert(!kLinked || (!kSmall && !kRec && !kWide), "linked frames: byU32, in-kernel emission");
+    const int b0 = kLinked ? lk->b0 : 0;                  // the block's first position (frame index)
     const int lane = threadIdx.x;
     Table<kSmall> T{tab};
     uint64_t clk[kClk] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -613,35 +950,41 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
     }
     int nrec = 0;
     bool recs_st = false;     // a record store was issued after this batch's candidate loads
-    {
+    if (!kLinked || !lk->keep_tab) {
         LDSA uint32_t* t4 = (LDSA uint32_t*)tab;
 #pragma unroll
         for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
     }
     constexpr bool kRingOn = !(kRec && LZH_PARSE_NORING);
     Ring R{ringw, in.sh, 0, 0, kRingOn, kRec};   // (the parse kernel's ring carries a 32-byte mirror)
+    if (kLinked) R.fill = max(((b0 + in.sh) & ~255) - 256, 0);   // (a block's ring starts just before it)
     OutRing O{outb, out.sh, 0};
-    const int endX = n + in.sh + 8;
+    const int endX = b0 + n + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
     wait_vm();
     R.ready = R.fill;
     wave_lds_fence();
 
-    int op = 0, anchor = 0;
+    int op = 0, anchor = b0;
+    bool aborted = false;                    // (kLinked) the limitedOutput budget ran out
+    if (kLinked) lk->abort = -1;
     RECS_DECL;                               // sequences waiting to be emitted
     uint64_t pr_m = 0;                       // a run batch whose records are not built yet
     int pr_base = 0, pr_anchor = 0, pr_e = 0, pr_cn = 0, pr_be = 0;
     uint32_t pr_ce = 0;
 
     if (n >= kMinLength) {
-        const int mfl1 = n - kMfLimit + 1;
-        const int mlimit = n - kLastLiterals;
+        const int mfl1 = b0 + n - kMfLimit + 1;
+        const int mlimit = b0 + n - kLastLiterals;
+        // (kLinked replay: positions past `stop` are not probed, a match end past it ends the parse)
+        const int stop = kLinked && lk->stop >= 0 ? lk->stop : (1 << 30);
+        const int mfe = kLinked ? min(mfl1, stop + 1) : mfl1;
         const int64_t a64 = (int64_t)acc << 6;
 
-        {   // position 0 enters the table before the first search (lz4.c:922-923)
-            const uint64_t v0 = kRingOn ? ((uint64_t)R.u32(0) | ((uint64_t)R.byte(4) << 32)) : in.w40(0);
+        {   // the first position enters the table before the first search (lz4.c:922-923)
+            const uint64_t v0 = kRingOn ? ((uint64_t)R.u32(b0) | ((uint64_t)R.byte(b0 + 4) << 32)) : in.w40(b0);
             const uint32_t h0 = hash_of<kSmall>((uint32_t)v0, (uint32_t)(v0 >> 32));
-            if (lane == 0) T.put(h0, 0);
+            if (lane == 0) T.put(h0, (uint32_t)b0);
             wave_lds_fence();
         }
         // Parse state.  Run batches (acceleration 1, a search in its first 64 probes): lanes
@@ -651,9 +994,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         // (any other schedule): one sequence per batch, the search from s with k0 probes done.
         bool runb = kFast || acc == 1, retest = false, go = true;
         const int dlim = kFast ? 2 + 62 * acc : 64;      // last run-batch probe: segment origin + dlim
-        int base = 1, q = 1, qlim = dlim, pins = -1;
-        int so = 0;                              // segment origin (kFast pattern phase)
-        int s = 1, k0 = 0;
+        int base = b0 + 1, q = b0 + 1, qlim = b0 + dlim, pins = -1;
+        int so = b0;                             // segment origin (kFast pattern phase)
+        int s = b0 + 1, k0 = 0;
         // probe pattern from a segment origin (bits = offsets): PER = {0, acc, 2acc, ..}, PAT = {0, 1, 2 + PER}
         uint64_t PER = ~0ull, PAT = ~0ull;
         if (kFast) {
@@ -662,7 +1005,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             PAT = 3ull | (PER << 2);
         }
 
-        for (int guard = 0; (LZH_UNI_GO ? unii((int)go) != 0 : go) && guard < 4 * n + 64; guard++) {
+        for (int guard = 0; (LZH_UNI_GO ? unii((int)go) != 0 : go) && !(kLinked && aborted) && guard < 4 * n + 64; guard++) {
 #if LZH_LOOP_UNI
             runb = unii(runb) != 0; retest = unii(retest) != 0;
             base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
@@ -670,6 +1013,13 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             R.fill = unii(R.fill); R.ready = unii(R.ready); O.flushed = unii(O.flushed);
             so = unii(so);
 #endif
+            if constexpr (kWide) {
+                if (runb) {
+                    go = run_batch128(in, R, T, recs, lane, mfl1, mlimit, endX, base, q, qlim, pins, s, k0, runb,
+                                      retest, anchor, nrec, rc_lit, rc_off, rc_mlx, rc_m);
+                    continue;
+                }
+            }
             LZ_STAT(0, 1);
 #if defined(LZH_PAD_SALU) || defined(LZH_PAD_VALU)
             {   // (issue-resource experiments: extra dependent scalar / vector instructions per batch)
@@ -707,7 +1057,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             bool valid;
             if (runb) {
                 p = base + lane;
-                valid = p + 1 <= mfl1;        // forwardIp <= mflimitPlusOne (lz4.c:969)
+                valid = p + 1 <= mfl1 && (!kLinked || p <= stop);   // forwardIp <= mflimitPlusOne (lz4.c:969)
             } else {
                 int64_t pp, nxt;
                 if (retest && lane == 0) {
@@ -720,7 +1070,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     pp = (int64_t)s + o;
                     nxt = pp + st;
                 }
-                valid = nxt <= mfl1;
+                valid = nxt <= mfl1 && (!kLinked || pp <= stop);
                 p = valid ? (int)pp : 0;
             }
             const uint64_t vmask = ballot(valid);
@@ -868,7 +1218,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         int sl = __builtin_ctzll(r0);
                         bool endip = false;                            // a match ended past mflimit
                         // link: next member lane, or 0x80 for the rare cases (long match, parse end)
-                        const int link = (lng || p + kMinMatch + cn >= mfl1) ? 0x80 : f;
+                        const int link = (lng || p + kMinMatch + cn >= mfe) ? 0x80 : f;
 #if LZH_PARSE_LIFT
                         // chain membership lane-parallel (binary lifting over the links, as the decoder's
                         // chain_members): jumps of 1, 2, 4, 8 links; a member takes >= 4 lanes, so <= 16
@@ -918,7 +1268,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                             } else {
                                 es = rdlanei(e, sl);
                             }
-                            if (base + es >= mfl1) { endip = true; break; }  // lz4.c:1142
+                            if (base + es >= mfe) { endip = true; break; }   // lz4.c:1142
                             if (fs >= LZH_WAVE) break;
                             sl = fs;
                         }
@@ -974,9 +1324,31 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 // the sequences' records are built under the next batch's loads (RUN_RECORDS)
                 pr_m = Mm; pr_base = base; pr_anchor = anchor; pr_e = e; pr_cn = cn; pr_be = be; pr_ce = ce;
                 LZ_CLK(6);                                             // records
+                // table: the last inserted lane of each slot, or the slot's old value
+                auto restore = [&](uint64_t Iw) {
+                    const bool inI = lane_on(Iw);
+                    if (LZH_BRFREE && vmask == ~0ull) {
+                        // every lane stores its slot's final value (all lanes of a slot agree):
+                        // the slot's last inserted lane, else its old value
+                        const uint64_t gi = grp & Iw;
+                        T.put(h, gi ? (uint32_t)(base + 63 - __builtin_clzll(gi)) : old);
+                    } else if (!losers) {
+                        if (valid && !inI) T.put(h, old);
+                    } else {
+                        const uint64_t gi = grp & Iw;
+                        const bool wr = valid && (gi == 0 || (inI && (gi & ~((2ull << lane) - 1ull)) == 0));
+                        if (wr) T.put(h, inI ? (uint32_t)p : old);
+                    }
+                    wave_lds_fence();
+                };
                 if (endp) {
                     go = false;
                     if (Mm) anchor = base + eL;
+                    if (kLinked) {   // the next block starts from this table: no ip-2 fill after a match
+                        // ending past mflimit (lz4.c:1142-1146)
+                        const bool endm = Mm && base + eL >= mfe;
+                        restore(endm && eL - 2 < LZH_WAVE ? I & ~(1ull << (eL - 2)) : I);
+                    }
                 } else {
                     if (Mm) {
                         const int ip = base + eL;
@@ -995,21 +1367,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         q = base + hi0 + 1;
                         pins = -1;
                     }
-                    // table: the last inserted lane of each slot, or the slot's old value
-                    const bool inI = lane_on(I);
-                    if (LZH_BRFREE && vmask == ~0ull) {
-                        // every lane stores its slot's final value (all lanes of a slot agree):
-                        // the slot's last inserted lane, else its old value
-                        const uint64_t gi = grp & I;
-                        T.put(h, gi ? (uint32_t)(base + 63 - __builtin_clzll(gi)) : old);
-                    } else if (!losers) {
-                        if (valid && !inI) T.put(h, old);
-                    } else {
-                        const uint64_t gi = grp & I;
-                        const bool wr = valid && (gi == 0 || (inI && (gi & ~((2ull << lane) - 1ull)) == 0));
-                        if (wr) T.put(h, inI ? (uint32_t)p : old);
-                    }
-                    wave_lds_fence();
+                    restore(I);
                     if (!Mm && hi0 == qlim - base) {                   // 64 probes done: stride batches
                         runb = false;
                         s = so + 1;
@@ -1074,6 +1432,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 {
                     const int lit = P - bk - anchor, mlx = bk + cnt;
                     rc_anc = (uint32_t)anchor;
+                    rc_p = (uint32_t)P;
                     rc_lit = kRec ? (uint32_t)P : (uint32_t)lit;   // kRec: the match start P
                     rc_off = (uint32_t)(P - M);
                     rc_mlx = (uint32_t)mlx;
@@ -1083,7 +1442,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 }
                 const int ip = P + kMinMatch + cnt;
                 anchor = ip;
-                if (ip >= mfl1) {
+                if (ip >= mfe) {
                     go = false;
                 } else if (acc == 1 || kFast) {                        // back to run batches
                     runb = true;
@@ -1109,15 +1468,26 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
     wait_vm();
     R.ready = R.fill;
     wave_lds_fence();
-    RUN_RECORDS();
-    RECS_OUT();
+    if (!aborted) {
+        RUN_RECORDS();
+        RECS_OUT();
+    }
     if (kRec) {
         if (lane == 0) { rec_hdr[0] = (uint32_t)nrec; rec_hdr[1] = (uint32_t)anchor; }
     } else {
-        if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
-        op = emit_seq(in, R, out, O, op, anchor, n - anchor, false, 0, 0, lane);
-        O.flush(out, op, lane);
-        if (lane == 0) *out_size = (uint32_t)op;
+        const int run = b0 + n - anchor;
+        if (kLinked && !aborted && op + run + 1 + (run + 240) / 255 > lk->cap) {   // last literals (lz4.c:1207-1216)
+            lk->abort = -2;
+            aborted = true;
+        }
+        if (kLinked && aborted) {   // the block is stored raw: nothing to emit
+            if (lane == 0 && out_size) *out_size = (uint32_t)n;
+        } else {
+            if (op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
+            op = emit_seq(in, R, out, O, op, anchor, run, false, 0, 0, lane);
+            O.flush(out, op, lane);
+            if (lane == 0 && out_size) *out_size = (uint32_t)op;
+        }
     }
     if (kStats && lane == 0) {
         for (int i = 0; i < kCtr; i++) atomicAdd(&stats[i], (unsigned long long)ctr[i]);
@@ -1155,6 +1525,93 @@ lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_read
         if (acc > 1) lz4v3::compress_chunk<false, false, false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
         else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
     }
+}
+
+// LZ4 frames with linked blocks (LZ4F_blockLinked, the LZ4F default; lz4frame.c:651-655, :777-782):
+// one wave per frame walks its blocks in order with one byU32 table, as LZ4_compress_fast_continue
+// does over a stable source (lz4.c:1565-1628, prefix mode).  Each block is compressed with the
+// limitedOutput budget size - 1 (LZ4F_makeBlock, lz4frame.c:740-763); a block that does not fit is
+// stored raw (bcs = its size) and its table is rebuilt as the reference leaves it at the failing
+// check: the table is saved to `snap` (16 KiB per frame) before every block and a failed block is
+// replayed from it up to the failing probe.  A frame of one block is independent (lz4frame.c:394-395)
+// and goes through the chunk codec.  Block i of frame f: staging slot f * bpf + b, size bcs[i].
+template <bool kFast>
+__device__ void lz4f_linked_frame(const Bytes& rin, uint64_t s, uint64_t bs, uint32_t bpf, uint64_t f, int acc,
+                                  uint8_t* stage, uint64_t stride, uint32_t* bcs, uint32_t* snap, LDSA uint32_t* tab,
+                                  LDSA uint32_t* ring, LDSA uint8_t* outb) {
+    const int lane = threadIdx.x;
+    const rsrc_t nr = make_rsrc(nullptr, 0);
+    const uint32_t nb = (uint32_t)((s + bs - 1) / bs);
+    const rsrc_t sn = make_rsrc(snap + f * 4096, 16384);
+    for (uint32_t b = 0; b < nb; b++) {
+        const int b0 = (int)(b * bs), bn = (int)min<uint64_t>(bs, s - b * bs);
+        const uint64_t i = f * bpf + b;
+        if (b > 0) {   // the table before this block (a failed block replays from it)
+            wave_lds_fence();
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int d = 4 * (k * LZH_WAVE + lane);
+                const u32x4 v = {tab[d], tab[d + 1], tab[d + 2], tab[d + 3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, sn, 4 * d, 0, 0);
+            }
+        }
+        Bytes rout;
+        rout.init(stage + i * stride, stride);
+        lz4v3::LinkCtl L{b0, bn - 1, -1, b > 0, -1};
+        lz4v3::compress_chunk<false, false, false, kFast, false, true>(rin, bn, rout, acc, tab, ring, outb, bcs + i,
+                                                                        nullptr, nr, nullptr, &L);
+        if (L.abort >= 0) {   // replay up to the failing probe: the table the next block starts from
+            if (b > 0) {
+                wait_vm();
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int d = 4 * (k * LZH_WAVE + lane);
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(sn, 4 * d, 0, 0);
+                    tab[d] = v[0]; tab[d + 1] = v[1]; tab[d + 2] = v[2]; tab[d + 3] = v[3];
+                }
+                wave_lds_fence();
+            }
+            Bytes nul;
+            nul.r = nr;
+            nul.sh = 0;
+            lz4v3::LinkCtl Rp{b0, 0x7fffffff, L.abort, b > 0, -1};
+            lz4v3::compress_chunk<false, false, false, kFast, false, true>(rin, bn, nul, acc, tab, ring, outb, nullptr,
+                                                                            nullptr, nr, nullptr, &Rp);
+        }
+        wave_lds_fence();
+    }
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_lz4f_linked_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t fs, uint64_t bs, uint32_t bpf,
+                       int acc, uint8_t* stage, uint64_t stride, uint32_t* bcs, uint32_t* snap) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4];
+    const uint64_t f = blockIdx.x;
+    const uint64_t foff = f * fs;
+    if (foff >= n_total) return;
+    const uint64_t s = min(fs, n_total - foff);
+    Bytes rin;
+    rin.init(in + foff, min<uint64_t>(in_readable - foff, s + 64));
+    LDSA uint32_t* tab = (LDSA uint32_t*)lds;
+    LDSA uint32_t* ring = tab + 4096;
+    LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
+    if (s <= bs) {   // one block: independent (the chunk codec with its own table type)
+        const rsrc_t nr = make_rsrc(nullptr, 0);
+        Bytes rout;
+        rout.init(stage + f * bpf * stride, stride);
+        uint32_t* cs = bcs + f * bpf;
+        const int n = (int)s;
+        if (n < 65547) {
+            if (acc > 1) lz4v3::compress_chunk<true, false, false, true>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
+            else lz4v3::compress_chunk<true, false>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
+        } else {
+            if (acc > 1) lz4v3::compress_chunk<false, false, false, true>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
+            else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
+        }
+        return;
+    }
+    if (acc > 1) lz4f_linked_frame<true>(rin, s, bs, bpf, f, acc, stage, stride, bcs, snap, tab, ring, outb);
+    else lz4f_linked_frame<false>(rin, s, bs, bpf, f, acc, stage, stride, bcs, snap, tab, ring, outb);
 }
 
 // debug twin of the parse kernel with event counters and phase clocks (tools/lz4_stats.py)
@@ -1214,7 +1671,7 @@ lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, 
     uint32_t* hdr = rec_hdr + 2 * chunk;
     if (n < 65547) {
         if (acc > 1) lz4v3::compress_chunk<true, false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
-        else lz4v3::compress_chunk<true, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+        else lz4v3::compress_chunk<true, false, true, false, LZH_WIDE>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
     } else {
         if (acc > 1) lz4v3::compress_chunk<false, false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
         else lz4v3::compress_chunk<false, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
@@ -1436,6 +1893,15 @@ hipError_t lzh_launch_lz4_split(const uint8_t* in, uint64_t n_total, uint64_t in
     if (stage_mask & 2)
         hipLaunchKernelGGL(lzh_lz4_emit_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable, chunk_size,
                            (const uint8_t*)recs, rs, (const uint32_t*)hdr, stage, stride, csizes, frame_size, bpf);
+    return hipGetLastError();
+}
+
+hipError_t lzh_launch_lz4f_linked(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t fs, uint64_t bs,
+                                  uint32_t bpf, int acc, uint8_t* stage, uint64_t stride, uint32_t* bcs, uint32_t* snap,
+                                  uint32_t nframes, hipStream_t s) {
+    if (nframes == 0) return hipSuccess;
+    hipLaunchKernelGGL(lzh_lz4f_linked_kernel, dim3(nframes), dim3(64), 0, s, in, n_total, in_readable, fs, bs, bpf, acc,
+                       stage, stride, bcs, snap);
     return hipGetLastError();
 }
 

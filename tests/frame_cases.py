@@ -39,3 +39,17 @@ def corrupt(rng, s: bytes) -> bytes:
         i = int(rng.integers(0, max(1, len(b) - 4)))
         b[i:i + 4] = int(rng.integers(0, 1 << 32)).to_bytes(4, "little")
     return bytes(b)
+
+
+def near_limit_blocks(rng, nblocks, bs=65536):
+    """Blocks whose LZ4 size lands near the raw limit (bs - 1): random bytes with copies of earlier
+    bytes spliced in at a per-block density, some copies reaching back into the previous block."""
+    d = rng.integers(0, 256, nblocks * bs + int(rng.integers(0, 5000)), dtype=np.uint8)
+    for b in range(nblocks):
+        for _ in range(int(rng.integers(150, 330))):
+            dst = b * bs + int(rng.integers(8, bs - 8))
+            src = dst - int(rng.integers(4, 65535 if rng.random() < 0.2 else 4000))
+            if src >= 0:
+                ln = int(rng.integers(8, 17))
+                d[dst:dst + ln] = d[src:src + ln].copy()
+    return d

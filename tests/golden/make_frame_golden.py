@@ -5,9 +5,9 @@ Run in the build container (needs oracle/_ref/libref.so: lz4 1.9.3 incl. lz4fram
 xxhash.c compiled from /root/reference by `make -C oracle ref`).  Inputs come from
 lzbench_amd.datagen (deterministic), so only digests are stored:
 
-  lz4f   one LZ4 frame per chunk: LZ4F_compressFrame with independent blocks and the listed
-         params (bits 0-2 blockSizeID, 0x10 block checksum, 0x20 content checksum, 0x40 content
-         size, bits 8-15 acceleration), lzbench's raw-store rule per chunk
+  lz4f   one LZ4 frame per chunk: LZ4F_compressFrame with the listed params (bits 0-2
+         blockSizeID, 0x10 block checksum, 0x20 content checksum, 0x40 content size, 0x80 linked
+         blocks, bits 8-15 acceleration), lzbench's raw-store rule per chunk
   nvlz4  one nvcomp LZ4 container per chunk around reference LZ4_compress_default blocks of
          1 << (15 + level) bytes (the layout itself is a restatement: nvcomp cannot be built)
 
@@ -44,6 +44,13 @@ CASES = [
     ("lz4f", "text", 16 * MiB, 16 * MiB, 7 | 0x70),
     ("lz4f", "text", 4 * MiB, 65536, 0x300),
     ("lz4f", "json", 4 * MiB + 3, 200 * 1024, 4 | 0x1100),
+    # linked blocks (0x80 = LZ4F_blockLinked, what LZ4F_compressFrame does with default preferences)
+    ("lz4f", "text", 8 * MiB, 131072, 0x80),
+    ("lz4f", "mixed", 8 * MiB, 1 << 20, 0x80),
+    ("lz4f", "json", 6 * MiB + 12345, 1 << 20, 5 | 0x80 | 0x20),
+    ("lz4f", "random", 4 * MiB, 262144, 0x80 | 0x10),
+    ("lz4f", "binary", 4 * MiB, 262144, 0x80 | 0x300),
+    ("lz4f", "mixed", 6 * MiB + 7, 300 * 1024, 0x80 | 0x40),
     ("nvlz4", "text", 8 * MiB, 65536, 0),
     ("nvlz4", "json", 8 * MiB + 99, 1 << 20, 1),
     ("nvlz4", "mixed", 8 * MiB, 4 << 20, 3),

@@ -155,4 +155,5 @@ def test_level_supported():
     assert lib.lzh_level_supported(3, 3, 65536) == 0
     assert lib.lzh_level_supported(3, -5, 1 << 20) == 1
     assert lib.lzh_level_supported(4, 0x88, 65536) == 0 and lib.lzh_level_supported(4, 0x74, 65536) == 1
+    assert lib.lzh_level_supported(4, 0x80, 65536) == 1 and lib.lzh_level_supported(4, 0x3F4, 1 << 20) == 1
     assert lib.lzh_level_supported(5, 6, 65536) == 0 and lib.lzh_level_supported(0, 1, 65536) == 1

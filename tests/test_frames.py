@@ -62,20 +62,6 @@ def test_lz4f_raw_block_boundary():
         assert a == b
 
 
-def _near_limit_blocks(rng, nblocks, bs=65536):
-    """Blocks whose LZ4 size lands near the raw limit (bs - 1): random bytes with copies of earlier
-    bytes spliced in at a per-block density, some copies reaching back into the previous block."""
-    d = rng.integers(0, 256, nblocks * bs + int(rng.integers(0, 5000)), dtype=np.uint8)
-    for b in range(nblocks):
-        for _ in range(int(rng.integers(150, 330))):
-            dst = b * bs + int(rng.integers(8, bs - 8))
-            src = dst - int(rng.integers(4, 65535 if rng.random() < 0.2 else 4000))
-            if src >= 0:
-                ln = int(rng.integers(8, 17))
-                d[dst:dst + ln] = d[src:src + ln].copy()
-    return d
-
-
 def test_lz4f_linked_raw_decisions_vs_reference():
     """Linked frames whose blocks barely do or do not fit size - 1 bytes: a block that fails is stored
     raw and the parse stopped where the first limitedOutput check failed -- the next block starts from
@@ -87,7 +73,7 @@ def test_lz4f_linked_raw_decisions_vs_reference():
     rng = np.random.default_rng(17)
     raw = comp = 0
     for t in range(60):
-        d = _near_limit_blocks(rng, int(rng.integers(2, 6)))
+        d = F.near_limit_blocks(rng, int(rng.integers(2, 6)))
         for p in (0x80, 0x90):
             cap = int(R.ref_lz4f_bound(len(d), p)) + 64
             a = _frame(R.ref_lz4f_compress, d, p, cap)

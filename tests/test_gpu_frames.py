@@ -1,5 +1,5 @@
 """GPU framed formats through the C-ABI: LZ4 frames (LZ4F_compressFrame with
-independent blocks) and nvcomp LZ4 containers, one per chunk, against the REFERENCE digests of
+independent or linked blocks) and nvcomp LZ4 containers, one per chunk, against the REFERENCE digests of
 tests/golden/frames.json and the reference build; decoding of reference frames and of corrupted
 frames (verdicts against the CPU restatement, itself pinned to the reference LZ4F_decompress by
 tests/test_frames.py).  Run with -m gpu."""
@@ -41,7 +41,7 @@ def test_frames_vs_reference_digests(torch_cuda, case):
 @pytest.mark.parametrize("n,chunk", [(1, 65536), (12, 65536), (13, 64), (65535, 65536), (65537, 65536),
                                      (300001, 65536), (300001, 100000), (5 << 20, 1 << 22), (777777, 777777)])
 def test_frames_edge_sizes_vs_restatement(torch_cuda, codec, n, chunk):
-    levels = [0, 5, 0x74, 0x204] if codec == "lz4f" else [0, 2, 5]
+    levels = [0, 5, 0x74, 0x204, 0x80, 0x84, 0xF4, 0x380] if codec == "lz4f" else [0, 2, 5]
     for kind in ("text", "random"):
         data = L.datagen(kind, n, seed=n)
         for lvl in levels:
@@ -94,7 +94,8 @@ def test_device_resident_frames(torch_cuda):
         assert (dc.out[:n].cpu().numpy() == data).all()
 
 
-@pytest.mark.parametrize("codec,params", [("lz4f", 0), ("lz4f", 0x70), ("lz4f", 0x15), ("nvlz4", 0)])
+@pytest.mark.parametrize("codec,params", [("lz4f", 0), ("lz4f", 0x70), ("lz4f", 0x15), ("lz4f", 0x80), ("lz4f", 0xB0),
+                                          ("nvlz4", 0)])
 def test_corrupt_frames_verdicts(torch_cuda, codec, params):
     torch = torch_cuda
     if codec == "lz4f" and not O.have_ref():
@@ -135,6 +136,22 @@ def test_corrupt_frames_verdicts(torch_cuda, codec, params):
             assert out[j * part:(j + 1) * part].tobytes() == dst[:part].tobytes()
         elif r == -2:
             assert st == -2
+
+
+@pytest.mark.parametrize("params", [0x80, 0x90, 0x280])
+def test_linked_frames_near_the_raw_limit(torch_cuda, params):
+    """Linked frames (LZ4F's default) whose blocks barely do or do not fit size - 1 bytes: a failing
+    block is stored raw and the next block starts from the table as the reference left it at the
+    failing check (oracle/frame_oracle.c lz4f_linked_block, pinned to LZ4F_compressFrame by
+    tests/test_frames.py), so every later block's bytes check the GPU's abort point and replay."""
+    rng = np.random.default_rng(params)
+    chunk = 5 * 65536
+    data = np.concatenate([F.near_limit_blocks(rng, 5)[:chunk] for _ in range(12)])
+    exp, ecs = O.compress_chunks(data, "lz4f", chunk, params)
+    packed, cs = L.compress_chunks(data, "lz4frame", chunk, level=params)
+    assert (cs == ecs).all() and len(packed) == len(exp) and (packed == exp).all()
+    out = L.decompress_chunks(packed, cs, len(data), "lz4frame", chunk)
+    assert (out == data).all()
 
 
 def _with_dict_id(frame: bytes, flip_only: bool) -> bytes:
