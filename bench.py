@@ -130,19 +130,21 @@ def cpu_baseline(sample: np.ndarray, codec: str, chunk: int, level: int, iters: 
 
 
 def traffic_for(kernel, workload):
-    """HBM-side bytes per dispatch of `kernel` from the committed PMC profile (profiles/traffic.json,
+    """HBM-side bytes per dispatch of `kernel` from the committed PMC profiles (profiles/traffic*.json,
     written by tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes on the
-    same workload), or None when no profile covers this kernel/workload."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
-    try:
-        with open(path) as f:
-            t = json.load(f)
-        if t.get("workload_key") != workload:
-            return None
-        k = t["kernels"].get(kernel)
-        return None if k is None else int(k["traffic_bytes_per_dispatch"])
-    except (OSError, KeyError, ValueError):
-        return None
+    same workload; one file per workload), or None when no profile covers this kernel/workload."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic*.json"))):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+            if t.get("workload_key") != workload:
+                continue
+            k = t["kernels"].get(kernel)
+            return None if k is None else int(k["traffic_bytes_per_dispatch"])
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 def fullsize_digest(corpus, codec, chunk, level, n, seed):
@@ -407,7 +409,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": traffic_for(kname, wkey),
-            "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE + WRITE_SIZE, separate passes, per launch)",
+            "traffic_source": "profiles/traffic*.json (rocprofv3 FETCH_SIZE + WRITE_SIZE, separate passes, per launch)",
             "kernel": kname,
             "kernel_ms": round(k_ms, 3),
             "algorithmic_bytes_per_launch": int(algo_bytes),

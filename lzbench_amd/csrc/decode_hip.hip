@@ -310,104 +310,6 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
-#ifndef LZH_DEC_DPPOWN
-#define LZH_DEC_DPPOWN 0   // (DPP prefix-max owner: measured neutral for lz4, 1 % slower for snappy)
-#endif
-// Wave-wide inclusive prefix maximum (DPP; -1 is the identity for the marks below).
-__device__ __forceinline__ int wave_incl_max(int x) {
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));   // row_shr:1
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));   // row_shr:2
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));   // row_shr:4
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));   // row_shr:8
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));   // row_bcast:15
-    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));   // row_bcast:31
-    return x;
-}
-
-// Assemble a group's output [op, op + total): sequence k (member lane k, output start excl) is
-// litk literal bytes from stream position ip + lrel, then mlk match bytes copied from offset offk
-// (byte-by-byte semantics); a literal-only member has mlk = 0, a copy-only member litk = 0.
-// One output byte per lane per pass; the owner is the last start mark at or before the byte.
-template <class W, class SinkType>
-__device__ __forceinline__ void emit_group1(const W& w, SinkType& O, LDSA uint8_t* mark, int ip, int op,
-                                            int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
-                                            int off, int lane) {
-    const bool kmem = lane_on(keep);
-    int carry = 63 - __builtin_clzll(keep);                      // (pass 0 always has a start at 0)
-    const uint32_t xl = ((uint32_t)excl << 10) | lrel;           // (lrel < 1024, excl < 2^22)
-    // Branch-free pass body: lanes that have nothing to store write to harmless places (the mark
-    // scratch's second half, or output bytes past `total` / of this pass that a later round or
-    // group overwrites before any flush), so no exec-mask juggling per conditional access.
-    for (int pass = 0; pass * LZH_WAVE < total; pass++) {
-        const int pb = pass * LZH_WAVE;
-        mark[lane] = 0xff;
-        wave_lds_fence();
-        const bool mine = kmem && excl >= pb && excl < pb + LZH_WAVE;
-        mark[mine ? excl - pb : LZH_WAVE + lane] = (uint8_t)lane;
-        wave_lds_fence();
-        const int mv = (int)mark[lane];
-        int k;
-        if (LZH_DEC_DPPOWN) {
-            // members' lane ids grow with their output starts: the owner is a prefix maximum
-            const int km = wave_incl_max(mv == 0xff ? -1 : mv);
-            k = km >= 0 ? km : carry;
-        } else {
-            const uint64_t S = ballot(mv != 0xff);
-            const uint64_t le = S & ((2ull << lane) - 1ull);
-            const int js = le ? 63 - __builtin_clzll(le) : lane;
-            const int own_here = (int)lane_gather((uint32_t)mv, js);
-            k = le ? own_here : carry;
-        }
-        carry = rdlanei(k, 63);
-        const uint32_t a = lane_gather(pA, k);
-        const uint32_t xk = lane_gather(xl, k);
-        const uint32_t b = xk & 1023u;
-        const int ek = (int)(xk >> 10);
-        const int offk = (int)lane_gather((uint32_t)off, k);
-        const int litk = (int)(a & 0xffffu);
-        const int ob = pb + lane;
-        const bool act = ob < total;
-        const int u = ob - ek;
-        const bool is_lit = u < litk;
-        const uint32_t lb = w.lane_byte(ip + (int)b + (is_lit ? u : 0));
-        const int mu = u - litk;
-        const int mstart = op + ek + litk;
-        int src = mstart - offk + mu;
-        if (ballot(act && !is_lit && mu >= offk)) {                // overlapping copy: period offk
-            const int md = (int)((uint32_t)mu % (uint32_t)max(offk, 1));
-            src = (!is_lit && mu >= offk) ? mstart - offk + md : src;
-        }
-        const int pbase = op + pb;
-        const bool near = !is_lit && src >= O.ringlo && src >= pbase + LZH_WAVE - SinkType::kWin;
-        const bool inpass = !is_lit && src >= pbase;
-        const uint32_t g = O.get(src);
-        uint32_t v = is_lit ? lb : g;
-        bool done = is_lit || (near && !inpass);
-        const bool far = act && !is_lit && !near;
-        if (ballot(far)) {   // far sources were flushed long ago: their stores must be done
-            wait_vm();
-            const uint32_t gv = O.out.b_sc1(far ? src : 0);
-            v = far ? gv : v;
-            done = done || far;
-        }
-        O.put(op + ob, v);
-        uint64_t dm = ballot(act && done) | ~ballot(act);
-        for (int r = 0; r < LZH_WAVE && ~dm; r++) {
-            const int sl = src - pbase;
-            const bool ready = !lane_on(dm) && ((dm >> (sl & 63)) & 1ull);
-            const uint32_t vv = O.get(src);
-            v = ready ? vv : v;
-            O.put(op + ob, v);
-            dm |= ballot(ready);
-        }
-        O.maybe_flush(min(pbase + LZH_WAVE, op + total), lane);
-    }
-}
-
-
-#ifndef LZH_DEC_PAIR
-#define LZH_DEC_PAIR 1   // 0: one byte per lane per pass (emit_group1)
-#endif
 // Output byte ob (group-relative) from its owner's fields, precomputed per member so that a byte
 // costs adds and compares only: lend = the owner's literal end (group-relative), lsb = stream
 // position of its literal byte at ob = lsb + ob, msrc = absolute output position of its match
@@ -434,15 +336,8 @@ __device__ __forceinline__ uint32_t owned_byte(const W& w, const SinkType& O, in
 }
 
 // The part of a 128-byte pass after its far reads are issued (their data are used here first):
-// store the bytes, resolve in-pass sources in dependency rounds, flush.  A group's last pass with far
-// reads can be left pending (Tail::live) and finished after the next group's parse -- which reads
-// only the input window, never the output window -- so that parse runs under the far reads' round
-// trip.  Finish before anything else touches the output window.
-#ifndef LZH_DEC_DEFER
-#define LZH_DEC_DEFER 0   // (measured: lz4 -b64 text 3.9 -> 4.2 ms, snappy -b256 6.6 -> 7.2 ms with it)
-#endif
+// store the bytes, resolve in-pass sources in dependency rounds, flush.
 struct Tail {
-    bool live;
     bool far0, far1, done0, done1;
     uint32_t v0, v1, g0, g1;
     int src0, src1, ob0, ob1, pbase, op, total;
@@ -475,26 +370,15 @@ __device__ __forceinline__ void pass_tail(SinkType& O, Tail& t, int lane) {
         dm1 |= ballot(rd1);
     }
     O.maybe_flush(min(pbase + kP, op + t.total), lane);
-    t.live = false;
-}
-
-template <class SinkType>
-__device__ __forceinline__ void finish_tail(SinkType& O, Tail& t, int lane) {
-    if (t.live) pass_tail(O, t, lane);
 }
 
 // Two output bytes per lane per pass (128-byte passes): a byte pair has at most two owners (the
 // member owning its first byte, and one starting at its second), so each pass gathers two sets of
-// member fields instead of one per 64 bytes.  Marks: 128 bytes + 64 bytes of scratch.  kDefer: the
-// last pass's tail may stay pending in t (see Tail).
-template <bool kDefer = false, class W, class SinkType>
+// member fields instead of one per 64 bytes.  Marks: 128 bytes + 64 bytes of scratch.
+template <class W, class SinkType>
 __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t* mark, int ip, int op,
                                            int total, uint64_t keep, int excl, uint32_t pA, uint32_t lrel,
-                                           int off, int lane, Tail* tp = nullptr) {
-    if (!LZH_DEC_PAIR) {
-        emit_group1(w, O, mark, ip, op, total, keep, excl, pA, lrel, off, lane);
-        return;
-    }
+                                           int off, int lane) {
     constexpr int kP = 2 * LZH_WAVE;
     const bool kmem = lane_on(keep);
     int carry = 63 - __builtin_clzll(keep);                      // (pass 0 always has a start at 0)
@@ -503,8 +387,7 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
     const int m_lsb = ip + (int)lrel - excl;
     const int m_msrc = op - off;
     const uint64_t below = (1ull << lane) - 1ull;
-    Tail lt;
-    Tail& t = kDefer ? *tp : lt;
+    Tail t;
     for (int pb = 0; pb < total; pb += kP) {
         DMARK(10);
         ((volatile LDSA uint16_t*)mark)[lane] = 0xffffu;
@@ -553,10 +436,6 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
         t.far0 = far0; t.far1 = far1; t.done0 = done0; t.done1 = done1;
         t.v0 = v0; t.v1 = v1; t.src0 = src0; t.src1 = src1; t.ob0 = ob0; t.ob1 = ob1;
         t.pbase = pbase; t.op = op; t.total = total;
-        if (kDefer && anyfar && pb + kP >= total) {   // the group's last pass: finish it later
-            t.live = true;
-            return;
-        }
         DMARK(13);
         pass_tail(O, t, lane);
         DMARK(14);
@@ -567,23 +446,7 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
 // >= 64 = leaves the group, 255 = the lane itself is not taken), by binary lifting: jump tables
 // J_k = link^(2^k) through ds_bpermute, then every lane lifts from lane 0 to the furthest chain
 // lane <= itself.  No scalar walk (the decoder is scalar-issue bound).
-#ifndef LZH_DEC_WALK
-#define LZH_DEC_WALK 0
-#endif
 __device__ __forceinline__ uint64_t chain_members(int link, int lane) {
-    if (LZH_DEC_WALK) {
-        // scalar walk: one v_readlane per member (links strictly increase, so <= 64 steps)
-        uint64_t M = 0;
-        int sl = 0;
-        for (int it = 0; it < LZH_WAVE; it++) {
-            const int nx = rdlanei(link, sl);
-            if (nx == 255) break;
-            M |= 1ull << sl;
-            if (nx >= LZH_WAVE) break;
-            sl = nx;
-        }
-        return M;
-    }
     // (every member takes >= 2 stream bytes -- a snappy literal tag + 1 byte or a COPY_1, LZ4 >= 3 --
     // so a chain from lane 0 has at most 32 members: jumps of 1..16 reach every one of them)
     const int J0 = min(link, LZH_WAVE);
@@ -609,8 +472,6 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
     w.bind(in, ring);
     w.load(0, lane);
     int ip = 0, op = 0;
-    Tail tl;
-    tl.live = false;
     for (int guard = 0; guard <= cs; guard++) {
         DCLK(t0);
         DMARK(0);
@@ -645,7 +506,6 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
                                  (mc == 15 && po + 3 >= cs - 4) || off == 0 || off > opm + prefix || opm + ml > cap - 5);
         const uint64_t badm = ballot(bad);
         const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
-        finish_tail(O, tl, lane);   // (the previous group's last pass: its far reads ran under this parse)
         if (!keep) {
             const int r = checked::lz4_one(in, cs, O, w, cap, ip, op, lane, prefix);
             DST(6, 1);
@@ -661,10 +521,8 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
         const int ip_next = ip + rdlanei(pe - ip, lastk);
         DCLK(t1);
         DMARK(3);
-#ifndef LZH_ABL_NOEMIT
-        emit_group<LZH_DEC_DEFER>(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)ml << 16),
-                         (uint32_t)(p1 - ip), off, lane, &tl);
-#endif
+        emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)ml << 16), (uint32_t)(p1 - ip),
+                   off, lane);
 #if LZH_DEC_STATS
         DCLK(t2);
         DST(0, 1);
@@ -676,7 +534,6 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
         op += total;
         ip = ip_next;
     }
-    finish_tail(O, tl, lane);
     return op;
 }
 
@@ -705,8 +562,6 @@ __device__ int snappy_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t*
     if (ulen > (uint32_t)cap) return -1;
     const int ul = (int)ulen;
     int op = 0;
-    Tail tl;
-    tl.live = false;
     for (int guard = 0; guard <= cs && ip < cs; guard++) {
         ip = unii(ip); op = unii(op);
         O.flushed = unii(O.flushed); O.ringlo = unii(O.ringlo);
@@ -751,7 +606,6 @@ __device__ int snappy_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t*
         const bool bad = mem && (x >= cs || !okr || opm + len > ul || (kind != 0 && off > opm));
         const uint64_t badm = ballot(bad);
         const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
-        finish_tail(O, tl, lane);
         if (!keep) {
             // one tag through the checked path (snappy.cc:848-952 rules)
             const uint32_t cc = w.byte(ip++);
@@ -794,12 +648,11 @@ __device__ int snappy_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t*
         const int lastk = 63 - __builtin_clzll(keep);
         const int total = rdlanei(incl, lastk);
         const int ip_next = ip + rdlanei(nx - ip, lastk);
-        emit_group<LZH_DEC_DEFER>(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)(len - lit) << 16),
-                         (uint32_t)(p1 - ip), off, lane, &tl);
+        emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)(len - lit) << 16),
+                   (uint32_t)(p1 - ip), off, lane);
         op += total;
         ip = ip_next;
     }
-    finish_tail(O, tl, lane);
     return op == ul ? op : -1;
 }
 

@@ -18,9 +18,6 @@
 // Long catch-ups / matches / literal runs beyond the windows take lane-parallel slow paths.
 #include "common.h"
 
-#define LZH_STR_(x) #x
-#define LZH_STR(x) LZH_STR_(x)
-
 namespace lz4v3 {
 
 // optional per-kernel event counters (debug builds of the launch only; nullptr in production)
@@ -108,22 +105,6 @@ struct Ring {
         fill += 256;
     }
 };
-
-#ifndef LZH_UNI_GO
-#define LZH_UNI_GO 0   // (1 measured 3.5 % slower: 14.47 -> 14.97 ms, profiles/r03_h) the batch loop's exit test through readfirstlane (a uniform loop, no exec-mask latch)
-#endif
-
-#ifndef LZH_LOOP_UNI
-#define LZH_LOOP_UNI 1   // readfirstlane the loop-carried parse state at the top of every batch
-#endif
-
-#ifndef LZH_PARSE_LIFT
-#define LZH_PARSE_LIFT 0   // chain membership by binary lifting (lane gathers) instead of the scalar walk
-#endif
-
-#ifndef LZH_PARSE_NORING
-#define LZH_PARSE_NORING 0   // parse kernel without the LDS input ring (16 KiB LDS: 10 waves per CU)
-#endif
 
 __device__ __forceinline__ int ext_len_bytes(int v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
 
@@ -545,45 +526,6 @@ __device__ __forceinline__ uint64_t lane_bits(int lo, int hi) {   // bits lo..hi
     return ((2ull << hi) - 1ull) & (~0ull << lo);                 // 2 << 63 wraps to 0: all ones
 }
 
-// ---- 128-position run batches (kWide): lane l holds positions base+l (half 0) and base+64+l (half 1);
-// 128-bit position masks are pairs of 64-bit ballots (word 0 = half 0, word 1 = half 1).
-constexpr int kOut128 = 128;      // link code: the chain continues past the batch
-constexpr int kExh128 = 129;      // link code: the 65 step-1 probes of the segment end inside the batch, no hit
-constexpr int kSpc128 = 130;      // link code: long match (count past the window) or a match end past mflimit
-
-__device__ __forceinline__ int msb64(uint64_t m) { return 63 - __builtin_clzll(m); }   // (m != 0)
-
-// first hit of A0:A1 in the segment [e, e + 64] (the re-test at a match end e plus 64 step-1 search
-// probes, lz4.c:955-969) clipped to the batch; kExh128 when the segment lies inside the batch (e <= 63)
-// and has no hit, kOut128 when it runs past the batch
-__device__ __forceinline__ int next_hit128(uint64_t A0, uint64_t A1, int e) {
-    const int ec = min(e, 127);
-    const uint64_t m0 = ec < 64 ? A0 & (~0ull << ec) : 0ull;
-    const uint64_t m1 = ec < 64 ? A1 & ((2ull << ec) - 1ull) : A1 & (~0ull << (ec & 63));
-    const int r = m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : (e < 64 ? kExh128 : kOut128));
-    return e >= 128 ? kOut128 : r;
-}
-
-// candidate window taken from the input ring (a candidate inside the batch) compared with the P side:
-// ok = 4-byte seed (lz4.c:1005), len = LZ4_count bytes past +4 capped at 20
-__device__ __forceinline__ bool eval_ring(const PSide& P, const PSide& Q, bool valid, int& len) {
-    len = first_diff20(P.q0 ^ Q.q0, P.q1 ^ Q.q1, P.q2 ^ Q.q2, P.q3 ^ Q.q3, P.q4 ^ Q.q4);
-    return valid && P.w == Q.w;
-}
-
-// the same against a global candidate window (MWin) without the catch-up bytes
-__device__ __forceinline__ bool eval_fwd(const PSide& P, const MWin& W, bool valid, int& len) {
-    const uint32_t s = (uint32_t)W.sm;
-    const uint32_t mw = __builtin_amdgcn_alignbyte(W.d2, W.d1, s);
-    const uint32_t x0 = P.q0 ^ __builtin_amdgcn_alignbyte(W.d3, W.d2, s);
-    const uint32_t x1 = P.q1 ^ __builtin_amdgcn_alignbyte(W.d4, W.d3, s);
-    const uint32_t x2 = P.q2 ^ __builtin_amdgcn_alignbyte(W.d5, W.d4, s);
-    const uint32_t x3 = P.q3 ^ __builtin_amdgcn_alignbyte(W.d6, W.d5, s);
-    const uint32_t x4 = P.q4 ^ __builtin_amdgcn_alignbyte(W.d7, W.d6, s);
-    len = first_diff20(x0, x1, x2, x3, x4);
-    return valid && mw == P.w;
-}
-
 // Group lanes by table slot (one ballot per slot that has a collision): grp = lanes sharing
 // this lane's slot; prev = the closest earlier lane in it (-1 if none).
 __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t losers, uint64_t& grp, int& prev,
@@ -645,266 +587,6 @@ __device__ __forceinline__ void slot_groups(uint32_t h, bool valid, uint64_t los
         }                                                                                          \
     } while (0)
 
-// P side at p from the ring when the batch is in it, else from global memory
-__device__ __forceinline__ PSide p_side_at(bool rg, const Ring& R, const Bytes& in, int p) {
-    return rg ? p_side_ring_m<false>(R, p) : p_side_global(in, p);
-}
-
-#ifndef LZH_WIDE
-#define LZH_WIDE 0   // 128-position run batches in the parse kernel (acceleration 1, byU16): measured slower (text 15.9 -> 18.2 ms compress), kept off
-#endif
-
-// One 128-position run batch of the parse kernel (acceleration 1, byU16 table, records out):
-// positions base .. base+127, two per lane (base+l, base+64+l).  The same resolve as the 64-lane
-// run batch in compress_chunk -- hash, read the slot (the candidate), claim it, read it back; the
-// candidate windows of all 128 positions in one memory round trip; the chain of sequences from the
-// batch's search start by a scalar walk over per-position links; probed / inserted sets; colliders
-// re-resolved until consistent -- over twice the input per round trip, resolve and loop overhead.
-// Positions of one segment (a match end re-tested, then 64 step-1 search probes, lz4.c:955-969 and
-// :1148-1200) may now end inside the batch: the walk stops there and stride batches take over.
-// Records go out at the end of the batch.  Returns false when the parse has ended.
-__device__ __forceinline__ bool run_batch128(const Bytes& in, Ring& R, const Table<true>& T, rsrc_t recs, int lane,
-                                             int mfl1, int mlimit, int endX, int& base, int& q, int& qlim, int& pins,
-                                             int& s, int& k0, bool& runb, bool& retest, int& anchor, int& nrec,
-                                             uint32_t rc_lit, uint32_t rc_off, uint32_t rc_mlx, uint64_t& rc_m) {
-    constexpr int W = LZH_WAVE;
-    {   // a stride batch's pending record (its one sequence)
-        if (uni64(rc_m)) {
-            if (lane == 0) st_b64(recs, 8 * nrec, rc_lit | (rc_mlx << 24), (rc_mlx >> 8) | (rc_off << 16));
-            nrec = unii(nrec + 1);
-        }
-        rc_m = 0;
-    }
-    const int p0 = base + lane, p1 = p0 + W;
-    const bool v0 = p0 + 1 <= mfl1, v1 = p1 + 1 <= mfl1;   // forwardIp <= mflimitPlusOne (lz4.c:969)
-    const uint64_t vm0 = ballot(v0), vm1 = ballot(v1);
-    const int fv = __builtin_popcountll(vm0) + __builtin_popcountll(vm1);   // valid positions: [0, fv)
-    const bool rg = R.has(base - 4, base + 2 * W + 28);
-    const PSide s0 = p_side_at(rg, R, in, p0), s1 = p_side_at(rg, R, in, p1);
-    const uint32_t h0 = hash_of<true>(s0.w, 0), h1 = hash_of<true>(s1.w, 0);
-    const uint32_t old0 = T.get(h0), old1 = T.get(h1);
-    MWin W0, W1;
-    W0.load(in, old0, v0);                                    // (issued before the claim round trip)
-    W1.load(in, old1, v1);
-    // claims (the half-1 stores come second: a slot claimed in both halves holds a half-1 position)
-    if (vm0 == ~0ull) T.put(h0, (uint32_t)p0); else if (v0) T.put(h0, (uint32_t)p0);
-    if (vm1 == ~0ull) T.put(h1, (uint32_t)p1); else if (v1) T.put(h1, (uint32_t)p1);
-    wave_lds_fence();
-    const uint32_t bk0 = T.get(h0), bk1 = T.get(h1);
-    const uint64_t los = ballot(v0 && bk0 != (uint32_t)p0) | ballot(v1 && bk1 != (uint32_t)p1);
-    // slot groups (under the candidate loads): every position of a slot read back the same claim
-    // winner w (0..127), so equal w <=> same slot; equality bit-sliced over 7 ballots per half.
-    // g00 = half-0 members of x0's slot; g10 / g11 = half-0 / half-1 members of x1's slot.
-    const uint64_t self = 1ull << lane, below = self - 1ull;
-    uint64_t g00 = self, g10 = 0, g11 = self;
-    int prev0 = -1, prev1 = -1;                               // closest earlier position of the slot
-    if (los) {
-        const uint32_t w0 = bk0 - (uint32_t)base, w1 = bk1 - (uint32_t)base;
-        uint32_t a_lo = 0, a_hi = 0, b_lo = 0, b_hi = 0, c_lo = 0, c_hi = 0;
-#pragma unroll
-        for (int b = 0; b < 7; b++) {
-            const uint64_t m0 = ballot((w0 >> b) & 1u), m1 = ballot((w1 >> b) & 1u);
-            const uint32_t t0 = (uint32_t)__builtin_amdgcn_sbfe((int)w0, b, 1);
-            const uint32_t t1 = (uint32_t)__builtin_amdgcn_sbfe((int)w1, b, 1);
-            a_lo |= (uint32_t)m0 ^ t0; a_hi |= (uint32_t)(m0 >> 32) ^ t0;
-            b_lo |= (uint32_t)m0 ^ t1; b_hi |= (uint32_t)(m0 >> 32) ^ t1;
-            c_lo |= (uint32_t)m1 ^ t1; c_hi |= (uint32_t)(m1 >> 32) ^ t1;
-        }
-        g00 = v0 ? ~(((uint64_t)a_hi << 32) | a_lo) & vm0 : self;
-        g10 = v1 ? ~(((uint64_t)b_hi << 32) | b_lo) & vm0 : 0ull;
-        g11 = v1 ? ~(((uint64_t)c_hi << 32) | c_lo) & vm1 : self;
-        const uint64_t e0b = g00 & below, e1b = g11 & below;
-        prev0 = (v0 && e0b) ? msb64(e0b) : -1;
-        prev1 = v1 ? (e1b ? W + msb64(e1b) : (g10 ? msb64(g10) : -1)) : -1;
-    }
-    // colliders: the usual candidate is the closest earlier position of the slot; its window is in
-    // the ring (the batch's own bytes): pre-evaluated under the candidate loads
-    const uint64_t coll0 = ballot(prev0 >= 0), coll1 = ballot(prev1 >= 0);
-    bool okp0 = false, okp1 = false;
-    int lep0 = 0, lep1 = 0;
-    if (coll0 | coll1) {
-        const PSide Q0 = p_side_at(rg, R, in, base + max(prev0, 0)), Q1 = p_side_at(rg, R, in, base + max(prev1, 0));
-        okp0 = eval_ring(s0, Q0, v0, lep0);
-        okp1 = eval_ring(s1, Q1, v1, lep1);
-    }
-    wait_vm();
-    R.ready = R.fill;
-    wave_lds_fence();
-    {   // ring refill after the wait: it completes under the next batch
-        const int target = min(base + in.sh + kAhead, endX + 256);
-        for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
-    }
-    int len0, len1;
-    const bool ok0 = eval_fwd(s0, W0, v0, len0), ok1 = eval_fwd(s1, W1, v1, len1);
-
-    // ---- resolve (lz4.c:1142-1200: match end -> ip-2 fill -> re-test -> search from ip+1)
-    const int lo = q - base, hi0 = min(qlim - base, 2 * W - 1);   // the first segment's probes: lo..hi0
-    const uint64_t P0a = lo < W ? lane_bits(lo, min(hi0, W - 1)) : 0ull;
-    const uint64_t P0b = hi0 >= W ? lane_bits(max(lo, W) - W, hi0 - W) : 0ull;
-    const uint64_t I0 = pins >= 0 ? 1ull : 0ull;              // a pending ip-2 fill at base (lz4.c:1146)
-    int ak0 = prev0, ak1 = prev1;                             // assumed candidate (-1: the slot's old value)
-    bool oe0 = prev0 >= 0 ? okp0 : ok0, oe1 = prev1 >= 0 ? okp1 : ok1;
-    int le0 = prev0 >= 0 ? lep0 : len0, le1 = prev1 >= 0 ? lep1 : len1;
-    uint32_t ce0 = prev0 >= 0 ? (uint32_t)(base + prev0) : old0, ce1 = prev1 >= 0 ? (uint32_t)(base + prev1) : old1;
-    uint64_t Mm0 = 0, Mm1 = 0, Ia0 = 0, Ia1 = 0;
-    int cn0 = 0, cn1 = 0, e0 = 0, e1 = 0, eL = 0, fin = kOut128;
-    bool endip = false;
-    for (int round = 0; round <= 2 * W; round++) {
-        const uint64_t A0 = ballot(oe0), A1 = ballot(oe1);
-        // if position x starts a sequence: match count, end, next hit in the segment at the end
-        cn0 = min(le0, mlimit - (p0 + kMinMatch));
-        cn1 = min(le1, mlimit - (p1 + kMinMatch));
-        const bool lg0 = oe0 && le0 == 20 && p0 + kMinMatch + 20 < mlimit;
-        const bool lg1 = oe1 && le1 == 20 && p1 + kMinMatch + 20 < mlimit;
-        e0 = max(lane + kMinMatch + cn0, 0);
-        e1 = max(W + lane + kMinMatch + cn1, 0);
-        const int lk0 = (lg0 || p0 + kMinMatch + cn0 >= mfl1) ? kSpc128 : next_hit128(A0, A1, e0);
-        const int lk1 = (lg1 || p1 + kMinMatch + cn1 >= mfl1) ? kSpc128 : next_hit128(A0, A1, e1);
-        Mm0 = 0;
-        Mm1 = 0;
-        endip = false;
-        const uint64_t r0 = A0 & P0a, r1 = A1 & P0b;
-        uint64_t E0, E1;                                      // probed positions
-        if (!(r0 | r1)) {
-            E0 = P0a;
-            E1 = P0b;
-            fin = hi0 == qlim - base ? kExh128 : kOut128;
-            Ia0 = I0 | E0;
-            Ia1 = E1;
-        } else {
-            int sl = r0 ? __builtin_ctzll(r0) : W + __builtin_ctzll(r1);
-            int fs = kOut128;
-            for (;;) {                                        // (links strictly increase: the walk ends)
-                if (sl < W) {
-                    for (;;) {
-                        Mm0 |= 1ull << sl;
-                        fs = rdlanei(lk0, sl);
-                        if (fs >= W) break;
-                        sl = fs;
-                    }
-                    if (fs < kOut128) sl = fs;                // into half 1
-                }
-                if (sl >= W) {
-                    for (;;) {
-                        Mm1 |= 1ull << (sl - W);
-                        fs = rdlanei(lk1, sl - W);
-                        if (fs >= kOut128) break;
-                        sl = fs;
-                    }
-                }
-                if (fs != kSpc128) break;                     // the chain leaves the batch / the segment ends
-                const bool h1s = sl >= W;
-                const int sk = sl & (W - 1);
-                int es;
-                if (rdlane((uint32_t)(h1s ? lg1 : lg0), sk)) {   // match runs past the 20-byte window
-                    const int c = slow_count(in, base + sl, (int)rdlane(h1s ? ce1 : ce0, sk), mlimit, lane);
-                    es = sl + kMinMatch + c;
-                    if (h1s) { cn1 = lane == sk ? c : cn1; e1 = lane == sk ? es : e1; }
-                    else { cn0 = lane == sk ? c : cn0; e0 = lane == sk ? es : e0; }
-                    fs = next_hit128(A0, A1, es);
-                } else {
-                    es = rdlanei(h1s ? e1 : e0, sk);
-                }
-                if (base + es >= mfl1) { endip = true; break; }   // lz4.c:1142
-                if (fs >= kOut128) break;
-                sl = fs;
-            }
-            fin = fs;
-            eL = rdlanei(sl >= W ? e1 : e0, sl & (W - 1));
-            // j = the last member at or before each position: positions strictly inside its match are
-            // not probed, its segment [e, e + 64] is; ip-2 of each member is inserted (lz4.c:1146)
-            const uint64_t ml0 = Mm0 & (below | self), ml1 = Mm1 & (below | self);
-            const int j0 = ml0 ? msb64(ml0) : -1;
-            const int j1 = ml1 ? W + msb64(ml1) : (Mm0 ? msb64(Mm0) : -1);
-            const uint32_t epk = (uint32_t)min(e0, 0xffff) | ((uint32_t)min(e1, 0xffff) << 16);
-            const uint32_t g0 = lane_gather(epk, j0 & (W - 1)), g1 = lane_gather(epk, j1 & (W - 1));
-            const int ej0 = (int)(g0 & 0xffffu), ej1 = (int)(j1 >= W ? g1 >> 16 : g1 & 0xffffu);
-            const int x0 = lane, x1 = W + lane;
-            bool pr0 = j0 >= 0 ? (x0 == j0 || (x0 >= ej0 && x0 <= ej0 + 64)) : lane_on(P0a);
-            bool pr1 = j1 >= 0 ? (x1 == j1 || (x1 >= ej1 && x1 <= ej1 + 64)) : lane_on(P0b);
-            if (endip) { pr0 = pr0 && x0 < eL; pr1 = pr1 && x1 < eL; }
-            E0 = ballot(pr0);
-            E1 = ballot(pr1);
-            Ia0 = ballot(j0 >= 0 && x0 == ej0 - 2) | I0 | E0;
-            Ia1 = ballot(j1 >= 0 && x1 == ej1 - 2) | E1;
-        }
-        if (!((coll0 & E0) | (coll1 & E1))) break;
-        // each probed collider's real candidate: the latest earlier inserted position of its slot
-        const uint64_t k0m = g00 & below & Ia0, k1m = g11 & below & Ia1, k1z = g10 & Ia0;
-        const int kt0 = k0m ? msb64(k0m) : -1;
-        const int kt1 = k1m ? W + msb64(k1m) : (k1z ? msb64(k1z) : -1);
-        const bool fx0 = lane_on(E0) && kt0 != ak0, fx1 = lane_on(E1) && kt1 != ak1;
-        if (!(ballot(fx0) | ballot(fx1))) break;
-        const bool far0 = fx0 && kt0 >= 0 && kt0 != prev0, far1 = fx1 && kt1 >= 0 && kt1 != prev1;
-        if (fx0) {
-            ak0 = kt0;
-            oe0 = kt0 < 0 ? ok0 : okp0;
-            ce0 = kt0 < 0 ? old0 : (uint32_t)(base + kt0);
-            le0 = kt0 < 0 ? len0 : lep0;
-        }
-        if (fx1) {
-            ak1 = kt1;
-            oe1 = kt1 < 0 ? ok1 : okp1;
-            ce1 = kt1 < 0 ? old1 : (uint32_t)(base + kt1);
-            le1 = kt1 < 0 ? len1 : lep1;
-        }
-        if (ballot(far0) | ballot(far1)) {                    // an older position of the slot than prev
-            const PSide F0 = p_side_at(rg, R, in, base + (far0 ? kt0 : 0));
-            const PSide F1 = p_side_at(rg, R, in, base + (far1 ? kt1 : 0));
-            int l0, l1;
-            const bool o0 = eval_ring(s0, F0, v0, l0), o1 = eval_ring(s1, F1, v1, l1);
-            if (far0) { oe0 = o0; le0 = l0; }
-            if (far1) { oe1 = o1; le1 = l1; }
-        }
-    }
-    // ---- records: match start P | match length - 4 << 24 | offset << 48 (catch-up: the emission kernel)
-    const bool anym = (Mm0 | Mm1) != 0;
-    if (anym) {
-        const int n0 = __builtin_popcountll(Mm0);
-        if (lane_on(Mm0)) {
-            const int ri = nrec + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(Mm0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Mm0, 0u));
-            st_b64(recs, 8 * ri, (uint32_t)p0 | ((uint32_t)cn0 << 24), ((uint32_t)cn0 >> 8) | (((uint32_t)p0 - ce0) << 16));
-        }
-        if (lane_on(Mm1)) {
-            const int ri = nrec + n0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(Mm1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Mm1, 0u));
-            st_b64(recs, 8 * ri, (uint32_t)p1 | ((uint32_t)cn1 << 24), ((uint32_t)cn1 >> 8) | (((uint32_t)p1 - ce1) << 16));
-        }
-        nrec = unii(nrec + n0 + __builtin_popcountll(Mm1));
-    }
-    // the parse ends here: a match end past mflimit, or the search reaches the invalid positions
-    const bool endp = anym ? (endip || (eL < 2 * W && fv <= min(eL + 64, 2 * W - 1))) : hi0 >= fv;
-    if (endp) {
-        if (anym) anchor = base + eL;
-        return false;
-    }
-    {   // table: each slot ends with its last inserted position, else its old value (all members of a
-        // slot store the same value; a half-1 member's store comes last)
-        const uint64_t gi0 = g00 & Ia0, gi1 = g11 & Ia1, gz = g10 & Ia0;
-        const uint32_t val0 = gi0 ? (uint32_t)(base + msb64(gi0)) : old0;
-        const uint32_t val1 = gi1 ? (uint32_t)(base + W + msb64(gi1)) : (gz ? (uint32_t)(base + msb64(gz)) : old1);
-        if (vm0 == ~0ull) T.put(h0, val0); else if (v0) T.put(h0, val0);
-        if (vm1 == ~0ull) T.put(h1, val1); else if (v1) T.put(h1, val1);
-        wave_lds_fence();
-    }
-    if (anym) {
-        const int ip = base + eL;
-        anchor = ip;
-        if (fin == kExh128) {                                 // 65 step-1 probes done: stride batches
-            runb = false; s = ip + 1; k0 = W; retest = false;
-        } else if (eL < 2 * W) {                              // searched to the batch end
-            q = base + 2 * W; qlim = ip + 64; pins = -1;
-        } else {                                              // re-test in a later batch
-            q = ip; qlim = ip + 64; pins = eL - 2 >= 2 * W ? ip - 2 : -1;
-        }
-    } else if (fin == kExh128) {
-        runb = false; s = qlim - 64 + 1; k0 = W; retest = false;
-    } else {
-        q = base + 2 * W; pins = -1;
-    }
-    if (runb) base = pins >= 0 ? pins : q;
-    return true;
-}
-
 // One block of an LZ4 frame with linked blocks (kLinked; lzh_lz4f_linked_kernel): the parse of
 // LZ4_compress_fast_continue in prefix mode (lz4.c:1565-1628 -> LZ4_compress_generic with byU32,
 // withPrefix64k, noDictIssue, limitedOutput): positions are frame indices, the block is
@@ -928,11 +610,11 @@ struct LinkCtl {
 // e+1, e+2, then steps of acc for 64 probes: offsets {0, 1, 2, 2+acc, 2+2acc, ..} from e.  Run
 // batches cover the first 64 search probes of each segment (as with acc 1); later probes and the
 // chunk tail (where a probe's forwardIp could pass mflimit) go through stride batches.
-template <bool kSmall, bool kStats, bool kRec = false, bool kFast = false, bool kWide = false, bool kLinked = false>
+template <bool kSmall, bool kStats, bool kRec = false, bool kFast = false, bool kLinked = false>
 __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab,
                                LDSA uint32_t* ringw, LDSA uint8_t* outb, uint32_t* out_size,
                                unsigned long long* stats, rsrc_t recs, uint32_t* rec_hdr, LinkCtl* lk = nullptr) {
-    static_assert(!kLinked || (!kSmall && !kRec && !kWide), "linked frames: byU32, in-kernel emission");
+    static_assert(!kLinked || (!kSmall && !kRec), "linked frames: byU32, in-kernel emission");
     const int b0 = kLinked ? lk->b0 : 0;                  // the block's first position (frame index)
     const int lane = threadIdx.x;
     Table<kSmall> T{tab};
@@ -955,7 +637,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
 #pragma unroll
         for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
     }
-    constexpr bool kRingOn = !(kRec && LZH_PARSE_NORING);
+    constexpr bool kRingOn = true;
     Ring R{ringw, in.sh, 0, 0, kRingOn, kRec};   // (the parse kernel's ring carries a 32-byte mirror)
     if (kLinked) R.fill = max(((b0 + in.sh) & ~255) - 256, 0);   // (a block's ring starts just before it)
     OutRing O{outb, out.sh, 0};
@@ -1005,34 +687,14 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             PAT = 3ull | (PER << 2);
         }
 
-        for (int guard = 0; (LZH_UNI_GO ? unii((int)go) != 0 : go) && !(kLinked && aborted) && guard < 4 * n + 64; guard++) {
-#if LZH_LOOP_UNI
+        for (int guard = 0; go && !(kLinked && aborted) && guard < 4 * n + 64; guard++) {
+            // (the loop-carried parse state is wave-uniform: readfirstlane keeps it in SGPRs)
             runb = unii(runb) != 0; retest = unii(retest) != 0;
             base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
             op = unii(op); anchor = unii(anchor); rc_tot = unii(rc_tot); nrec = unii(nrec);
             R.fill = unii(R.fill); R.ready = unii(R.ready); O.flushed = unii(O.flushed);
             so = unii(so);
-#endif
-            if constexpr (kWide) {
-                if (runb) {
-                    go = run_batch128(in, R, T, recs, lane, mfl1, mlimit, endX, base, q, qlim, pins, s, k0, runb,
-                                      retest, anchor, nrec, rc_lit, rc_off, rc_mlx, rc_m);
-                    continue;
-                }
-            }
             LZ_STAT(0, 1);
-#if defined(LZH_PAD_SALU) || defined(LZH_PAD_VALU)
-            {   // (issue-resource experiments: extra dependent scalar / vector instructions per batch)
-                uint32_t pad_ = (uint32_t)guard;
-#ifdef LZH_PAD_SALU
-                asm volatile(".rept " LZH_STR(LZH_PAD_SALU) "\n s_add_u32 %0, %0, 1\n .endr" : "+s"(pad_));
-#endif
-#ifdef LZH_PAD_VALU
-                asm volatile(".rept " LZH_STR(LZH_PAD_VALU) "\n v_add_u32 %0, %0, 1\n .endr" : "+v"(pad_));
-#endif
-                asm volatile("" ::"v"(pad_));
-            }
-#endif
             if (kFast && runb && base + LZH_WAVE - 1 + acc > mfl1) {
                 // near the chunk end a probe's forwardIp may pass mflimit: stride batches take over
                 // (the pending ip-2 insert first, then the re-test or the next search probe)
@@ -1219,43 +881,16 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         bool endip = false;                            // a match ended past mflimit
                         // link: next member lane, or 0x80 for the rare cases (long match, parse end)
                         const int link = (lng || p + kMinMatch + cn >= mfe) ? 0x80 : f;
-#if LZH_PARSE_LIFT
-                        // chain membership lane-parallel (binary lifting over the links, as the decoder's
-                        // chain_members): jumps of 1, 2, 4, 8 links; a member takes >= 4 lanes, so <= 16
-                        // members per batch and 15 jumps reach all of them.  Codes >= 64 end the chain.
-                        // (the gathers run on every lane: a ds_bpermute does not see exec-masked lanes)
-                        const int J0 = min(link, LZH_WAVE);
-                        const int G1 = (int)lane_gather((uint32_t)J0, J0 & (LZH_WAVE - 1));
-                        const int J1 = J0 < LZH_WAVE ? G1 : LZH_WAVE;
-                        const int G2 = (int)lane_gather((uint32_t)J1, J1 & (LZH_WAVE - 1));
-                        const int J2 = J1 < LZH_WAVE ? G2 : LZH_WAVE;
-                        const int G3 = (int)lane_gather((uint32_t)J2, J2 & (LZH_WAVE - 1));
-                        const int J3 = J2 < LZH_WAVE ? G3 : LZH_WAVE;
-#endif
                         LZ_CLK(10);                            // (stats: per-lane links)
                         // (links strictly increase, so the walks end)
                         for (;;) {
                             int fs;
-#if LZH_PARSE_LIFT
-                            {   // every lane lifts from sl to the furthest chain lane <= itself
-                                int x = sl, y;
-                                y = (int)lane_gather((uint32_t)J3, x); x = y <= lane ? y : x;
-                                y = (int)lane_gather((uint32_t)J2, x); x = y <= lane ? y : x;
-                                y = (int)lane_gather((uint32_t)J1, x); x = y <= lane ? y : x;
-                                y = (int)lane_gather((uint32_t)J0, x); x = y <= lane ? y : x;
-                                const uint64_t on = ballot(x == lane && lane >= sl);
-                                Mm |= on;
-                                sl = 63 - __builtin_clzll(on);           // the last member
-                                fs = rdlanei(link, sl);
-                            }
-#else
                             for (;;) {                                 // common case: plain links
                                 Mm |= 1ull << sl;
                                 fs = rdlanei(link, sl);
                                 if (fs >= LZH_WAVE) break;
                                 sl = fs;
                             }
-#endif
                             if (fs != 0x80) break;                     // the chain leaves the batch
                             int es;
                             if (rdlane((uint32_t)lng, sl)) {           // match runs past the window
@@ -1502,10 +1137,7 @@ lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_read
                            uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t chunk0,
                            unsigned long long* stats) {
     // table 16 KiB | input ring 1 KiB | output ring 512 B  (17.5 KiB: 9 waves per CU)
-#ifndef LZH_LDS_PAD
-#define LZH_LDS_PAD 0
-#endif
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4 + LZH_LDS_PAD / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4];
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t off = chunk * chunk_size;
     if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
@@ -1558,7 +1190,7 @@ __device__ void lz4f_linked_frame(const Bytes& rin, uint64_t s, uint64_t bs, uin
         Bytes rout;
         rout.init(stage + i * stride, stride);
         lz4v3::LinkCtl L{b0, bn - 1, -1, b > 0, -1};
-        lz4v3::compress_chunk<false, false, false, kFast, false, true>(rin, bn, rout, acc, tab, ring, outb, bcs + i,
+        lz4v3::compress_chunk<false, false, false, kFast, true>(rin, bn, rout, acc, tab, ring, outb, bcs + i,
                                                                         nullptr, nr, nullptr, &L);
         if (L.abort >= 0) {   // replay up to the failing probe: the table the next block starts from
             if (b > 0) {
@@ -1575,7 +1207,7 @@ __device__ void lz4f_linked_frame(const Bytes& rin, uint64_t s, uint64_t bs, uin
             nul.r = nr;
             nul.sh = 0;
             lz4v3::LinkCtl Rp{b0, 0x7fffffff, L.abort, b > 0, -1};
-            lz4v3::compress_chunk<false, false, false, kFast, false, true>(rin, bn, nul, acc, tab, ring, outb, nullptr,
+            lz4v3::compress_chunk<false, false, false, kFast, true>(rin, bn, nul, acc, tab, ring, outb, nullptr,
                                                                             nullptr, nr, nullptr, &Rp);
         }
         wave_lds_fence();
@@ -1653,10 +1285,7 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                      uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint64_t frame_size, uint32_t bpf) {
-#ifndef LZH_PARSE_LDS_PAD
-#define LZH_PARSE_LDS_PAD 0   // (occupancy experiments: extra LDS bytes per wave)
-#endif
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + (LZH_PARSE_NORING ? 0 : lz4v3::kRing / 4 + 8) + LZH_PARSE_LDS_PAD / 4];   // table | ring + mirror
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + 8];   // table | ring + mirror
     const uint64_t chunk = blockIdx.x;
     uint64_t off;
     int n;
@@ -1671,7 +1300,7 @@ lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, 
     uint32_t* hdr = rec_hdr + 2 * chunk;
     if (n < 65547) {
         if (acc > 1) lz4v3::compress_chunk<true, false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
-        else lz4v3::compress_chunk<true, false, true, false, LZH_WIDE>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+        else lz4v3::compress_chunk<true, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
     } else {
         if (acc > 1) lz4v3::compress_chunk<false, false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
         else lz4v3::compress_chunk<false, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
