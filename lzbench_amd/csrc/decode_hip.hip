@@ -672,7 +672,6 @@ __device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, c
     uint64_t ooff, ioff;
     int part, cs;
     bool raw;
-    uint32_t nlink = 1;      // blocks this wave decodes (a linked frame's, in order)
     if (desc) {   // framed layouts: one 32-byte block descriptor each (frame_hip.hip FrameDesc)
         const uint32_t* d = desc + 8 * chunk;
         ioff = (uint64_t)uni(d[1]) << 32 | uni(d[0]);
@@ -681,8 +680,7 @@ __device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, c
         part = (int)uni(d[5]);
         const uint32_t fl = uni(d[6]);
         raw = (fl & 1u) != 0;
-        if (fl & 4u) return;                    // a linked frame's later block: its first block's wave decodes it
-        if (fl & 2u) nlink = uni(d[7]);
+        if (fl & 6u) return;                    // a linked frame's block: lzh_decompress_linked_kernel
         if (part == 0) { if (lane == 0) status[chunk] = 0; return; }   // unused slot
     } else {
         ooff = chunk * chunk_size;
@@ -696,41 +694,23 @@ __device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, c
     if (lane < 16) g_dst[lane] = 0;
     DCLK(tk0);
 #endif
-    const uint64_t foff = ooff;              // (linked: the frame's output start)
-    for (uint32_t bi = 0; bi < nlink; bi++) {
-        if (bi > 0) {   // next block of a linked frame: its matches may reach into the blocks before it
-            const uint32_t* d = desc + 8 * (chunk + bi);
-            ioff = (uint64_t)uni(d[1]) << 32 | uni(d[0]);
-            ooff = (uint64_t)uni(d[3]) << 32 | uni(d[2]);
-            cs = (int)uni(d[4]);
-            part = (int)uni(d[5]);
-            raw = (uni(d[6]) & 1u) != 0;
-            wait_vm();   // (the previous block's output stores are done before its bytes are read back)
-        }
-        const int prefix = (int)(ooff - foff);
-        const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
-        Bytes rin, rout;
-        rin.init(packed + ioff, readable);
-        rout.init(out + foff, (uint64_t)prefix + part);
-        rout.sh += prefix;                    // (block positions; earlier output at negative ones)
-        int r;
-        if (raw) {
-            copy_raw(rin, rout, part, lane);
-            r = part;
-        } else {
-            owin::SinkT<KW> O{win, rout, 0, 0};
-            LDSA uint8_t* mark = win + KW;
-            LDSA uint8_t* ring = mark + 3 * LZH_WAVE;
-            r = codec == 0 ? groups::lz4_decode(rin, cs, O, mark, ring, part, lane, prefix)
-                           : groups::snappy_decode(rin, cs, O, mark, ring, part, lane);
-            if (r > 0) O.flush(r, lane);
-        }
-        if (lane == 0) status[chunk + bi] = r;
-        if (r < 0) {   // the frame is bad: its remaining blocks are not decoded
-            for (uint32_t bj = bi + 1 + (uint32_t)lane; bj < nlink; bj += LZH_WAVE) status[chunk + bj] = -1;
-            break;
-        }
+    const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+    Bytes rin, rout;
+    rin.init(packed + ioff, readable);
+    rout.init(out + ooff, (uint64_t)part);
+    int r;
+    if (raw) {
+        copy_raw(rin, rout, part, lane);
+        r = part;
+    } else {
+        owin::SinkT<KW> O{win, rout, 0, 0};
+        LDSA uint8_t* mark = win + KW;
+        LDSA uint8_t* ring = mark + 3 * LZH_WAVE;
+        r = codec == 0 ? groups::lz4_decode(rin, cs, O, mark, ring, part, lane)
+                       : groups::snappy_decode(rin, cs, O, mark, ring, part, lane);
+        if (r > 0) O.flush(r, lane);
     }
+    if (lane == 0) status[chunk] = r;
 #if LZH_DEC_STATS
     DST(11, 1);
     DST(12, __builtin_amdgcn_s_memtime() - tk0);
@@ -752,6 +732,54 @@ LZH_DEC_KERNEL(lzh_decompress_v2_kernel, owin::kW)
 LZH_DEC_KERNEL(lzh_decompress_w8k_kernel, 8192)
 LZH_DEC_KERNEL(lzh_decompress_w16k_kernel, 16384)
 #undef LZH_DEC_KERNEL
+
+// LZ4 frames with linked blocks (frame_hip.hip marks their descriptors: flags 2 = a frame's first
+// block, pad = its block count; 4 = a later block): one wave per frame decodes the blocks in order,
+// each with the frame's output before it as its prefix (LZ4F_updateDict's prefix mode,
+// lz4frame.c:1290-1306; LZ4_decompress_safe_usingDict, lz4.c:2404-2416): a match may reach back
+// into earlier blocks (read from global memory, the window starts empty per block), and the offset
+// check fails only past the frame's start.  Waves of other descriptors exit at once.
+extern "C" __global__ void __launch_bounds__(64)
+lzh_decompress_linked_kernel(const uint8_t* packed, uint64_t packed_readable, uint8_t* out, int32_t* status,
+                             const uint32_t* desc) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[owin::kW + 3 * LZH_WAVE + kRingBytes];
+    const int lane = threadIdx.x;
+    const uint64_t chunk = blockIdx.x;
+    const uint32_t* d0 = desc + 8 * chunk;
+    if (!(uni(d0[6]) & 2u)) return;
+    const uint32_t nlink = uni(d0[7]);
+    const uint64_t foff = (uint64_t)uni(d0[3]) << 32 | uni(d0[2]);   // the frame's output start
+    for (uint32_t bi = 0; bi < nlink; bi++) {
+        const uint32_t* d = desc + 8 * (chunk + bi);
+        const uint64_t ioff = (uint64_t)uni(d[1]) << 32 | uni(d[0]);
+        const uint64_t ooff = (uint64_t)uni(d[3]) << 32 | uni(d[2]);
+        const int cs = (int)uni(d[4]), part = (int)uni(d[5]);
+        const bool raw = (uni(d[6]) & 1u) != 0;
+        wait_vm();   // (the previous block's output stores are done before its bytes are read back)
+        const int prefix = (int)(ooff - foff);
+        const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+        Bytes rin, rout;
+        rin.init(packed + ioff, readable);
+        rout.init(out + foff, (uint64_t)prefix + part);
+        rout.sh += prefix;                    // (block positions; earlier output at negative ones)
+        int r;
+        if (raw) {
+            copy_raw(rin, rout, part, lane);
+            r = part;
+        } else {
+            owin::Sink O{(LDSA uint8_t*)win, rout, 0, 0};
+            LDSA uint8_t* mark = (LDSA uint8_t*)win + owin::kW;
+            LDSA uint8_t* ring = mark + 3 * LZH_WAVE;
+            r = groups::lz4_decode(rin, cs, O, mark, ring, part, lane, prefix);
+            if (r > 0) O.flush(r, lane);
+        }
+        if (lane == 0) status[chunk + bi] = r;
+        if (r < 0) {   // the frame is bad: its remaining blocks are not decoded
+            for (uint32_t bj = bi + 1 + (uint32_t)lane; bj < nlink; bj += LZH_WAVE) status[chunk + bj] = -1;
+            break;
+        }
+    }
+}
 
 #if LZH_DEC_STATS
 extern "C" int lzh_debug_dec_stats(unsigned long long* host, int reset) {
@@ -1834,6 +1862,9 @@ hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t pack
     }
     hipLaunchKernelGGL(k, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable, offsets, csizes, n_total,
                        chunk_size, out, status, 0u, (const uint32_t*)desc);
+    if (desc && codec == 0)   // LZ4 frames: the linked ones (descriptors the kernel above skipped)
+        hipLaunchKernelGGL(lzh_decompress_linked_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, out,
+                           status, (const uint32_t*)desc);
     return hipGetLastError();
 }
 

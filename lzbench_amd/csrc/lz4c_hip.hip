@@ -959,7 +959,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 // the sequences' records are built under the next batch's loads (RUN_RECORDS)
                 pr_m = Mm; pr_base = base; pr_anchor = anchor; pr_e = e; pr_cn = cn; pr_be = be; pr_ce = ce;
                 LZ_CLK(6);                                             // records
-                // table: the last inserted lane of each slot, or the slot's old value
+                // (kLinked) the table restore at the end of a block (as in the else branch below)
                 auto restore = [&](uint64_t Iw) {
                     const bool inI = lane_on(Iw);
                     if (LZH_BRFREE && vmask == ~0ull) {
@@ -1002,7 +1002,21 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         q = base + hi0 + 1;
                         pins = -1;
                     }
-                    restore(I);
+                    // table: the last inserted lane of each slot, or the slot's old value
+                    const bool inI = lane_on(I);
+                    if (LZH_BRFREE && vmask == ~0ull) {
+                        // every lane stores its slot's final value (all lanes of a slot agree):
+                        // the slot's last inserted lane, else its old value
+                        const uint64_t gi = grp & I;
+                        T.put(h, gi ? (uint32_t)(base + 63 - __builtin_clzll(gi)) : old);
+                    } else if (!losers) {
+                        if (valid && !inI) T.put(h, old);
+                    } else {
+                        const uint64_t gi = grp & I;
+                        const bool wr = valid && (gi == 0 || (inI && (gi & ~((2ull << lane) - 1ull)) == 0));
+                        if (wr) T.put(h, inI ? (uint32_t)p : old);
+                    }
+                    wave_lds_fence();
                     if (!Mm && hi0 == qlim - base) {                   // 64 probes done: stride batches
                         runb = false;
                         s = so + 1;
@@ -1157,93 +1171,6 @@ lzh_lz4_compress_v2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_read
         if (acc > 1) lz4v3::compress_chunk<false, false, false, true>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
         else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, csizes + chunk, stats, nr, nullptr);
     }
-}
-
-// LZ4 frames with linked blocks (LZ4F_blockLinked, the LZ4F default; lz4frame.c:651-655, :777-782):
-// one wave per frame walks its blocks in order with one byU32 table, as LZ4_compress_fast_continue
-// does over a stable source (lz4.c:1565-1628, prefix mode).  Each block is compressed with the
-// limitedOutput budget size - 1 (LZ4F_makeBlock, lz4frame.c:740-763); a block that does not fit is
-// stored raw (bcs = its size) and its table is rebuilt as the reference leaves it at the failing
-// check: the table is saved to `snap` (16 KiB per frame) before every block and a failed block is
-// replayed from it up to the failing probe.  A frame of one block is independent (lz4frame.c:394-395)
-// and goes through the chunk codec.  Block i of frame f: staging slot f * bpf + b, size bcs[i].
-template <bool kFast>
-__device__ void lz4f_linked_frame(const Bytes& rin, uint64_t s, uint64_t bs, uint32_t bpf, uint64_t f, int acc,
-                                  uint8_t* stage, uint64_t stride, uint32_t* bcs, uint32_t* snap, LDSA uint32_t* tab,
-                                  LDSA uint32_t* ring, LDSA uint8_t* outb) {
-    const int lane = threadIdx.x;
-    const rsrc_t nr = make_rsrc(nullptr, 0);
-    const uint32_t nb = (uint32_t)((s + bs - 1) / bs);
-    const rsrc_t sn = make_rsrc(snap + f * 4096, 16384);
-    for (uint32_t b = 0; b < nb; b++) {
-        const int b0 = (int)(b * bs), bn = (int)min<uint64_t>(bs, s - b * bs);
-        const uint64_t i = f * bpf + b;
-        if (b > 0) {   // the table before this block (a failed block replays from it)
-            wave_lds_fence();
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const int d = 4 * (k * LZH_WAVE + lane);
-                const u32x4 v = {tab[d], tab[d + 1], tab[d + 2], tab[d + 3]};
-                __builtin_amdgcn_raw_buffer_store_b128(v, sn, 4 * d, 0, 0);
-            }
-        }
-        Bytes rout;
-        rout.init(stage + i * stride, stride);
-        lz4v3::LinkCtl L{b0, bn - 1, -1, b > 0, -1};
-        lz4v3::compress_chunk<false, false, false, kFast, true>(rin, bn, rout, acc, tab, ring, outb, bcs + i,
-                                                                        nullptr, nr, nullptr, &L);
-        if (L.abort >= 0) {   // replay up to the failing probe: the table the next block starts from
-            if (b > 0) {
-                wait_vm();
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const int d = 4 * (k * LZH_WAVE + lane);
-                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(sn, 4 * d, 0, 0);
-                    tab[d] = v[0]; tab[d + 1] = v[1]; tab[d + 2] = v[2]; tab[d + 3] = v[3];
-                }
-                wave_lds_fence();
-            }
-            Bytes nul;
-            nul.r = nr;
-            nul.sh = 0;
-            lz4v3::LinkCtl Rp{b0, 0x7fffffff, L.abort, b > 0, -1};
-            lz4v3::compress_chunk<false, false, false, kFast, true>(rin, bn, nul, acc, tab, ring, outb, nullptr,
-                                                                            nullptr, nr, nullptr, &Rp);
-        }
-        wave_lds_fence();
-    }
-}
-
-extern "C" __global__ void __launch_bounds__(64)
-lzh_lz4f_linked_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t fs, uint64_t bs, uint32_t bpf,
-                       int acc, uint8_t* stage, uint64_t stride, uint32_t* bcs, uint32_t* snap) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4];
-    const uint64_t f = blockIdx.x;
-    const uint64_t foff = f * fs;
-    if (foff >= n_total) return;
-    const uint64_t s = min(fs, n_total - foff);
-    Bytes rin;
-    rin.init(in + foff, min<uint64_t>(in_readable - foff, s + 64));
-    LDSA uint32_t* tab = (LDSA uint32_t*)lds;
-    LDSA uint32_t* ring = tab + 4096;
-    LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
-    if (s <= bs) {   // one block: independent (the chunk codec with its own table type)
-        const rsrc_t nr = make_rsrc(nullptr, 0);
-        Bytes rout;
-        rout.init(stage + f * bpf * stride, stride);
-        uint32_t* cs = bcs + f * bpf;
-        const int n = (int)s;
-        if (n < 65547) {
-            if (acc > 1) lz4v3::compress_chunk<true, false, false, true>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
-            else lz4v3::compress_chunk<true, false>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
-        } else {
-            if (acc > 1) lz4v3::compress_chunk<false, false, false, true>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
-            else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
-        }
-        return;
-    }
-    if (acc > 1) lz4f_linked_frame<true>(rin, s, bs, bpf, f, acc, stage, stride, bcs, snap, tab, ring, outb);
-    else lz4f_linked_frame<false>(rin, s, bs, bpf, f, acc, stage, stride, bcs, snap, tab, ring, outb);
 }
 
 // debug twin of the parse kernel with event counters and phase clocks (tools/lz4_stats.py)
@@ -1495,6 +1422,95 @@ lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, u
     if (lane == 0) csizes[chunk] = (uint32_t)op;
 }
 
+#ifndef LZH_NO_LINKED_KERNEL
+// LZ4 frames with linked blocks (LZ4F_blockLinked, the LZ4F default; lz4frame.c:651-655, :777-782):
+// one wave per frame walks its blocks in order with one byU32 table, as LZ4_compress_fast_continue
+// does over a stable source (lz4.c:1565-1628, prefix mode).  Each block is compressed with the
+// limitedOutput budget size - 1 (LZ4F_makeBlock, lz4frame.c:740-763); a block that does not fit is
+// stored raw (bcs = its size) and its table is rebuilt as the reference leaves it at the failing
+// check: the table is saved to `snap` (16 KiB per frame) before every block and a failed block is
+// replayed from it up to the failing probe.  A frame of one block is independent (lz4frame.c:394-395)
+// and goes through the chunk codec.  Block i of frame f: staging slot f * bpf + b, size bcs[i].
+template <bool kFast>
+__device__ void lz4f_linked_frame(const Bytes& rin, uint64_t s, uint64_t bs, uint32_t bpf, uint64_t f, int acc,
+                                  uint8_t* stage, uint64_t stride, uint32_t* bcs, uint32_t* snap, LDSA uint32_t* tab,
+                                  LDSA uint32_t* ring, LDSA uint8_t* outb) {
+    const int lane = threadIdx.x;
+    const rsrc_t nr = make_rsrc(nullptr, 0);
+    const uint32_t nb = (uint32_t)((s + bs - 1) / bs);
+    const rsrc_t sn = make_rsrc(snap + f * 4096, 16384);
+    for (uint32_t b = 0; b < nb; b++) {
+        const int b0 = (int)(b * bs), bn = (int)min<uint64_t>(bs, s - b * bs);
+        const uint64_t i = f * bpf + b;
+        if (b > 0) {   // the table before this block (a failed block replays from it)
+            wave_lds_fence();
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int d = 4 * (k * LZH_WAVE + lane);
+                const u32x4 v = {tab[d], tab[d + 1], tab[d + 2], tab[d + 3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, sn, 4 * d, 0, 0);
+            }
+        }
+        Bytes rout;
+        rout.init(stage + i * stride, stride);
+        lz4v3::LinkCtl L{b0, bn - 1, -1, b > 0, -1};
+        lz4v3::compress_chunk<false, false, false, kFast, true>(rin, bn, rout, acc, tab, ring, outb, bcs + i,
+                                                                        nullptr, nr, nullptr, &L);
+        if (L.abort >= 0) {   // replay up to the failing probe: the table the next block starts from
+            if (b > 0) {
+                wait_vm();
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int d = 4 * (k * LZH_WAVE + lane);
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(sn, 4 * d, 0, 0);
+                    tab[d] = v[0]; tab[d + 1] = v[1]; tab[d + 2] = v[2]; tab[d + 3] = v[3];
+                }
+                wave_lds_fence();
+            }
+            Bytes nul;
+            nul.r = nr;
+            nul.sh = 0;
+            lz4v3::LinkCtl Rp{b0, 0x7fffffff, L.abort, b > 0, -1};
+            lz4v3::compress_chunk<false, false, false, kFast, true>(rin, bn, nul, acc, tab, ring, outb, nullptr,
+                                                                            nullptr, nr, nullptr, &Rp);
+        }
+        wave_lds_fence();
+    }
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_lz4f_linked_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t fs, uint64_t bs, uint32_t bpf,
+                       int acc, uint8_t* stage, uint64_t stride, uint32_t* bcs, uint32_t* snap) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + lz4v3::kOut / 4];
+    const uint64_t f = blockIdx.x;
+    const uint64_t foff = f * fs;
+    if (foff >= n_total) return;
+    const uint64_t s = min(fs, n_total - foff);
+    Bytes rin;
+    rin.init(in + foff, min<uint64_t>(in_readable - foff, s + 64));
+    LDSA uint32_t* tab = (LDSA uint32_t*)lds;
+    LDSA uint32_t* ring = tab + 4096;
+    LDSA uint8_t* outb = (LDSA uint8_t*)(ring + lz4v3::kRing / 4);
+    if (s <= bs) {   // one block: independent (the chunk codec with its own table type)
+        const rsrc_t nr = make_rsrc(nullptr, 0);
+        Bytes rout;
+        rout.init(stage + f * bpf * stride, stride);
+        uint32_t* cs = bcs + f * bpf;
+        const int n = (int)s;
+        if (n < 65547) {
+            if (acc > 1) lz4v3::compress_chunk<true, false, false, true>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
+            else lz4v3::compress_chunk<true, false>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
+        } else {
+            if (acc > 1) lz4v3::compress_chunk<false, false, false, true>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
+            else lz4v3::compress_chunk<false, false>(rin, n, rout, acc, tab, ring, outb, cs, nullptr, nr, nullptr);
+        }
+        return;
+    }
+    if (acc > 1) lz4f_linked_frame<true>(rin, s, bs, bpf, f, acc, stage, stride, bcs, snap, tab, ring, outb);
+    else lz4f_linked_frame<false>(rin, s, bs, bpf, f, acc, stage, stride, bcs, snap, tab, ring, outb);
+}
+
+#endif
 #include "launch.h"
 size_t lzh_lz4_rec_stride(uint64_t chunk_size) { return ((chunk_size / 4 + 4) * 8 + 255) / 256 * 256; }
 
@@ -1529,9 +1545,13 @@ hipError_t lzh_launch_lz4f_linked(const uint8_t* in, uint64_t n_total, uint64_t 
                                   uint32_t bpf, int acc, uint8_t* stage, uint64_t stride, uint32_t* bcs, uint32_t* snap,
                                   uint32_t nframes, hipStream_t s) {
     if (nframes == 0) return hipSuccess;
+#ifdef LZH_NO_LINKED_KERNEL
+    return hipErrorNotSupported;
+#else
     hipLaunchKernelGGL(lzh_lz4f_linked_kernel, dim3(nframes), dim3(64), 0, s, in, n_total, in_readable, fs, bs, bpf, acc,
                        stage, stride, bcs, snap);
     return hipGetLastError();
+#endif
 }
 
 // debug: run the v2 kernel with event counters (16 x u64 device buffer)
