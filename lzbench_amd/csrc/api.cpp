@@ -171,6 +171,7 @@ size_t lzh_decompress_temp_bytes(int codec, size_t n, size_t chunk_size) {
         const size_t nd = k * frame_maxbpf(codec, chunk_size);
         t += align_up(nd * 32, 256) + align_up(nd * 4, 256) + align_up(k * 4, 256) + 256;
     }
+    if (codec == LZH_CODEC_ZSTD) t += lzh_zstd_decode_temp(n, chunk_size);   // the split decoder (decode_hip.hip)
     return t;
 }
 
@@ -314,7 +315,7 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
     if (n == 0) return LZH_OK;
     Range range("lzh:decompress");
     const uint64_t* offs = d_offsets;
-    if (!offs || is_frame(codec)) {
+    if (!offs || is_frame(codec) || codec == LZH_CODEC_ZSTD) {
         if (!d_temp || temp_bytes < lzh_decompress_temp_bytes(codec, n, chunk_size)) return LZH_ESPACE;
     }
     if (!offs) {
@@ -340,7 +341,8 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
     }
     if (codec == LZH_CODEC_ZSTD)
         LZH_CHECK(lzh_launch_zstd_decompress((const uint8_t*)d_packed, packed_readable, offs, d_csizes, n, chunk_size,
-                                             (uint8_t*)d_out, d_status, (uint32_t)k, s));
+                                             (uint8_t*)d_out, d_status, (uint32_t)k,
+                                             (uint8_t*)d_temp + align_up((k + 1) * sizeof(uint64_t), 256), s));
     else
         LZH_CHECK(lzh_launch_decompress(codec, (const uint8_t*)d_packed, packed_readable, offs, d_csizes, n,
                                         chunk_size, (uint8_t*)d_out, d_status, (uint32_t)k, s));

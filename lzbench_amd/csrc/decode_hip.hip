@@ -916,15 +916,17 @@ __device__ __forceinline__ uint32_t c_sym(Cell c) { return c >> 18; }
 
 // per-wave LDS
 struct Lds {
-    uint8_t win[kZW + 3 * LZH_WAVE];     // output window | start marks + scratch (groups::emit_group)
     uint16_t huf[1 << kHufLogMax];      // Huffman decoding table: symbol | nbBits << 8
     Cell ll[512], ml[512], of[256];     // sequence FSE tables (ZSTD_seqSymbol's fields, packed)
     Cell wt[64];                       // FSE table of the Huffman weights (accuracy <= 6)
     uint8_t weights[256];
     int16_t norm[256];
     uint16_t next[256];
+    // (the split decoder's header kernel allocates the fields above only)
     uint32_t base[36 + 53];             // literal-length / match-length baselines (kLLBase, kMLBase)
+    uint8_t win[kZW + 3 * LZH_WAVE];     // output window | start marks + scratch (groups::emit_group)
 };
+constexpr size_t kLdsHdr = offsetof(Lds, base);
 
 __device__ __forceinline__ uint32_t lds_u32(const LDSA uint32_t* p) { return uni(*(volatile const LDSA uint32_t*)p); }
 __device__ __forceinline__ uint32_t lds_u16(const LDSA uint16_t* p) { return uni(*(volatile const LDSA uint16_t*)p); }
@@ -1790,19 +1792,598 @@ __device__ __forceinline__ int decode_frame(const Bytes& rin, const Bytes& lout,
 
 }  // namespace zstdd
 
+// ---------------------------------------------------------------------------------------
+// zstd decoding in three kernels.  The sequence section's decoding chain (bit reader, three FSE
+// states, repcodes: ZSTD_decodeSequence, zstd_decompress_block.c:1169-1270) is serial within a
+// block but independent between frames, so it runs one frame per LANE; what surrounds it is
+// wave-parallel per frame:
+//  1. lzh_zstd_hdr_kernel (one wave per frame): frame header, block walk, literal sections (the
+//     Huffman streams decode into the frame's output tail), sequence-section headers; the FSE
+//     tables it builds go to global memory per block.  Everything that does not need the output
+//     position is checked here, in decode_frame's order.
+//  2. lzh_zstd_seq_kernel (kFPW frames per wave, one per lane, tables in LDS): the sequences, with
+//     every check of ZSTD_execSequence that depends on the output position; writes (ll, ml, offset)
+//     per sequence.
+//  3. lzh_zstd_exec_kernel (one wave per frame): executes them 64 at a time (groups::emit_group),
+//     raw / RLE blocks and the content checksum.
+// A frame that does not fit the layout (more blocks than bmax, more sequences than smax, a length
+// of 2^17 or more) is decoded by lzh_zstd_decompress_kernel (the one-wave-per-frame decoder above)
+// after the three.  Verdicts equal decode_frame's: every check is made, on the same quantities;
+// only the order between checks differs, and every one of them reports kErrCorrupt.
+//
+// Literals of every block whose literal section is not raw live at the frame's output tail,
+// block after block: [n - L, n) for L literals in all, so that the output of an accepted frame
+// never overtakes a literal not yet copied (it holds every literal, and matches only add bytes).
+namespace zsplit {
+using namespace zstdd;
+
+constexpr int kFPW = 8;              // frames per sequence-decoding wave (lanes 0 .. kFPW-1)
+constexpr int kCells = 1280;         // one block's sequence tables: LL 512 | OF 256 | ML 512 cells
+constexpr int kGo = 0, kLegacy = 1, kDone = 2;
+constexpr int kLenBits = 17;         // (ll, ml, offset) packed as 17 + 17 + 30 bits
+
+struct ZBlk {                        // a block of the frame (header kernel)
+    uint32_t type;                   // 0 raw, 1 RLE, 2 compressed
+    uint32_t ltype;                  // literals section type (compressed blocks)
+    uint32_t pos;                    // raw: data position in the frame; RLE: the byte; else sequence stream start
+    uint32_t size;                   // raw / RLE: block size; else sequence stream bytes
+    uint32_t rs;                     // literals
+    uint32_t lit;                    // literals' position: ltype 0 in the frame, else in the output
+    uint32_t nseq;
+    uint32_t logs;                   // accuracy logs LL | OF << 8 | ML << 16
+    uint32_t tll, tof, tml;          // the blocks (of this frame) whose table slots hold LL / OF / ML
+    uint32_t pad;
+};
+struct ZFrame { int32_t nblk, n, ccrc, pad; };   // blocks, content size, checksum position (-1: none)
+struct ZExe { uint32_t op0, seq0; };             // a block's output position and first sequence
+
+struct ZLayout {
+    uint64_t bmax, smax, stride;
+    __host__ __device__ uint64_t exe() const { return bmax * sizeof(ZBlk); }
+    __host__ __device__ uint64_t cells() const { return exe() + bmax * sizeof(ZExe); }
+    __host__ __device__ uint64_t seqs() const { return cells() + bmax * kCells * 4; }
+};
+__host__ __device__ inline ZLayout zlayout(uint64_t chunk) {
+    ZLayout L;
+    L.bmax = (chunk + kBlockMax - 1) / kBlockMax + 1;   // the compressor writes ceil(chunk / 128 KiB) blocks
+    L.smax = chunk / 4 + 64;                            // (its matches are >= 4 bytes)
+    L.stride = (L.seqs() + L.smax * 8 + 255) & ~255ull;
+    return L;
+}
+
+// one compressed block's literal section and sequence-section header (decode_block up to the
+// sequences); lacc = the next literal position at the output tail
+__device__ __forceinline__ int hdr_block(const Bytes& rin, const Bytes& rout, ZWin& fw, LDSA Lds& L, FrameState& F,
+                                         int bs, int be, int& lacc, ZBlk& B, uint32_t* cells, int b, int& tll, int& tof,
+                                         int& tml, int lane) {
+    const uint32_t b0 = fbyte(fw, bs, lane);
+    const int ltype = (int)(b0 & 3u), sf = (int)((b0 >> 2) & 3u);
+    int rs, seqpos;
+    if (ltype <= 1) {
+        int hsz;
+        if ((sf & 1) == 0) { hsz = 1; rs = (int)(b0 >> 3); }
+        else if (sf == 1) { hsz = 2; rs = (int)((b0 >> 4) + (fbyte(fw, bs + 1, lane) << 4)); }
+        else { hsz = 3; rs = (int)((b0 >> 4) + (fbyte(fw, bs + 1, lane) << 4) + (fbyte(fw, bs + 2, lane) << 12)); }
+        if (rs > kBlockMax) return ZC;
+        if (ltype == 0) {
+            if (bs + hsz + rs > be) return ZC;
+            B.lit = (uint32_t)(bs + hsz);
+            seqpos = bs + hsz + rs;
+        } else {
+            if (bs + hsz + 1 > be) return ZC;   // (rs > fcs - op: the sequence kernel)
+            const uint32_t v = fbyte(fw, bs + hsz, lane);
+            for (int i = lane; i < rs; i += LZH_WAVE) rout.st8(lacc + i, v);
+            B.lit = (uint32_t)lacc;
+            lacc += rs;
+            seqpos = bs + hsz + 1;
+        }
+    } else {
+        const int hsz = sf <= 1 ? 3 : (sf == 2 ? 4 : 5);
+        const int bits = sf <= 1 ? 10 : (sf == 2 ? 14 : 18);
+        if (bs + hsz > be) return ZC;
+        uint64_t h = 0;
+        for (int i = 0; i < hsz; i++) h |= (uint64_t)fbyte(fw, bs + i, lane) << (8 * i);
+        rs = (int)((h >> 4) & ((1u << bits) - 1));
+        const int cs = (int)((h >> (4 + bits)) & ((1u << bits) - 1));
+        if (rs > kBlockMax || bs + hsz + cs > be) return ZC;
+        int p = bs + hsz;
+        if (ltype == 2) {
+            int tl = 0;
+            const int u = read_huf(fw, rin, p, bs + hsz + cs, L, tl, lane);
+            if (u < 0) return u;
+            F.hufV = true;
+            F.hufTl = tl;
+            F.hufX2 = sf != 0 && huf_select_x2(rs, cs);
+            p += u;
+        } else if (!F.hufV) {
+            return ZC;
+        }
+        if (rs == 0 && sf != 0 && ltype == 2) return ZC;
+        int hr = huf_streams(rin, p, bs + hsz + cs - p, sf == 0 ? 1 : 4, rout, lacc, rs, F.hufTl, L, lane);
+        if (hr == 1)
+            hr = F.hufX2 ? huf_streams_x2(rin, p, bs + hsz + cs - p, sf == 0 ? 1 : 4, rout, lacc, rs, F.hufTl, L, lane) : ZC;
+        if (hr < 0) return hr;
+        B.lit = (uint32_t)lacc;
+        lacc += rs;
+        seqpos = bs + hsz + cs;
+    }
+    B.ltype = (uint32_t)ltype;
+    B.rs = (uint32_t)rs;
+    // sequences section header (ZSTD_decodeSeqHeaders)
+    if (seqpos >= be) return ZC;
+    int p = seqpos;
+    int nseq = (int)fbyte(fw, p++, lane);
+    if (nseq >= 128) {
+        if (nseq == 255) {
+            if (p + 2 > be) return ZC;
+            nseq = (int)(fbyte(fw, p, lane) + (fbyte(fw, p + 1, lane) << 8)) + 0x7F00;
+            p += 2;
+        } else {
+            if (p + 1 > be) return ZC;
+            nseq = ((nseq - 128) << 8) + (int)fbyte(fw, p++, lane);
+        }
+    }
+    B.nseq = (uint32_t)nseq;
+    if (nseq > 0) {
+        if (p >= be) return ZC;
+        const uint32_t modes = fbyte(fw, p++, lane);
+        if (modes & 3u) return ZC;
+        // a table built in this block goes to the block's slot; "repeat" keeps the previous slot
+        auto table = [&](int mode, int which, LDSA Cell* T, int& al, bool& valid, int& slot, int cell0) -> bool {
+            const int u = seq_table(fw, p, be, mode, which, T, al, valid, L, lane);
+            if (u < 0) return false;
+            p += u;
+            if (mode != 3) {
+                uint32_t* dst = cells + (size_t)b * kCells + cell0;
+                for (int c = lane; c < (1 << al); c += LZH_WAVE) dst[c] = T[c];
+                slot = b;
+            }
+            return true;
+        };
+        if (!table((int)(modes >> 6), 0, L.ll, F.llA, F.llV, tll, 0)) return ZC;
+        if (!table((int)((modes >> 4) & 3u), 1, L.of, F.ofA, F.ofV, tof, 512)) return ZC;
+        if (!table((int)((modes >> 2) & 3u), 2, L.ml, F.mlA, F.mlV, tml, 768)) return ZC;
+        B.logs = (uint32_t)F.llA | ((uint32_t)F.ofA << 8) | ((uint32_t)F.mlA << 16);
+        B.tll = (uint32_t)tll; B.tof = (uint32_t)tof; B.tml = (uint32_t)tml;
+        B.pos = (uint32_t)p;
+        B.size = (uint32_t)(be - p);
+    } else if (p != be) {
+        return ZC;
+    }
+    return 0;
+}
+
+// the frame's header and blocks (decode_frame without the sequences); returns kGo / kLegacy or an error
+__device__ __forceinline__ int hdr_frame(const Bytes& rin, const Bytes& rout, int cs, LDSA Lds& L, int cap, uint8_t* zb,
+                                         const ZLayout& Z, ZFrame& fr, int lane) {
+    ZWin fw;
+    fw.bind(rin, nullptr);
+    fw.load(0, lane);
+    if (cs < 9) return ZC;
+    const uint32_t magic = fword(fw, 0, lane);
+    if (magic != 0xFD2FB528u) return (magic & 0xFFFFFFF0u) == 0x184D2A50u ? kErrUnsupported : kErrCorrupt;
+    const uint32_t fhd = fbyte(fw, 4, lane);
+    const int fcsf = (int)(fhd >> 6), single = (int)((fhd >> 5) & 1u);
+    if (fhd & 8u) return ZC;
+    const int ccrc = (fhd & 4u) ? 4 : 0;
+    int p = 5;
+    if (!single) {
+        const uint32_t wd = fbyte(fw, p++, lane);
+        if ((wd >> 3) + 10 > 27) return kErrUnsupported;
+    }
+    const int dsz = (int)(fhd & 3u) == 3 ? 4 : (int)(fhd & 3u);
+    uint32_t dict = 0;
+    for (int i = 0; i < dsz; i++) dict |= fbyte(fw, p + i, lane) << (8 * i);
+    p += dsz;
+    if (dict) return kErrUnsupported;
+    const int fsz = fcsf == 0 ? (single ? 1 : 0) : (fcsf == 1 ? 2 : (fcsf == 2 ? 4 : 8));
+    if (fsz == 0) return kErrUnsupported;
+    uint64_t fcs = 0;
+    for (int i = 0; i < fsz; i++) fcs |= (uint64_t)fbyte(fw, p + i, lane) << (8 * i);
+    if (fsz == 2) fcs += 256;
+    p += fsz;
+    if (fcs > (uint64_t)cap) return ZC;
+    const int n = (int)fcs;
+    // walk the block headers and literal-section sizes first: the tail layout needs the total
+    int nb = 0, ltot = 0;
+    {
+        int q = p;
+        for (int guard = 0; guard <= cs; guard++) {
+            if (q + 3 > cs) return ZC;
+            const uint32_t bh = fbyte(fw, q, lane) | (fbyte(fw, q + 1, lane) << 8) | (fbyte(fw, q + 2, lane) << 16);
+            q += 3;
+            const int last = (int)(bh & 1u), type = (int)((bh >> 1) & 3u), bsz = (int)(bh >> 3);
+            if (bsz > kBlockMax) return ZC;
+            if (++nb > (int)Z.bmax) return kLegacy;
+            if (type == 0) {
+                if (q + bsz > cs) return ZC;
+                q += bsz;
+            } else if (type == 1) {
+                if (q + 1 > cs) return ZC;
+                q += 1;
+            } else if (type == 2) {
+                if (q + bsz > cs || bsz < 1) return ZC;
+                const uint32_t b0 = fbyte(fw, q, lane);
+                const int ltype = (int)(b0 & 3u), sf = (int)((b0 >> 2) & 3u);
+                int rs;
+                if (ltype <= 1) {
+                    const int hsz = (sf & 1) == 0 ? 1 : (sf == 1 ? 2 : 3);
+                    if (q + hsz > cs) return ZC;
+                    rs = (sf & 1) == 0 ? (int)(b0 >> 3)
+                                       : (sf == 1 ? (int)((b0 >> 4) + (fbyte(fw, q + 1, lane) << 4))
+                                                  : (int)((b0 >> 4) + (fbyte(fw, q + 1, lane) << 4) +
+                                                          (fbyte(fw, q + 2, lane) << 12)));
+                } else {
+                    const int hsz = sf <= 1 ? 3 : (sf == 2 ? 4 : 5);
+                    const int bits = sf <= 1 ? 10 : (sf == 2 ? 14 : 18);
+                    if (hsz > bsz) return ZC;
+                    uint64_t h = 0;
+                    for (int i = 0; i < hsz; i++) h |= (uint64_t)fbyte(fw, q + i, lane) << (8 * i);
+                    rs = (int)((h >> 4) & ((1u << bits) - 1));
+                }
+                if (rs > kBlockMax) return ZC;
+                if (ltype != 0) ltot += rs;
+                q += bsz;
+            } else {
+                return ZC;
+            }
+            if (last) break;
+        }
+    }
+    if (ltot > n) return ZC;   // an accepted frame's output holds every literal
+    ZBlk* blk = (ZBlk*)zb;
+    uint32_t* cells = (uint32_t*)(zb + Z.cells());
+    FrameState F{1, 4, 8, 0, 0, 0, false, false, false, false, false, 0, {0, 0, 0, 0, 0, 0, 0, 0}, 0};
+    int lacc = n - ltot, tll = 0, tof = 0, tml = 0;
+    for (int b = 0; b < nb; b++) {
+        const uint32_t bh = fbyte(fw, p, lane) | (fbyte(fw, p + 1, lane) << 8) | (fbyte(fw, p + 2, lane) << 16);
+        p += 3;
+        const int type = (int)((bh >> 1) & 3u), bsz = (int)(bh >> 3);
+        ZBlk B{};
+        B.type = (uint32_t)type;
+        if (type == 0) {
+            B.pos = (uint32_t)p;
+            B.size = (uint32_t)bsz;
+            p += bsz;
+        } else if (type == 1) {
+            B.pos = fbyte(fw, p, lane);
+            B.size = (uint32_t)bsz;
+            p += 1;
+        } else {
+            const int r = hdr_block(rin, rout, fw, L, F, p, p + bsz, lacc, B, cells, b, tll, tof, tml, lane);
+            if (r < 0) return r;
+            p += bsz;
+        }
+        if (lane == 0) blk[b] = B;
+    }
+    if (p + ccrc != cs) return ZC;
+    fr.nblk = nb;
+    fr.n = n;
+    fr.ccrc = ccrc ? p : -1;
+    return kGo;
+}
+
+// Per-lane backward bit reader over one frame's sequence stream (SeqBits with per-lane global
+// loads: every lane reads its own frame).  Positions are bits from A (the stream start rounded
+// down to a dword); loads below the packed buffer or past its end are clamped (those bits are
+// garbage that the overrun checks reject, as in BackBits).
+struct LaneBits {
+    const uint8_t* g;
+    int64_t A, lim;
+    int P, D8, lo, na, nxt;
+    uint64_t c;
+    uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+    __device__ __forceinline__ uint32_t ld(int D) const {
+        int64_t x = A + D;
+        x = x < 0 ? 0 : (x > lim ? lim : x);
+        return __builtin_nontemporal_load((const uint32_t*)(g + x));
+    }
+    __device__ __forceinline__ bool init(const uint8_t* packed, uint64_t readable, int64_t s0, int size) {
+        g = packed;
+        lim = ((int64_t)readable - 4) & ~3ll;
+        A = s0 & ~3ll;
+        const int x0 = (int)(s0 & 3);
+        if (size <= 0) return false;
+        const int X = x0 + size - 1;
+        const uint32_t last = (ld(X & ~3) >> (8 * (X & 3))) & 0xffu;
+        if (last == 0) return false;
+        lo = 8 * x0;
+        P = 8 * X + hb32(last);
+        D8 = ((P - 32) >> 5) << 5;
+        const int D = D8 >> 3;
+        c = ((uint64_t)ld(D + 4) << 32) | ld(D);
+        a0 = ld(D - 4); a1 = ld(D - 8); a2 = ld(D - 12); a3 = ld(D - 16);
+        b0 = ld(D - 20); b1 = ld(D - 24); b2 = ld(D - 28); b3 = ld(D - 32);
+        na = 4;
+        nxt = D - 36;
+        return true;
+    }
+    __device__ __forceinline__ int left() const { return P - lo; }
+    __device__ __forceinline__ uint32_t get(int n) {
+        if (P - n < D8) {
+            c = (c << 32) | a0;
+            a0 = a1; a1 = a2; a2 = a3;
+            D8 -= 32;
+            if (--na == 0) {
+                a0 = b0; a1 = b1; a2 = b2; a3 = b3;
+                b0 = ld(nxt); b1 = ld(nxt - 4); b2 = ld(nxt - 8); b3 = ld(nxt - 12);
+                nxt -= 16;
+                na = 4;
+            }
+        }
+        const uint32_t v = (uint32_t)((c >> (P - n - D8)) & ((1ull << n) - 1ull));
+        P -= n;
+        return v;
+    }
+};
+
+// one frame's sequences (this lane's): ZSTD_decompressSequences' decode + execSequence checks
+__device__ __forceinline__ int seq_frame(const uint8_t* packed, uint64_t readable, int64_t ioff, uint8_t* zb,
+                                         const ZLayout& Z, const ZFrame fr, LDSA uint32_t* T, const LDSA uint32_t* base) {
+    const ZBlk* blk = (const ZBlk*)zb;
+    ZExe* ex = (ZExe*)(zb + Z.exe());
+    const uint32_t* cells = (const uint32_t*)(zb + Z.cells());
+    uint64_t* seqs = (uint64_t*)(zb + Z.seqs());
+    const int n = fr.n;
+    int rep0 = 1, rep1 = 4, rep2 = 8, op = 0, si = 0;
+    int cll = -1, cof = -1, cml = -1, all = -1, aof = -1, aml = -1;   // tables now in LDS
+    for (int b = 0; b < fr.nblk; b++) {
+        const ZBlk B = blk[b];
+        if (B.type != 2) {
+            if ((int)B.size > n - op) return ZC;
+            ex[b] = ZExe{(uint32_t)op, (uint32_t)si};
+            op += (int)B.size;
+            continue;
+        }
+        const int rs = (int)B.rs;
+        if (B.ltype != 0 && rs > n - op) return ZC;
+        ex[b] = ZExe{(uint32_t)op, (uint32_t)si};
+        int lp = 0;
+        const int nseq = (int)B.nseq;
+        if (nseq > 0) {
+            const int lA = (int)(B.logs & 255u), oA = (int)((B.logs >> 8) & 255u), mA = (int)(B.logs >> 16);
+            if ((int)B.tll != cll || lA != all) {
+                const uint32_t* s = cells + (size_t)B.tll * kCells;
+                for (int c = 0; c < (1 << lA); c++) T[c] = s[c];
+                cll = (int)B.tll; all = lA;
+            }
+            if ((int)B.tof != cof || oA != aof) {
+                const uint32_t* s = cells + (size_t)B.tof * kCells + 512;
+                for (int c = 0; c < (1 << oA); c++) T[512 + c] = s[c];
+                cof = (int)B.tof; aof = oA;
+            }
+            if ((int)B.tml != cml || mA != aml) {
+                const uint32_t* s = cells + (size_t)B.tml * kCells + 768;
+                for (int c = 0; c < (1 << mA); c++) T[768 + c] = s[c];
+                cml = (int)B.tml; aml = mA;
+            }
+            LaneBits sb;
+            if (!sb.init(packed, readable, ioff + (int64_t)B.pos, (int)B.size)) return ZC;
+            uint32_t sLL = sb.get(lA), sOF = sb.get(oA), sML = sb.get(mA);
+            for (int i = 0; i < nseq; i++) {
+                const Cell eL = T[sLL], eO = T[512 + sOF], eM = T[768 + sML];
+                const int ofc = (int)c_sym(eO);
+                const int llc = (int)c_sym(eL), mlc = (int)c_sym(eM);
+                const int ll0 = llc == 0;
+                int off;
+                if (ofc > 1) {
+                    off = (int)((1u << ofc) - 3u + sb.get(ofc));
+                    rep2 = rep1; rep1 = rep0; rep0 = off;
+                } else if (ofc == 0) {
+                    off = ll0 ? rep1 : rep0;
+                    if (ll0) { rep1 = rep0; rep0 = off; }
+                } else {
+                    const int idx = 1 + ll0 + (int)sb.get(1);
+                    int t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
+                    t += t == 0;
+                    if (idx != 1) rep2 = rep1;
+                    rep1 = rep0;
+                    rep0 = off = t;
+                }
+                const int am = c_add(eM), al = c_add(eL);
+                const uint32_t xb = sb.get(am + al);
+                const int ml = (int)base[36 + mlc] + (int)(xb >> al);
+                const int ll = (int)base[llc] + (int)(xb & ((1u << al) - 1u));
+                if (i + 1 < nseq) {
+                    const int nl = c_nb(eL), nm = c_nb(eM), no = c_nb(eO);
+                    const uint32_t sbits = sb.get(nl + nm + no);
+                    sLL = c_next(eL) + (sbits >> (nm + no));
+                    sML = c_next(eM) + ((sbits >> no) & ((1u << nm) - 1u));
+                    sOF = c_next(eO) + (sbits & ((1u << no) - 1u));
+                    if (sb.left() < 0) return ZC;
+                } else {
+                    const int extra = c_nb(eL) + c_nb(eM) + c_nb(eO);
+                    if (sb.left() > extra || sb.left() < 0) return ZC;
+                }
+                const int lrem = rs - lp;
+                if (ll > lrem || off > op + ll || (int64_t)op + ll + ml > (int64_t)(n - (lrem - ll))) return ZC;
+                if (ll >= (1 << kLenBits) || ml >= (1 << kLenBits) || si >= (int)Z.smax) return kLegacy;
+                seqs[si++] = (uint64_t)ll | ((uint64_t)ml << kLenBits) | ((uint64_t)off << (2 * kLenBits));
+                lp += ll;
+                op += ll + ml;
+            }
+        }
+        const int rem = rs - lp;
+        if (rem > n - op) return ZC;
+        op += rem;
+    }
+    if (op != n) return ZC;
+    return kGo;
+}
+
+// one frame's output from its blocks and sequences (one wave)
+__device__ __forceinline__ int exec_frame(const Bytes& rin, const Bytes& rout, const Bytes& lout, ZSink& O, LDSA uint8_t* mark,
+                                          const uint8_t* zb, const ZLayout& Z, const ZFrame& fr, int lane) {
+    const ZBlk* blk = (const ZBlk*)zb;
+    const ZExe* ex = (const ZExe*)(zb + Z.exe());
+    const uint64_t* seqs = (const uint64_t*)(zb + Z.seqs());
+    ZWin fw, lw;
+    fw.bind(rin, nullptr);
+    int op = 0;
+    for (int b = 0; b < fr.nblk; b++) {
+        const uint32_t type = blk[b].type, pos = blk[b].pos, size = blk[b].size;
+        if (type == 0) {
+            fw.load((int)pos, lane);
+            O.literals(fw, rin, (int)pos, op, (int)size, lane);
+            op += (int)size;
+            continue;
+        }
+        if (type == 1) {
+            for (int base = 0; base < (int)size; base += LZH_WAVE) {
+                if (base + lane < (int)size) O.put(op + base + lane, pos);
+                O.maybe_flush(op + min(base + LZH_WAVE, (int)size), lane);
+            }
+            op += (int)size;
+            continue;
+        }
+        const Bytes& lsrc = blk[b].ltype == 0 ? rin : lout;
+        const int lpos = (int)blk[b].lit, rs = (int)blk[b].rs, nseq = (int)blk[b].nseq;
+        const uint64_t* S = seqs + ex[b].seq0;
+        lw.bind(lsrc, nullptr);
+        lw.load(lpos, lane);
+        int lp = 0;
+        for (int s0 = 0; s0 < nseq;) {
+            const int i = s0 + lane;
+            const bool v = i < nseq;
+            const uint64_t q = v ? S[i] : 0ull;
+            const int ll = (int)(q & ((1u << kLenBits) - 1u)), ml = (int)((q >> kLenBits) & ((1u << kLenBits) - 1u));
+            const int off = (int)(q >> (2 * kLenBits));
+            const bool big = ll > 255 || ml > 4095;
+            const int lin = groups::wave_incl_scan(ll);
+            const int k = ffs64(ballot(!v || big || lin > 384));
+            if (k > 0) {   // the first k sequences as a group
+                const int o = ll + ml;
+                const int oin = groups::wave_incl_scan(o);
+                const int gl = rdlanei(lin, k - 1), go = rdlanei(oin, k - 1);
+                const int ip = lpos + lp;
+                if (!lw.covers(ip, ip + gl + 16)) lw.load(ip, lane);
+                const uint64_t keep = k == LZH_WAVE ? ~0ull : ((1ull << k) - 1ull);
+                groups::emit_group(lw, O, mark, ip, op, go, keep, oin - o, (uint32_t)ll | ((uint32_t)ml << 16),
+                                   (uint32_t)(lin - ll), off, lane);
+                op += go;
+                lp += gl;
+                s0 += k;
+            } else {       // a long sequence on its own
+                const int bl = rdlanei(ll, 0), bm = rdlanei(ml, 0), bo = rdlanei(off, 0);
+                O.literals(lw, lsrc, lpos + lp, op, bl, lane);
+                O.match(op + bl, bo, bm, lane);
+                op += bl + bm;
+                lp += bl;
+                s0 += 1;
+            }
+        }
+        const int rem = rs - lp;
+        if (rem > 0) {
+            O.literals(lw, lsrc, lpos + lp, op, rem, lane);
+            op += rem;
+        }
+    }
+    O.flush(op, lane);
+    if (fr.ccrc >= 0) {   // ZSTD_decompressFrame's checksum check (zstd_decompress.c:1011-1020)
+        wait_vm();
+        fw.load(fr.ccrc, lane);
+        const uint32_t want = fword(fw, fr.ccrc, lane);
+        if ((uint32_t)xxh64_wave(O.out, op, lane) != want) return kErrChecksum;
+    }
+    return op;
+}
+
+}  // namespace zsplit
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_zstd_hdr_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, const uint32_t* csizes,
+                    uint64_t n_total, uint64_t chunk_size, uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst,
+                    zsplit::ZFrame* zfr) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_raw[(zstdd::kLdsHdr + 3) / 4];
+    LDSA zstdd::Lds& L = *(LDSA zstdd::Lds*)lds_raw;
+    const int lane = threadIdx.x;
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t ooff = chunk * chunk_size;
+    if (ooff >= n_total) return;
+    const int part = (int)min(chunk_size, n_total - ooff);
+    const uint64_t ioff = offsets[chunk];
+    const int cs = (int)csizes[chunk];
+    const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+    Bytes rin, rout;
+    rin.init(packed + ioff, readable);
+    rout.init(out + ooff, (uint64_t)part);
+    if (cs == part) {                                  // stored raw by the chunk loop (lzbench.cpp:284-288)
+        copy_raw(rin, rout, part, lane);
+        if (lane == 0) {
+            status[chunk] = part;
+            zst[chunk] = zsplit::kDone;
+        }
+        return;
+    }
+    const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
+    zsplit::ZFrame fr{0, 0, -1, 0};
+    const int r = zsplit::hdr_frame(rin, rout, cs, L, part, zt + chunk * Z.stride, Z, fr, lane);
+    if (lane == 0) {
+        if (r == zsplit::kGo) zfr[chunk] = fr;
+        zst[chunk] = r == zsplit::kGo ? zsplit::kGo : (r == zsplit::kLegacy ? zsplit::kLegacy : zsplit::kDone);
+        if (r < 0) status[chunk] = r;
+    }
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t chunk_size,
+                    uint32_t nchunks, int32_t* status, uint8_t* zt, int32_t* zst, const zsplit::ZFrame* zfr) {
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[zsplit::kFPW * zsplit::kCells];
+    __shared__ uint32_t base[36 + 53];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 36 + 53; i += LZH_WAVE) base[i] = i < 36 ? zstdd::kLLBase[i] : zstdd::kMLBase[i - 36];
+    __syncthreads();
+    const uint32_t f = blockIdx.x * zsplit::kFPW + (uint32_t)lane;
+    if (lane >= zsplit::kFPW || f >= nchunks || zst[f] != zsplit::kGo) return;
+    const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
+    const int r = zsplit::seq_frame(packed, packed_readable, (int64_t)offsets[f], zt + (uint64_t)f * Z.stride, Z, zfr[f],
+                                    (LDSA uint32_t*)tabs + lane * zsplit::kCells, (const LDSA uint32_t*)base);
+    if (r == zsplit::kLegacy) {
+        zst[f] = zsplit::kLegacy;
+    } else if (r != zsplit::kGo) {
+        status[f] = r;
+        zst[f] = zsplit::kDone;
+    }
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_zstd_exec_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, const uint32_t* csizes,
+                     uint64_t n_total, uint64_t chunk_size, uint8_t* out, int32_t* status, const uint8_t* zt,
+                     const int32_t* zst, const zsplit::ZFrame* zfr) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[zstdd::kZW + 3 * LZH_WAVE];
+    const int lane = threadIdx.x;
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t ooff = chunk * chunk_size;
+    if (ooff >= n_total || zst[chunk] != zsplit::kGo) return;
+    const int part = (int)min(chunk_size, n_total - ooff);
+    const uint64_t ioff = offsets[chunk];
+    const int cs = (int)csizes[chunk];
+    const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+    Bytes rin, rout, lout;
+    rin.init(packed + ioff, readable);
+    rout.init(out + ooff, (uint64_t)part);
+    lout.init(out + ooff, (uint64_t)part + 3);
+    const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
+    zstdd::ZSink O{(LDSA uint8_t*)win, rout, 0, 0};
+    const int r = zsplit::exec_frame(rin, rout, lout, O, (LDSA uint8_t*)win + zstdd::kZW, zt + chunk * Z.stride, Z,
+                                     zfr[chunk], lane);
+    if (lane == 0) status[chunk] = r;
+}
+
 #ifndef LZH_ZSTD_MINW
 #define LZH_ZSTD_MINW 1   // waves per SIMD the register allocation must allow (LDS allows 3)
 #endif
 extern "C" __global__ void __launch_bounds__(64, LZH_ZSTD_MINW)
 lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                            const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
-                           int32_t* status, uint32_t chunk0, unsigned long long* stats) {
+                           int32_t* status, uint32_t chunk0, unsigned long long* stats, const int32_t* zsel) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_raw[(sizeof(zstdd::Lds) + 3) / 4];
     LDSA zstdd::Lds& L = *(LDSA zstdd::Lds*)lds_raw;
     const int lane = threadIdx.x;
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     const uint64_t ooff = chunk * chunk_size;
     if (ooff >= n_total) return;
+    if (zsel && zsel[chunk] != zsplit::kLegacy) return;   // (decoded by the split kernels)
     const int part = (int)min(chunk_size, n_total - ooff);
     const uint64_t ioff = offsets[chunk];
     const int cs = (int)csizes[chunk];
@@ -1831,6 +2412,12 @@ lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, cons
 // Test hook: force the LZ4 / snappy decoder's output window (4096, 8192 or 16384; 0 = by chunk count)
 // so that the parity tests run every window kernel on the same streams.
 static int g_force_window = 0;
+// Test hook: 1 = decode zstd frames with the one-wave-per-frame kernel only (no split kernels)
+static int g_zstd_legacy = 0;
+extern "C" int lzh_debug_zstd_legacy(int on) {
+    g_zstd_legacy = on ? 1 : 0;
+    return 0;
+}
 extern "C" int lzh_debug_force_decode_window(int kw) {
     if (kw != 0 && kw != 4096 && kw != 8192 && kw != 16384) return -1;
     g_force_window = kw;
@@ -1870,8 +2457,21 @@ hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t pack
 
 hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                       const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
-                                      int32_t* status, uint32_t nchunks, hipStream_t s) {
+                                      int32_t* status, uint32_t nchunks, uint8_t* zt, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
+    const int32_t* zsel = nullptr;
+    if (zt && !g_zstd_legacy) {   // the split kernels; frames they leave go to the one-wave decoder below
+        const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
+        int32_t* zst = (int32_t*)(zt + (uint64_t)nchunks * Z.stride);
+        zsplit::ZFrame* zfr = (zsplit::ZFrame*)((uint8_t*)zst + (((uint64_t)nchunks * 4 + 255) & ~255ull));
+        hipLaunchKernelGGL(lzh_zstd_hdr_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
+                           n_total, chunk_size, out, status, zt, zst, zfr);
+        hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3((nchunks + zsplit::kFPW - 1) / zsplit::kFPW), dim3(64), 0, s, packed,
+                           packed_readable, offsets, chunk_size, nchunks, status, zt, zst, zfr);
+        hipLaunchKernelGGL(lzh_zstd_exec_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
+                           n_total, chunk_size, out, status, zt, zst, zfr);
+        zsel = zst;
+    }
     unsigned long long* stats = nullptr;
 #if LZH_ZSTD_STATS
     static unsigned long long* d_stats = nullptr;
@@ -1880,7 +2480,7 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
     stats = d_stats;
 #endif
     hipLaunchKernelGGL(lzh_zstd_decompress_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets,
-                       csizes, n_total, chunk_size, out, status, 0u, stats);
+                       csizes, n_total, chunk_size, out, status, 0u, stats, zsel);
 #if LZH_ZSTD_STATS
     unsigned long long h[zstdd::kZClk];
     (void)hipMemcpyAsync(h, d_stats, sizeof(h), hipMemcpyDeviceToHost, s);
@@ -1894,4 +2494,13 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
     fprintf(stderr, "\n");
 #endif
     return hipGetLastError();
+}
+
+// bytes of the split decoder's temp for n bytes in chunks of chunk_size (per frame: blocks, block
+// positions, sequence tables, sequences; then the frame states and frame fields)
+size_t lzh_zstd_decode_temp(uint64_t n, uint64_t chunk_size) {
+    if (!chunk_size) return 0;
+    const uint64_t k = (n + chunk_size - 1) / chunk_size;
+    const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
+    return k * Z.stride + ((k * 4 + 255) & ~255ull) + k * sizeof(zsplit::ZFrame) + 256;
 }

@@ -3,7 +3,12 @@ zstd 1.5.2 with lzbench's zstd-row parameters (compressors.cpp:1745-1773): the c
 frames, fresh frames over corpora x chunk sizes x levels (raw, RLE and compressed blocks,
 predefined / RLE / FSE / repeat tables, 1- and 4-stream Huffman literals, multi-block frames),
 edge sizes, and corrupted frames (no fault; the reference's accept / reject verdict, and its bytes).
-Parity is exact: the decoded bytes must equal the original input.  Run with -m gpu."""
+Parity is exact: the decoded bytes must equal the original input.  The decoder has two paths: the
+split kernels (header / sequences one frame per lane / execution) and the one-wave-per-frame kernel
+that takes the frames the split layout does not fit; `path` runs a test through each (the
+lzh_debug_zstd_legacy hook forces the second).  Run with -m gpu."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -23,14 +28,29 @@ def torch_cuda():
     return torch
 
 
-def gpu_decode(torch, packed, cs, n, chunk):
+PATHS = ["split", "legacy"]
+
+
+def _legacy(on):
+    f = L.lib().lzh_debug_zstd_legacy
+    f.restype = C.c_int
+    f.argtypes = [C.c_int]
+    assert f(1 if on else 0) == 0
+
+
+def gpu_decode(torch, packed, cs, n, chunk, path="split"):
     dc = L.DeviceCodec("zstd", n, chunk)
     d_packed = torch.zeros(len(packed) + 256, dtype=torch.uint8, device="cuda")
     if len(packed):
         d_packed[:len(packed)].copy_(torch.from_numpy(np.array(packed, dtype=np.uint8)))
     d_cs = torch.from_numpy(np.asarray(cs).astype(np.int32)).cuda()
-    dc.decompress(packed=d_packed, csizes=d_cs)
-    torch.cuda.synchronize()
+    dc.out.fill_(0xA5)
+    try:
+        _legacy(path == "legacy")
+        dc.decompress(packed=d_packed, csizes=d_cs)
+        torch.cuda.synchronize()
+    finally:
+        _legacy(False)
     return dc.status[:dc.k].cpu().numpy(), dc.out[:n].cpu().numpy()
 
 
@@ -39,11 +59,13 @@ def expected_sizes(n, chunk):
     return np.array([min(chunk, n - i * chunk) for i in range(k)])
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("case", cases(), ids=lambda c: c["name"])
-def test_golden_frames(torch_cuda, case):
+def test_golden_frames(torch_cuda, case, path):
     A = arrays()
     data = corpus(case)
-    st, out = gpu_decode(torch_cuda, A[case["name"] + "/packed"], A[case["name"] + "/csizes"], len(data), case["chunk"])
+    st, out = gpu_decode(torch_cuda, A[case["name"] + "/packed"], A[case["name"] + "/csizes"], len(data), case["chunk"],
+                         path)
     assert (st == expected_sizes(len(data), case["chunk"])).all(), st
     assert (out == data).all()
 
@@ -63,13 +85,14 @@ def test_reference_frames(torch_cuda, kind, chunk, level):
     assert (out == data).all()
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("n", [1, 5, 13, 255, 4096 + 3, 131072 - 1, 131072 + 1, 3 * 131072 + 77])
-def test_edge_sizes(torch_cuda, n):
+def test_edge_sizes(torch_cuda, n, path):
     if not O.have_ref():
         pytest.skip("reference build (oracle/_ref) not present")
     data = L.datagen("text", n, 7)
     packed, cs = O.compress_chunks(data, "zstd", 131072, 1)
-    st, out = gpu_decode(torch_cuda, packed, cs, n, 131072)
+    st, out = gpu_decode(torch_cuda, packed, cs, n, 131072, path)
     assert (st == expected_sizes(n, 131072)).all() and (out == data).all()
 
 
@@ -89,12 +112,12 @@ def _corrupt(rng, s: bytes) -> bytes:
     return bytes(b)
 
 
-def _verdicts(torch, streams, chunk):
+def _verdicts(torch, streams, chunk, path="split"):
     """GPU decode of every stream; the (index, gpu, reference) triples whose accept / reject verdicts
     differ (lzbench's length check: a frame is accepted when it decodes to exactly `chunk` bytes), and
     asserts the bytes of every frame both accept are the reference's."""
     blob = np.frombuffer(b"".join(streams), np.uint8)
-    st, out = gpu_decode(torch, blob, [len(s) for s in streams], len(streams) * chunk, chunk)
+    st, out = gpu_decode(torch, blob, [len(s) for s in streams], len(streams) * chunk, chunk, path)
     R = O.ref()
     mism = []
     for i, s in enumerate(streams):
@@ -115,8 +138,9 @@ def _plain_frames(kind, chunk, seed):
     return [packed[offs[i]:offs[i + 1]].tobytes() for i in range(len(cs)) if cs[i] != chunk]
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("corpus_kind", ["text", "json", "mixed"])
-def test_corrupt_frames(torch_cuda, corpus_kind):
+def test_corrupt_frames(torch_cuda, corpus_kind, path):
     """1024 randomly corrupted plain (unchecksummed) frames per corpus: the decoder never faults and
     its accept / reject verdict equals ZSTD_decompressDCtx's frame for frame (including the literal
     sections the reference decodes with the double-symbol Huffman decoder: HUF_selectDecoder,
@@ -131,7 +155,7 @@ def test_corrupt_frames(torch_cuda, corpus_kind):
         s = _corrupt(rng, valid[int(rng.integers(0, len(valid)))])
         if 0 < len(s) != chunk:
             streams.append(s)
-    mism, accepted = _verdicts(torch_cuda, streams, chunk)
+    mism, accepted = _verdicts(torch_cuda, streams, chunk, path)
     assert not mism, mism[:10]
     assert accepted > 0
 
@@ -176,8 +200,9 @@ def _huf_stream_spans(frame: bytes):
     return [(a, b) for a, b in spans if 0 <= a < b <= len(frame)]
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("corpus_kind,chunk", [("text", 32768), ("json", 65536), ("mixed", 131072)])
-def test_corrupt_huffman_streams(torch_cuda, corpus_kind, chunk):
+def test_corrupt_huffman_streams(torch_cuda, corpus_kind, chunk, path):
     """1024 frames per case corrupted inside the Huffman literal streams -- their first and last bytes
     (where the double-symbol decoder's last-symbol step and the 4-stream loop's bounds decide), the
     jump table, anywhere in a stream: verdict and bytes equal ZSTD_decompressDCtx's."""
@@ -202,7 +227,7 @@ def test_corrupt_huffman_streams(torch_cuda, corpus_kind, chunk):
         s = bytes(buf)
         if s != f:
             streams.append(s)
-    mism, accepted = _verdicts(torch_cuda, streams, chunk)
+    mism, accepted = _verdicts(torch_cuda, streams, chunk, path)
     assert not mism, mism[:10]
     assert accepted > 0
 
@@ -219,9 +244,10 @@ def _ref_checksum_frames(data, chunk, level):
     return frames
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("kind,chunk,level", [("text", 131072, 1), ("json", 65536, 1), ("mixed", 1 << 20, 1),
                                               ("random", 131072, 1), ("binary", 100000, -3)])
-def test_checksummed_frames(torch_cuda, kind, chunk, level):
+def test_checksummed_frames(torch_cuda, kind, chunk, level, path):
     """Frames with the XXH64 content checksum (fParams.checksumFlag): decoded and verified."""
     if not O.have_ref():
         pytest.skip("reference build (oracle/_ref) not present")
@@ -232,13 +258,14 @@ def test_checksummed_frames(torch_cuda, kind, chunk, level):
     frames = [f if len(f) != min(chunk, n - i * chunk) else None for i, f in enumerate(frames)]
     if any(f is None for f in frames):
         pytest.skip("a frame came out exactly chunk-sized (would read as stored raw)")
-    st, out = gpu_decode(torch, np.frombuffer(b"".join(frames), np.uint8), [len(f) for f in frames], n, chunk)
+    st, out = gpu_decode(torch, np.frombuffer(b"".join(frames), np.uint8), [len(f) for f in frames], n, chunk, path)
     assert (st == expected_sizes(n, chunk)).all() and (out == data).all()
     # a wrong checksum is rejected, as by the reference
     bad = [bytearray(f) for f in frames]
     for b in bad:
         b[-1 - (len(b) % 4)] ^= 0x10
-    st2, _ = gpu_decode(torch, np.frombuffer(b"".join(bytes(b) for b in bad), np.uint8), [len(b) for b in bad], n, chunk)
+    st2, _ = gpu_decode(torch, np.frombuffer(b"".join(bytes(b) for b in bad), np.uint8), [len(b) for b in bad], n, chunk,
+                        path)
     R = O.ref()
     for i, b in enumerate(bad):
         src = np.frombuffer(bytes(b), np.uint8).copy()
@@ -247,8 +274,9 @@ def test_checksummed_frames(torch_cuda, kind, chunk, level):
         assert (st2[i] >= 0) == (r >= 0), (i, st2[i], r)
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("corpus_kind", ["text", "json"])
-def test_corrupt_checksummed_frames_verdicts(torch_cuda, corpus_kind):
+def test_corrupt_checksummed_frames_verdicts(torch_cuda, corpus_kind, path):
     """Corrupted checksummed frames: with the content checksum on, the GPU decoder's verdict equals
     the reference's (ZSTD_decompressDCtx) frame for frame, and accepted frames decode identically."""
     if not O.have_ref():
@@ -264,7 +292,7 @@ def test_corrupt_checksummed_frames_verdicts(torch_cuda, corpus_kind):
         if 0 < len(s) != chunk:
             streams.append(s)
     blob = np.frombuffer(b"".join(streams), np.uint8)
-    st, out = gpu_decode(torch, blob, [len(s) for s in streams], len(streams) * chunk, chunk)
+    st, out = gpu_decode(torch, blob, [len(s) for s in streams], len(streams) * chunk, chunk, path)
     R = O.ref()
     mism = []
     for i, s in enumerate(streams):
@@ -277,3 +305,52 @@ def test_corrupt_checksummed_frames_verdicts(torch_cuda, corpus_kind):
         elif r >= 0:
             assert (out[i * chunk:(i + 1) * chunk] == dst[:chunk]).all(), f"stream {i}: bytes differ"
     assert not mism, mism[:10]
+
+
+@pytest.mark.parametrize("corpus_kind,chunk", [("text", 32768), ("mixed", 131072)])
+def test_split_and_legacy_statuses_equal(torch_cuda, corpus_kind, chunk):
+    """The two paths return the same status (size or error code) and bytes for every frame of a
+    corrupted set, frame for frame."""
+    if not O.have_ref():
+        pytest.skip("reference build (oracle/_ref) not present")
+    rng = np.random.default_rng(303 + chunk)
+    valid = _plain_frames(corpus_kind, chunk, 77)
+    streams = []
+    while len(streams) < 512:
+        s = _corrupt(rng, valid[int(rng.integers(0, len(valid)))])
+        if 0 < len(s) != chunk:
+            streams.append(s)
+    blob = np.frombuffer(b"".join(streams), np.uint8)
+    cs = [len(s) for s in streams]
+    st1, out1 = gpu_decode(torch_cuda, blob, cs, len(streams) * chunk, chunk, "split")
+    st2, out2 = gpu_decode(torch_cuda, blob, cs, len(streams) * chunk, chunk, "legacy")
+    assert (st1 == st2).all(), np.nonzero(st1 != st2)[0][:10]
+    for i in np.nonzero(st1 == chunk)[0]:
+        assert (out1[i * chunk:(i + 1) * chunk] == out2[i * chunk:(i + 1) * chunk]).all(), i
+
+
+def _raw_block_frame(data: bytes, block: int) -> bytes:
+    """A single-segment frame of raw blocks of `block` bytes (RFC 8878 3.1.1.2): more blocks than the
+    split layout holds for its chunk size, so the frame goes to the one-wave decoder."""
+    n = len(data)
+    hdr = bytearray(b"\x28\xb5\x2f\xfd")
+    hdr.append(0x20 | (2 << 6))          # single segment, 4-byte content size
+    hdr += n.to_bytes(4, "little")
+    out = bytearray(hdr)
+    for i in range(0, n, block):
+        part = data[i:i + block]
+        last = 1 if i + block >= n else 0
+        bh = last | (0 << 1) | (len(part) << 3)
+        out += bh.to_bytes(3, "little") + part
+    return bytes(out)
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_many_block_frames_take_the_one_wave_decoder(torch_cuda, path):
+    chunk = 131072
+    data = L.datagen("text", 4 * chunk, 5)
+    frames = [_raw_block_frame(data[i:i + chunk].tobytes(), 1000) for i in range(0, len(data), chunk)]
+    st, out = gpu_decode(torch_cuda, np.frombuffer(b"".join(frames), np.uint8), [len(f) for f in frames], len(data), chunk,
+                         path)
+    assert (st == chunk).all(), st
+    assert (out == data).all()

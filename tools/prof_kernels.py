@@ -11,6 +11,7 @@ ap.add_argument("--corpus", default="text")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--decompress", action="store_true")
 ap.add_argument("--level", type=int, default=0)
+ap.add_argument("--zstd-legacy", action="store_true", help="zstd: the one-wave-per-frame decoder only")
 a = ap.parse_args()
 import torch
 import lzbench_amd as L
@@ -21,6 +22,8 @@ d_in[:n].copy_(torch.from_numpy(host))
 dc = L.DeviceCodec(a.codec, n, a.chunk_kib << 10, level=a.level)
 dc.compress(d_in)
 torch.cuda.synchronize()
+if a.zstd_legacy:
+    L.lib().lzh_debug_zstd_legacy(1)
 t = time.time()
 for _ in range(a.reps):
     if a.decompress:
