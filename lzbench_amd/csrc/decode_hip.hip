@@ -1164,6 +1164,79 @@ __device__ __forceinline__ void build_fse(LDSA Cell* T, int al, int nsym, LDSA L
     }
 }
 
+// FSE_buildDTable for the sequence tables (nsym <= 53, size <= 512), lane-parallel, the same cells as
+// build_fse: (1) per symbol (lanes): the low-probability symbols' top cells and the running sum C of
+// the other counts; (2) per spread step i (lanes, 64 at a time): position (i * step) & mask, kept when
+// <= high, its rank among the kept ones gives the symbol (the last s with C[s] <= rank: a binary
+// search); (3) per position u ascending (lanes, 64 at a time): the symbol's next-state counter value
+// at u -- its initial count plus the same-symbol cells before u -- with the counters in one VGPR
+// (lane s holds symbol s's) and the cells of a 64-position batch taken one distinct symbol at a time.
+__device__ __forceinline__ void build_fse_par(LDSA Cell* T, int al, int nsym, LDSA Lds& L, int lane) {
+    const int size = 1 << al, mask = size - 1;
+    const int step = (size >> 1) + (size >> 3) + 3;
+    const uint64_t below = (1ull << lane) - 1ull;
+    // (1) symbols: lane s (nsym <= 64)
+    const int n = lane < nsym ? (int)L.norm[lane] : 0;
+    const bool lowp = n == -1;
+    const uint64_t lm = ballot(lowp);
+    const int nlow = __builtin_popcountll(lm);
+    const int high = size - 1 - nlow;
+    if (lowp) T[size - 1 - __builtin_popcountll(lm & below)] = (uint32_t)lane << 18;
+    int C = n > 0 ? n : 0;                            // exclusive prefix sum of the positive counts
+    {
+        int x = C;
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) {
+            const int y = __shfl_up(x, k);
+            if (lane >= k) x += y;
+        }
+        C = x - C;
+    }
+    L.next[lane < 256 ? lane : 0] = lane < nsym ? (uint16_t)C : (uint16_t)0xffffu;
+    wave_lds_fence();
+    // (2) the spread
+    int kept = 0;
+    for (int c = 0; c < size; c += LZH_WAVE) {
+        const int i = c + lane;
+        const int pos = (int)(((uint32_t)i * (uint32_t)step) & (uint32_t)mask);
+        const bool valid = i < size && pos <= high;
+        const uint64_t vm = ballot(valid);
+        const int rank = kept + __builtin_popcountll(vm & below);
+        kept += __builtin_popcountll(vm);
+        // the last symbol s < nsym with C[s] <= rank
+        int lo = 0, hi = nsym - 1;
+        while (ballot(valid && lo < hi)) {
+            const int mid = (lo + hi + 1) >> 1;
+            const bool le = (int)L.next[mid] <= rank;
+            if (valid && lo < hi) { lo = le ? mid : lo; hi = le ? hi : mid - 1; }
+        }
+        if (valid) T[pos] = (uint32_t)lo << 18;
+    }
+    wave_lds_fence();
+    // (3) next states, positions ascending
+    int cnt = lowp ? 1 : n;                           // lane s: symbol s's counter
+    for (int c = 0; c < size; c += LZH_WAVE) {
+        const int u = c + lane;
+        const bool on = u < size;
+        const uint32_t sym = on ? (T[u] >> 18) : 0xffu;
+        int nx = 0;
+        for (uint64_t rem = ballot(on); rem;) {
+            const int s0 = (int)rdlane(sym, __builtin_ctzll(rem));
+            const uint64_t m = ballot(on && sym == (uint32_t)s0) & rem;
+            const int base = rdlanei(cnt, s0);
+            if (lane_on(m)) nx = base + __builtin_popcountll(m & below);
+            if (lane == s0) cnt += __builtin_popcountll(m);
+            rem &= ~m;
+        }
+        if (on) {
+            const int nb = al - hb32((uint32_t)nx);
+            const uint32_t base = ((uint32_t)nx << nb) - (uint32_t)size;
+            T[u] = (sym << 18) | ((uint32_t)nb << 9) | base;
+        }
+    }
+    wave_lds_fence();
+}
+
 // sequence-table cells: symbol -> baseline value and extra-bit count (RFC 8878 3.1.1.3.2.1.1)
 __device__ __forceinline__ void seq_cells(LDSA Cell* T, int size, int which, int lane) {
     for (int u = lane; u < size; u += LZH_WAVE) {
@@ -1186,7 +1259,7 @@ __device__ __forceinline__ int seq_table(ZWin& fw, int pos, int end, int mode, i
             L.norm[s] = which == 0 ? kLLNorm[s] : (which == 1 ? kOFNorm[s] : kMLNorm[s]);
         wave_lds_fence();
         al = which == 1 ? 5 : 6;
-        build_fse(T, al, n, L, lane);
+        build_fse_par(T, al, n, L, lane);
         seq_cells(T, 1 << al, which, lane);
         valid = true;
         return 0;
@@ -1207,7 +1280,7 @@ __device__ __forceinline__ int seq_table(ZWin& fw, int pos, int end, int mode, i
         const int h = read_ncount(fw, pos, end, maxSym, maxLog, L, al, nsym, lane);
         if (h <= 0) return h < 0 ? h : ZC;
         if (pos + h > end) return ZC;
-        build_fse(T, al, nsym, L, lane);
+        build_fse_par(T, al, nsym, L, lane);
         seq_cells(T, 1 << al, which, lane);
         valid = true;
         return h;
@@ -1641,7 +1714,9 @@ __device__ __forceinline__ int decode_block(const Bytes& rin, const Bytes& lout,
             // validity (ZSTD_execSequence): literals available, offset within the output, room
             const int lrem = lrem0 - lpv - glit;      // literals not yet taken
             const int o0 = opv + opg + gout;          // output position of this sequence
-            if (ll > lrem || off > o0 + ll || (int64_t)o0 + ll + ml > (int64_t)(fcsv - (lrem - ll))) return ZC;
+            // (an offset code of 31 gives 2^31 - 3 + bits: compared unsigned, as the reference's size_t)
+            if (ll > lrem || (uint32_t)off > (uint32_t)(o0 + ll) || (int64_t)o0 + ll + ml > (int64_t)(fcsv - (lrem - ll)))
+                return ZC;
             const bool big = ll > 255 || ml > 4095;
             if (big || k == LZH_WAVE || glit + ll > 384) {
                 // emit the pending group
@@ -1818,7 +1893,12 @@ namespace zsplit {
 using namespace zstdd;
 
 constexpr int kFPW = 8;              // frames per sequence-decoding wave (lanes 0 .. kFPW-1)
-constexpr int kCells = 1280;         // one block's sequence tables: LL 512 | OF 256 | ML 512 cells
+// A block's sequence tables in global memory (kSlot bytes): LL u32[512] | ML u32[512] | OF u16[256].
+// LL / ML cell: next-state base (9) | nbBits << 9 (4) | extra bits << 13 (5) | pow << 18 | lo << 19
+// (7): the baseline is lo, or 2^extra + lo for the codes whose baseline is >= 128 (LL 2^n, ML
+// 2^n + 3): no baseline table on the chain.  OF cell (16 bits): e | code << 9 with e = 2 * base +
+// 2^nbBits (a next-state base is a multiple of 2^nbBits: nbBits = ctz(e)).
+constexpr int kSlot = 4608;
 constexpr int kGo = 0, kLegacy = 1, kDone = 2;
 constexpr int kLenBits = 17;         // (ll, ml, offset) packed as 17 + 17 + 30 bits
 
@@ -1836,12 +1916,21 @@ struct ZBlk {                        // a block of the frame (header kernel)
 };
 struct ZFrame { int32_t nblk, n, ccrc, pad; };   // blocks, content size, checksum position (-1: none)
 struct ZExe { uint32_t op0, seq0; };             // a block's output position and first sequence
+// a Huffman-coded literal section (header kernel -> literal kernel): its frame, the block whose
+// table slot holds its table, the table log, whether the reference would decode it with the
+// double-symbol decoder, streams, output position, symbols per stream (the 4th: last), streams
+constexpr int kHufSlot = 4096;                   // a table of up to 2^11 16-bit cells (symbol | nbBits << 8)
+struct ZHuf {
+    uint32_t frame, tblk, tl, x2, ns, dst, seg, last;
+    uint32_t s0[4], sz[4];
+};
 
 struct ZLayout {
     uint64_t bmax, smax, stride;
     __host__ __device__ uint64_t exe() const { return bmax * sizeof(ZBlk); }
     __host__ __device__ uint64_t cells() const { return exe() + bmax * sizeof(ZExe); }
-    __host__ __device__ uint64_t seqs() const { return cells() + bmax * kCells * 4; }
+    __host__ __device__ uint64_t hufs() const { return cells() + bmax * kSlot; }
+    __host__ __device__ uint64_t seqs() const { return hufs() + bmax * kHufSlot; }
 };
 __host__ __device__ inline ZLayout zlayout(uint64_t chunk) {
     ZLayout L;
@@ -1854,8 +1943,9 @@ __host__ __device__ inline ZLayout zlayout(uint64_t chunk) {
 // one compressed block's literal section and sequence-section header (decode_block up to the
 // sequences); lacc = the next literal position at the output tail
 __device__ __forceinline__ int hdr_block(const Bytes& rin, const Bytes& rout, ZWin& fw, LDSA Lds& L, FrameState& F,
-                                         int bs, int be, int& lacc, ZBlk& B, uint32_t* cells, int b, int& tll, int& tof,
-                                         int& tml, int lane) {
+                                         int bs, int be, int& lacc, ZBlk& B, uint8_t* cells, int b, int& tll, int& tof,
+                                         int& tml, int& thuf, uint8_t* hufs, ZHuf* jobs, uint32_t* njobs, uint32_t frame,
+                                         int lane) {
     const uint32_t b0 = fbyte(fw, bs, lane);
     const int ltype = (int)(b0 & 3u), sf = (int)((b0 >> 2) & 3u);
     int rs, seqpos;
@@ -1889,7 +1979,9 @@ __device__ __forceinline__ int hdr_block(const Bytes& rin, const Bytes& rout, ZW
         int p = bs + hsz;
         if (ltype == 2) {
             int tl = 0;
+            ZCLK(F, 0);
             const int u = read_huf(fw, rin, p, bs + hsz + cs, L, tl, lane);
+            ZCLK(F, 1);
             if (u < 0) return u;
             F.hufV = true;
             F.hufTl = tl;
@@ -1899,10 +1991,47 @@ __device__ __forceinline__ int hdr_block(const Bytes& rin, const Bytes& rout, ZW
             return ZC;
         }
         if (rs == 0 && sf != 0 && ltype == 2) return ZC;
-        int hr = huf_streams(rin, p, bs + hsz + cs - p, sf == 0 ? 1 : 4, rout, lacc, rs, F.hufTl, L, lane);
-        if (hr == 1)
-            hr = F.hufX2 ? huf_streams_x2(rin, p, bs + hsz + cs - p, sf == 0 ? 1 : 4, rout, lacc, rs, F.hufTl, L, lane) : ZC;
-        if (hr < 0) return hr;
+        if (F.hufTl > 11) return kLegacy;            // (the literal kernel's table slots hold 2^11 cells)
+        if (ltype == 2) {                            // the table to the block's slot
+            uint32_t* dst = (uint32_t*)(hufs + (size_t)b * kHufSlot);
+            const LDSA uint32_t* src = (const LDSA uint32_t*)L.huf;
+            for (int c = lane; c < (1 << F.hufTl) / 2; c += LZH_WAVE) dst[c] = src[c];
+            thuf = b;
+        }
+        // the streams' geometry and end marks, as huf_streams checks them; the literal kernel decodes
+        const int csize = bs + hsz + cs - p, ns = sf == 0 ? 1 : 4;
+        ZHuf J{};
+        J.frame = frame;
+        J.tblk = (uint32_t)thuf;
+        J.tl = (uint32_t)F.hufTl;
+        J.x2 = F.hufX2 ? 1u : 0u;
+        J.ns = (uint32_t)ns;
+        J.dst = (uint32_t)lacc;
+        if (ns == 4) {
+            if (csize < 10) return ZC;
+            const int z1 = (int)(fword(fw, p, lane) & 0xffffu), z2 = (int)(fword(fw, p + 2, lane) & 0xffffu),
+                      z3 = (int)(fword(fw, p + 4, lane) & 0xffffu);
+            const int z4 = csize - 6 - z1 - z2 - z3;
+            if (z4 < 1) return ZC;
+            const int seg = (rs + 3) / 4, last = rs - 3 * seg;
+            if (last < 0) return ZC;
+            if (z1 <= 0 || z2 <= 0 || z3 <= 0) return ZC;
+            J.seg = (uint32_t)seg;
+            J.last = (uint32_t)last;
+            const int p1 = p + 6;
+            J.s0[0] = (uint32_t)p1; J.s0[1] = (uint32_t)(p1 + z1); J.s0[2] = (uint32_t)(p1 + z1 + z2);
+            J.s0[3] = (uint32_t)(p1 + z1 + z2 + z3);
+            J.sz[0] = (uint32_t)z1; J.sz[1] = (uint32_t)z2; J.sz[2] = (uint32_t)z3; J.sz[3] = (uint32_t)z4;
+        } else {
+            if (csize <= 0) return ZC;
+            J.seg = J.last = (uint32_t)rs;
+            J.s0[0] = (uint32_t)p;
+            J.sz[0] = (uint32_t)csize;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k < ns && fbyte(fw, (int)(J.s0[k] + J.sz[k]) - 1, lane) == 0) return ZC;   // (BIT_initDStream: no end mark)
+        if (lane == 0) jobs[atomicAdd(njobs, 1u)] = J;
         B.lit = (uint32_t)lacc;
         lacc += rs;
         seqpos = bs + hsz + cs;
@@ -1929,20 +2058,33 @@ __device__ __forceinline__ int hdr_block(const Bytes& rin, const Bytes& rout, ZW
         const uint32_t modes = fbyte(fw, p++, lane);
         if (modes & 3u) return ZC;
         // a table built in this block goes to the block's slot; "repeat" keeps the previous slot
-        auto table = [&](int mode, int which, LDSA Cell* T, int& al, bool& valid, int& slot, int cell0) -> bool {
+        auto table = [&](int mode, int which, LDSA Cell* T, int& al, bool& valid, int& slot) -> bool {
             const int u = seq_table(fw, p, be, mode, which, T, al, valid, L, lane);
             if (u < 0) return false;
             p += u;
-            if (mode != 3) {
-                uint32_t* dst = cells + (size_t)b * kCells + cell0;
-                for (int c = lane; c < (1 << al); c += LZH_WAVE) dst[c] = T[c];
+            if (mode != 3) {   // the cells in the sequence kernel's formats (kSlot)
+                uint8_t* dst = cells + (size_t)b * kSlot;
+                for (int c = lane; c < (1 << al); c += LZH_WAVE) {
+                    const Cell e = T[c];
+                    const uint32_t nx = c_next(e), nb = (uint32_t)c_nb(e), add = (uint32_t)c_add(e), sym = c_sym(e);
+                    if (which == 1) {
+                        ((uint16_t*)(dst + 4096))[c] = (uint16_t)((2u * nx + (1u << nb)) | (sym << 9));
+                    } else {
+                        const uint32_t base = which == 0 ? kLLBase[sym] : kMLBase[sym];
+                        const uint32_t pw = base >= 128u;
+                        const uint32_t lo = pw ? base - (1u << add) : base;
+                        ((uint32_t*)(dst + (which == 0 ? 0 : 2048)))[c] = nx | (nb << 9) | (add << 13) | (pw << 18) | (lo << 19);
+                    }
+                }
                 slot = b;
             }
             return true;
         };
-        if (!table((int)(modes >> 6), 0, L.ll, F.llA, F.llV, tll, 0)) return ZC;
-        if (!table((int)((modes >> 4) & 3u), 1, L.of, F.ofA, F.ofV, tof, 512)) return ZC;
-        if (!table((int)((modes >> 2) & 3u), 2, L.ml, F.mlA, F.mlV, tml, 768)) return ZC;
+        ZCLK(F, 0);
+        if (!table((int)(modes >> 6), 0, L.ll, F.llA, F.llV, tll)) return ZC;
+        if (!table((int)((modes >> 4) & 3u), 1, L.of, F.ofA, F.ofV, tof)) return ZC;
+        if (!table((int)((modes >> 2) & 3u), 2, L.ml, F.mlA, F.mlV, tml)) return ZC;
+        ZCLK(F, 3);
         B.logs = (uint32_t)F.llA | ((uint32_t)F.ofA << 8) | ((uint32_t)F.mlA << 16);
         B.tll = (uint32_t)tll; B.tof = (uint32_t)tof; B.tml = (uint32_t)tml;
         B.pos = (uint32_t)p;
@@ -1954,8 +2096,9 @@ __device__ __forceinline__ int hdr_block(const Bytes& rin, const Bytes& rout, ZW
 }
 
 // the frame's header and blocks (decode_frame without the sequences); returns kGo / kLegacy or an error
-__device__ __forceinline__ int hdr_frame(const Bytes& rin, const Bytes& rout, int cs, LDSA Lds& L, int cap, uint8_t* zb,
-                                         const ZLayout& Z, ZFrame& fr, int lane) {
+__device__ __forceinline__ int hdr_frame_body(const Bytes& rin, const Bytes& rout, int cs, LDSA Lds& L, int cap,
+                                              uint8_t* zb, const ZLayout& Z, ZFrame& fr, int lane, FrameState& F,
+                                              ZHuf* jobs, uint32_t* njobs, uint32_t frame) {
     ZWin fw;
     fw.bind(rin, nullptr);
     fw.load(0, lane);
@@ -2032,9 +2175,8 @@ __device__ __forceinline__ int hdr_frame(const Bytes& rin, const Bytes& rout, in
     }
     if (ltot > n) return ZC;   // an accepted frame's output holds every literal
     ZBlk* blk = (ZBlk*)zb;
-    uint32_t* cells = (uint32_t*)(zb + Z.cells());
-    FrameState F{1, 4, 8, 0, 0, 0, false, false, false, false, false, 0, {0, 0, 0, 0, 0, 0, 0, 0}, 0};
-    int lacc = n - ltot, tll = 0, tof = 0, tml = 0;
+    uint8_t* cells = zb + Z.cells();
+    int lacc = n - ltot, tll = 0, tof = 0, tml = 0, thuf = 0;
     for (int b = 0; b < nb; b++) {
         const uint32_t bh = fbyte(fw, p, lane) | (fbyte(fw, p + 1, lane) << 8) | (fbyte(fw, p + 2, lane) << 16);
         p += 3;
@@ -2050,8 +2192,9 @@ __device__ __forceinline__ int hdr_frame(const Bytes& rin, const Bytes& rout, in
             B.size = (uint32_t)bsz;
             p += 1;
         } else {
-            const int r = hdr_block(rin, rout, fw, L, F, p, p + bsz, lacc, B, cells, b, tll, tof, tml, lane);
-            if (r < 0) return r;
+            const int r = hdr_block(rin, rout, fw, L, F, p, p + bsz, lacc, B, cells, b, tll, tof, tml, thuf, zb + Z.hufs(),
+                                    jobs, njobs, frame, lane);
+            if (r != 0) return r;   // (an error, or kLegacy)
             p += bsz;
         }
         if (lane == 0) blk[b] = B;
@@ -2063,153 +2206,384 @@ __device__ __forceinline__ int hdr_frame(const Bytes& rin, const Bytes& rout, in
     return kGo;
 }
 
-// Per-lane backward bit reader over one frame's sequence stream (SeqBits with per-lane global
-// loads: every lane reads its own frame).  Positions are bits from A (the stream start rounded
-// down to a dword); loads below the packed buffer or past its end are clamped (those bits are
-// garbage that the overrun checks reject, as in BackBits).
-struct LaneBits {
-    const uint8_t* g;
-    int64_t A, lim;
-    int P, D8, lo, na, nxt;
-    uint64_t c;
-    uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
-    __device__ __forceinline__ uint32_t ld(int D) const {
-        int64_t x = A + D;
-        x = x < 0 ? 0 : (x > lim ? lim : x);
-        return __builtin_nontemporal_load((const uint32_t*)(g + x));
-    }
-    __device__ __forceinline__ bool init(const uint8_t* packed, uint64_t readable, int64_t s0, int size) {
-        g = packed;
-        lim = ((int64_t)readable - 4) & ~3ll;
-        A = s0 & ~3ll;
-        const int x0 = (int)(s0 & 3);
-        if (size <= 0) return false;
-        const int X = x0 + size - 1;
-        const uint32_t last = (ld(X & ~3) >> (8 * (X & 3))) & 0xffu;
-        if (last == 0) return false;
-        lo = 8 * x0;
-        P = 8 * X + hb32(last);
-        D8 = ((P - 32) >> 5) << 5;
-        const int D = D8 >> 3;
-        c = ((uint64_t)ld(D + 4) << 32) | ld(D);
-        a0 = ld(D - 4); a1 = ld(D - 8); a2 = ld(D - 12); a3 = ld(D - 16);
-        b0 = ld(D - 20); b1 = ld(D - 24); b2 = ld(D - 28); b3 = ld(D - 32);
-        na = 4;
-        nxt = D - 36;
-        return true;
-    }
-    __device__ __forceinline__ int left() const { return P - lo; }
-    __device__ __forceinline__ uint32_t get(int n) {
-        if (P - n < D8) {
-            c = (c << 32) | a0;
-            a0 = a1; a1 = a2; a2 = a3;
-            D8 -= 32;
-            if (--na == 0) {
-                a0 = b0; a1 = b1; a2 = b2; a3 = b3;
-                b0 = ld(nxt); b1 = ld(nxt - 4); b2 = ld(nxt - 8); b3 = ld(nxt - 12);
-                nxt -= 16;
-                na = 4;
-            }
-        }
-        const uint32_t v = (uint32_t)((c >> (P - n - D8)) & ((1ull << n) - 1ull));
-        P -= n;
-        return v;
-    }
-};
+__device__ __forceinline__ int hdr_frame(const Bytes& rin, const Bytes& rout, int cs, LDSA Lds& L, int cap, uint8_t* zb,
+                                         const ZLayout& Z, ZFrame& fr, int lane, unsigned long long* stats, ZHuf* jobs,
+                                         uint32_t* njobs, uint32_t frame) {
+    FrameState F{1, 4, 8, 0, 0, 0, false, false, false, false, false, 0, {0, 0, 0, 0, 0, 0, 0, 0}, 0};
+    if (LZH_ZSTD_STATS) F.clk_last = __builtin_amdgcn_s_memtime();
+    const int r = hdr_frame_body(rin, rout, cs, L, cap, zb, Z, fr, lane, F, jobs, njobs, frame);
+    ZCLK(F, 7);
+    if (LZH_ZSTD_STATS && stats && lane == 0)
+        for (int i = 0; i < kZClk; i++) atomicAdd(&stats[i], (unsigned long long)F.clk[i]);
+    return r;
+}
 
-// one frame's sequences (this lane's): ZSTD_decompressSequences' decode + execSequence checks
-__device__ __forceinline__ int seq_frame(const uint8_t* packed, uint64_t readable, int64_t ioff, uint8_t* zb,
-                                         const ZLayout& Z, const ZFrame fr, LDSA uint32_t* T, const LDSA uint32_t* base) {
+// The sequence kernel's LDS (kFPW lanes; a "row" holds one dword per lane, as an LDS-DMA
+// (global_load_lds_dword) writes it: lane i at row + 4 i): LL cells 512 rows, ML 512, OF 128 (two
+// 16-bit cells a dword), the bit-stream ring (64 rows: stream dword d at row d mod 64, two halves of
+// 32-dword blocks, + a mirror of row 0), the sequences buffered between flush points (kSB per lane,
+// 8 bytes).  39 456 bytes: 4 waves per CU.
+constexpr int kRow = 4 * kFPW;
+constexpr int kSB = 16;                         // steps between flush / fill points
+constexpr int kLdsML = 512 * kRow, kLdsOF = 1024 * kRow, kLdsRing = 1152 * kRow, kLdsSB = 1217 * kRow;
+constexpr int kLdsSeq = kLdsSB + kSB * kFPW * 8;
+
+__device__ __forceinline__ void dma_row(const uint8_t* src, LDSA uint8_t* row) {
+    __builtin_amdgcn_global_load_lds((const void*)src, (LDSA void*)row, 4, 0, 0);
+}
+// s_waitcnt immediate for vmcnt(n) alone (gfx9: vmcnt bits [3:0] and [15:14], expcnt / lgkmcnt at max)
+constexpr int vmcnt_imm(int n) { return 0x0F70 | (n & 15) | ((n >> 4) << 14); }
+// one dword per lane from a buffer resource into an LDS row (out-of-range offsets read 0, so a
+// negative or oversized per-lane offset needs no clamp).  (No instruction offset: an LDS-DMA adds it
+// to the LDS address as well.)
+__device__ __forceinline__ void dma_rs(rsrc_t r, LDSA uint8_t* row, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDSA void*)row, 4, voff, 0, 0, 0);
+}
+// a buffer resource over [base, base + bytes), bytes clamped to the 32-bit record count
+__device__ __forceinline__ rsrc_t rsrc_over(const void* base, uint64_t bytes) {
+    return make_rsrc(base, (uint32_t)min<uint64_t>(bytes, 0xffffffffull));
+}
+
+// c ? a : b as one v_cndmask on the condition's lane mask (no branch)
+__device__ __forceinline__ int vsel(bool c, int a, int b) {
+    int r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(__builtin_amdgcn_ballot_w64(c)));
+    return r;
+}
+
+}  // namespace zsplit
+
+// Sequences, one frame per lane (lanes 0 .. kFPW-1), in lock-step steps of one sequence per lane:
+// ZSTD_decodeSequence (zstd_decompress_block.c:1169-1270) with the FSE tables and the bit stream in
+// LDS, and every check of ZSTD_execSequence that depends on the output position (decode_block's).
+// A step reads the three cells, then the sequence's four bit fields at once (offset extra bits, match
+// and literal length extra bits, the three state updates: their widths are known from the cells, so
+// are the positions) -- two LDS round trips per sequence, no bit container.  The steps run in
+// intervals of kSB; between intervals (a uniform point, all lanes): wait for the memory operations
+// issued before, flush the buffered sequences, mark the fills issued at the previous point ready,
+// start blocks (raw / RLE / empty ones pass through), give the upper ring block back once the reader
+// is below it, issue the fills lanes asked for -- a block's tables and 32-dword stream blocks -- as
+// LDS-DMA rows masked to those lanes (no load result passes through registers: a per-lane register
+// prefetch would be waited for at once, the wave's memory counter does not tell lanes apart), and
+// set each lane's lowest safe position (the ready data must cover the <= 90 bits a sequence reads).
+// A wave issues one instruction per 4 cycles whatever its lanes do, so the step is kept lean: no
+// branches but the skip and the block's end.
+extern "C" __global__ void __launch_bounds__(64)
+lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t chunk_size,
+                    uint32_t nchunks, int32_t* status, uint8_t* zt, int32_t* zst, const zsplit::ZFrame* zfr,
+                    unsigned long long* stats) {
+    using namespace zsplit;
+    using namespace zstdd;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsSeq];
+    LDSA uint8_t* const S = (LDSA uint8_t*)lds;
+    const int lane = threadIdx.x;
+    const uint32_t f = blockIdx.x * kFPW + (uint32_t)lane;
+    const bool live = lane < kFPW && f < nchunks && zst[f] == kGo;
+    const ZLayout Z = zlayout(chunk_size);
+    uint8_t* const zb = zt + (uint64_t)(live ? f : 0) * Z.stride;
     const ZBlk* blk = (const ZBlk*)zb;
     ZExe* ex = (ZExe*)(zb + Z.exe());
-    const uint32_t* cells = (const uint32_t*)(zb + Z.cells());
     uint64_t* seqs = (uint64_t*)(zb + Z.seqs());
-    const int n = fr.n;
-    int rep0 = 1, rep1 = 4, rep2 = 8, op = 0, si = 0;
-    int cll = -1, cof = -1, cml = -1, all = -1, aof = -1, aml = -1;   // tables now in LDS
-    for (int b = 0; b < fr.nblk; b++) {
-        const ZBlk B = blk[b];
-        if (B.type != 2) {
-            if ((int)B.size > n - op) return ZC;
-            ex[b] = ZExe{(uint32_t)op, (uint32_t)si};
-            op += (int)B.size;
-            continue;
-        }
-        const int rs = (int)B.rs;
-        if (B.ltype != 0 && rs > n - op) return ZC;
-        ex[b] = ZExe{(uint32_t)op, (uint32_t)si};
-        int lp = 0;
-        const int nseq = (int)B.nseq;
-        if (nseq > 0) {
-            const int lA = (int)(B.logs & 255u), oA = (int)((B.logs >> 8) & 255u), mA = (int)(B.logs >> 16);
-            if ((int)B.tll != cll || lA != all) {
-                const uint32_t* s = cells + (size_t)B.tll * kCells;
-                for (int c = 0; c < (1 << lA); c++) T[c] = s[c];
-                cll = (int)B.tll; all = lA;
-            }
-            if ((int)B.tof != cof || oA != aof) {
-                const uint32_t* s = cells + (size_t)B.tof * kCells + 512;
-                for (int c = 0; c < (1 << oA); c++) T[512 + c] = s[c];
-                cof = (int)B.tof; aof = oA;
-            }
-            if ((int)B.tml != cml || mA != aml) {
-                const uint32_t* s = cells + (size_t)B.tml * kCells + 768;
-                for (int c = 0; c < (1 << mA); c++) T[768 + c] = s[c];
-                cml = (int)B.tml; aml = mA;
-            }
-            LaneBits sb;
-            if (!sb.init(packed, readable, ioff + (int64_t)B.pos, (int)B.size)) return ZC;
-            uint32_t sLL = sb.get(lA), sOF = sb.get(oA), sML = sb.get(mA);
-            for (int i = 0; i < nseq; i++) {
-                const Cell eL = T[sLL], eO = T[512 + sOF], eM = T[768 + sML];
-                const int ofc = (int)c_sym(eO);
-                const int llc = (int)c_sym(eL), mlc = (int)c_sym(eM);
-                const int ll0 = llc == 0;
-                int off;
-                if (ofc > 1) {
-                    off = (int)((1u << ofc) - 3u + sb.get(ofc));
-                    rep2 = rep1; rep1 = rep0; rep0 = off;
-                } else if (ofc == 0) {
-                    off = ll0 ? rep1 : rep0;
-                    if (ll0) { rep1 = rep0; rep0 = off; }
-                } else {
-                    const int idx = 1 + ll0 + (int)sb.get(1);
-                    int t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
-                    t += t == 0;
-                    if (idx != 1) rep2 = rep1;
-                    rep1 = rep0;
-                    rep0 = off = t;
-                }
-                const int am = c_add(eM), al = c_add(eL);
-                const uint32_t xb = sb.get(am + al);
-                const int ml = (int)base[36 + mlc] + (int)(xb >> al);
-                const int ll = (int)base[llc] + (int)(xb & ((1u << al) - 1u));
-                if (i + 1 < nseq) {
-                    const int nl = c_nb(eL), nm = c_nb(eM), no = c_nb(eO);
-                    const uint32_t sbits = sb.get(nl + nm + no);
-                    sLL = c_next(eL) + (sbits >> (nm + no));
-                    sML = c_next(eM) + ((sbits >> no) & ((1u << nm) - 1u));
-                    sOF = c_next(eO) + (sbits & ((1u << no) - 1u));
-                    if (sb.left() < 0) return ZC;
-                } else {
-                    const int extra = c_nb(eL) + c_nb(eM) + c_nb(eO);
-                    if (sb.left() > extra || sb.left() < 0) return ZC;
-                }
-                const int lrem = rs - lp;
-                if (ll > lrem || off > op + ll || (int64_t)op + ll + ml > (int64_t)(n - (lrem - ll))) return ZC;
-                if (ll >= (1 << kLenBits) || ml >= (1 << kLenBits) || si >= (int)Z.smax) return kLegacy;
-                seqs[si++] = (uint64_t)ll | ((uint64_t)ml << kLenBits) | ((uint64_t)off << (2 * kLenBits));
-                lp += ll;
-                op += ll + ml;
-            }
-        }
-        const int rem = rs - lp;
-        if (rem > n - op) return ZC;
-        op += rem;
+    int nblk = 0, n = 0;
+    int64_t ioff = 0;
+    if (live) {
+        const ZFrame fr = zfr[f];
+        nblk = fr.nblk;
+        n = fr.n;
+        ioff = (int64_t)offsets[f];
     }
-    if (op != n) return ZC;
-    return kGo;
+    // the wave's frames are consecutive: one resource over the packed stream from the first one's
+    // offset (stream fills), one over their temp (table fills); per-lane 32-bit offsets into them
+    const uint32_t f0 = min(blockIdx.x * kFPW, nchunks - 1);
+    const uint64_t pbase = offsets[f0] & ~3ull;
+    const rsrc_t rp = rsrc_over(packed + pbase, packed_readable > pbase ? packed_readable - pbase : 0);
+    uint8_t* const zb0 = zt + (uint64_t)f0 * Z.stride;
+    const rsrc_t rz = rsrc_over(zb0, (uint64_t)kFPW * Z.stride);
+    uint64_t* const dummy = (uint64_t*)(zt + (uint64_t)nchunks * Z.stride);   // (512 bytes: see the flush)
+    const int lo4 = lane * 4;
+    int phase = live ? 0 : 3, res = kGo;   // 0 block start, 1 waiting for fills, 2 sequences, 3 finished
+    int b = 0, op = 0, sfl = 0, nbuf = 0, rep0 = 1, rep1 = 4, rep2 = 8;
+    int rs = 0, lp = 0, nseq = 0, i = 0, lA = 0, oA = 0, mA = 0;
+    uint32_t sLL = 0, sOF = 0, sML = 0;
+    uint32_t tLL = 0, tOF = 0, tML = 0;   // the block's table slots (offsets in rz)
+    int64_t A = 0;                       // the stream's first byte rounded down to a dword (absolute)
+    int P = 0, lo = 0;                   // bits [lo, P) of the stream are unread (positions from A)
+    int hb0 = 0, hb1 = 0;                // the 32-dword stream blocks in ring halves 0 / 1
+    int rdy = 0, req = 0, iss = 0;       // halves ready / requested / in flight (bits 0, 1)
+    int lowok = 1 << 30;                 // a step runs while P >= lowok
+    bool treq = false, tiss = false, trdy = false;
+    const int smax = (int)Z.smax;
+
+    // bits [q, q + w) of the stream (w <= 31): rows of dwords q / 32 and the one above, a funnel
+    // shift and a bit-field extract
+    auto fld = [&](int q, int w) -> uint32_t {
+        const LDSA uint8_t* a = S + kLdsRing + ((q >> 5) & 63) * kRow + lo4;
+        const uint32_t v = __builtin_amdgcn_alignbit(*(const LDSA uint32_t*)(a + kRow), *(const LDSA uint32_t*)a,
+                                                     (uint32_t)q & 31u);
+        return __builtin_amdgcn_ubfe(v, 0u, (uint32_t)w);
+    };
+
+    uint64_t sst[6] = {0, 0, 0, 0, 0, 0}, tmark = 0;   // (LZH_ZSTD_STATS: uniform points, steps, ...)
+    uint64_t recv[kSB];
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the compiler's own wait tracking sees it
+    for (int ival = 0;; ival++) {
+        if (LZH_ZSTD_STATS) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (ival) sst[1] += t - tmark;
+            tmark = t;
+            sst[2]++;
+        }
+        // ---- uniform point
+        // every memory operation but the previous point's kSB flush stores (issued after its fills) is done
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(kSB));
+        {   // (the buffered records read now, stored at the end of the point)
+#pragma unroll
+            for (int j = 0; j < kSB; j++) recv[j] = *(const LDSA uint64_t*)(S + kLdsSB + (j * kFPW + lane) * 8);
+        }
+        rdy |= iss;
+        iss = 0;
+        if (tiss) { tiss = false; trdy = true; }
+        if (phase == 1 && trdy && rdy == 3) {   // the block's first states (LL, OF, ML)
+            sLL = fld(P - lA, lA);
+            sOF = fld(P - lA - oA, oA);
+            sML = fld(P - lA - oA - mA, mA);
+            P -= lA + oA + mA;
+            phase = 2;
+        }
+        if (LZH_ZSTD_STATS) sst[3] += ballot(phase == 0) != 0;
+        while (phase == 0) {   // the next blocks, up to one with sequences (or the end of the frame)
+            if (b == nblk) {
+                if (op != n) res = ZC;
+                phase = 3;
+                break;
+            }
+            const ZBlk B = blk[b];
+            const int si = sfl + nbuf;
+            if (B.type != 2) {
+                if ((int)B.size > n - op) { res = ZC; phase = 3; break; }
+                ex[b] = ZExe{(uint32_t)op, (uint32_t)si};
+                op += (int)B.size;
+                b++;
+                continue;
+            }
+            rs = (int)B.rs;
+            if (B.ltype != 0 && rs > n - op) { res = ZC; phase = 3; break; }
+            ex[b] = ZExe{(uint32_t)op, (uint32_t)si};
+            lp = 0;
+            i = 0;
+            nseq = (int)B.nseq;
+            b++;
+            if (nseq == 0) {
+                if (rs > n - op) { res = ZC; phase = 3; break; }
+                op += rs;
+                continue;
+            }
+            lA = (int)(B.logs & 255u);
+            oA = (int)((B.logs >> 8) & 255u);
+            mA = (int)(B.logs >> 16);
+            const uint32_t zoff = (uint32_t)(zb - zb0 + Z.cells());
+            tLL = zoff + B.tll * kSlot;
+            tML = zoff + B.tml * kSlot + 2048;
+            tOF = zoff + B.tof * kSlot + 4096;
+            treq = true;
+            trdy = false;
+            // the stream's end mark (BIT_initDStream) and the two blocks below it
+            const int64_t s0 = ioff + (int64_t)B.pos;
+            const int size = (int)B.size;
+            if (size <= 0) { res = ZC; phase = 3; break; }
+            A = s0 & ~3ll;
+            const int x0 = (int)(s0 & 3), X = x0 + size - 1;
+            const uint32_t last = packed[A + X];
+            if (last == 0) { res = ZC; phase = 3; break; }
+            lo = 8 * x0;
+            P = 8 * X + hb32(last);
+            const int bt = (P - 1) >> 10;
+            hb0 = (bt & 1) ? bt - 1 : bt;
+            hb1 = (bt & 1) ? bt : bt - 1;
+            rdy = 0;
+            iss = 0;
+            req = 3;
+            phase = 1;
+        }
+        if (phase == 2) {   // the upper block, once the reader is below it, takes the block under the lower one
+            const int top = (P - 1) >> 10;
+            const bool r0 = (rdy & 1) != 0 && hb0 > top && hb0 > hb1, r1 = (rdy & 2) != 0 && hb1 > top && hb1 > hb0;
+            if (r0) { hb0 = hb1 - 1; rdy &= ~1; req |= 1; }
+            if (r1) { hb1 = hb0 - 1; rdy &= ~2; req |= 2; }
+        }
+        if (ballot(treq)) {
+            if (treq) {
+#pragma unroll 16
+                for (int r = 0; r < 512; r += 16) {
+                    const uint32_t o = tLL + 4 * r;
+                    dma_rs(rz, S + (r + 0) * kRow, o); dma_rs(rz, S + (r + 1) * kRow, o + 4);
+                    dma_rs(rz, S + (r + 2) * kRow, o + 8); dma_rs(rz, S + (r + 3) * kRow, o + 12);
+                    dma_rs(rz, S + (r + 4) * kRow, o + 16); dma_rs(rz, S + (r + 5) * kRow, o + 20);
+                    dma_rs(rz, S + (r + 6) * kRow, o + 24); dma_rs(rz, S + (r + 7) * kRow, o + 28);
+                    dma_rs(rz, S + (r + 8) * kRow, o + 32); dma_rs(rz, S + (r + 9) * kRow, o + 36);
+                    dma_rs(rz, S + (r + 10) * kRow, o + 40); dma_rs(rz, S + (r + 11) * kRow, o + 44);
+                    dma_rs(rz, S + (r + 12) * kRow, o + 48); dma_rs(rz, S + (r + 13) * kRow, o + 52);
+                    dma_rs(rz, S + (r + 14) * kRow, o + 56); dma_rs(rz, S + (r + 15) * kRow, o + 60);
+                }
+                for (int r = 0; r < 512; r += 16) {
+                    const uint32_t o = tML + 4 * r;
+                    LDSA uint8_t* d = S + kLdsML + r * kRow;
+                    dma_rs(rz, d, o); dma_rs(rz, d + kRow, o + 4); dma_rs(rz, d + 2 * kRow, o + 8);
+                    dma_rs(rz, d + 3 * kRow, o + 12); dma_rs(rz, d + 4 * kRow, o + 16); dma_rs(rz, d + 5 * kRow, o + 20);
+                    dma_rs(rz, d + 6 * kRow, o + 24); dma_rs(rz, d + 7 * kRow, o + 28); dma_rs(rz, d + 8 * kRow, o + 32);
+                    dma_rs(rz, d + 9 * kRow, o + 36); dma_rs(rz, d + 10 * kRow, o + 40); dma_rs(rz, d + 11 * kRow, o + 44);
+                    dma_rs(rz, d + 12 * kRow, o + 48); dma_rs(rz, d + 13 * kRow, o + 52); dma_rs(rz, d + 14 * kRow, o + 56);
+                    dma_rs(rz, d + 15 * kRow, o + 60);
+                }
+                for (int r = 0; r < 128; r += 16) {
+                    const uint32_t o = tOF + 4 * r;
+                    LDSA uint8_t* d = S + kLdsOF + r * kRow;
+                    dma_rs(rz, d, o); dma_rs(rz, d + kRow, o + 4); dma_rs(rz, d + 2 * kRow, o + 8);
+                    dma_rs(rz, d + 3 * kRow, o + 12); dma_rs(rz, d + 4 * kRow, o + 16); dma_rs(rz, d + 5 * kRow, o + 20);
+                    dma_rs(rz, d + 6 * kRow, o + 24); dma_rs(rz, d + 7 * kRow, o + 28); dma_rs(rz, d + 8 * kRow, o + 32);
+                    dma_rs(rz, d + 9 * kRow, o + 36); dma_rs(rz, d + 10 * kRow, o + 40); dma_rs(rz, d + 11 * kRow, o + 44);
+                    dma_rs(rz, d + 12 * kRow, o + 48); dma_rs(rz, d + 13 * kRow, o + 52); dma_rs(rz, d + 14 * kRow, o + 56);
+                    dma_rs(rz, d + 15 * kRow, o + 60);
+                }
+                treq = false;
+                tiss = true;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            if (ballot(req & (1 << h))) {
+                if (req & (1 << h)) {   // the block's 32 dwords (offsets below the resource read 0)
+                    const uint32_t o = (uint32_t)(A - (int64_t)pbase + 128ll * (h ? hb1 : hb0));
+                    LDSA uint8_t* d = S + kLdsRing + h * 32 * kRow;
+                    dma_rs(rp, d, o); dma_rs(rp, d + kRow, o + 4); dma_rs(rp, d + 2 * kRow, o + 8);
+                    dma_rs(rp, d + 3 * kRow, o + 12); dma_rs(rp, d + 4 * kRow, o + 16); dma_rs(rp, d + 5 * kRow, o + 20);
+                    dma_rs(rp, d + 6 * kRow, o + 24); dma_rs(rp, d + 7 * kRow, o + 28); dma_rs(rp, d + 8 * kRow, o + 32);
+                    dma_rs(rp, d + 9 * kRow, o + 36); dma_rs(rp, d + 10 * kRow, o + 40); dma_rs(rp, d + 11 * kRow, o + 44);
+                    dma_rs(rp, d + 12 * kRow, o + 48); dma_rs(rp, d + 13 * kRow, o + 52); dma_rs(rp, d + 14 * kRow, o + 56);
+                    dma_rs(rp, d + 15 * kRow, o + 60); dma_rs(rp, d + 16 * kRow, o + 64); dma_rs(rp, d + 17 * kRow, o + 68);
+                    dma_rs(rp, d + 18 * kRow, o + 72); dma_rs(rp, d + 19 * kRow, o + 76); dma_rs(rp, d + 20 * kRow, o + 80);
+                    dma_rs(rp, d + 21 * kRow, o + 84); dma_rs(rp, d + 22 * kRow, o + 88); dma_rs(rp, d + 23 * kRow, o + 92);
+                    dma_rs(rp, d + 24 * kRow, o + 96); dma_rs(rp, d + 25 * kRow, o + 100); dma_rs(rp, d + 26 * kRow, o + 104);
+                    dma_rs(rp, d + 27 * kRow, o + 108); dma_rs(rp, d + 28 * kRow, o + 112); dma_rs(rp, d + 29 * kRow, o + 116);
+                    dma_rs(rp, d + 30 * kRow, o + 120); dma_rs(rp, d + 31 * kRow, o + 124);
+                    if (h == 0) dma_rs(rp, S + kLdsRing + 64 * kRow, o);   // (the mirror of row 0)
+                    req &= ~(1 << h);
+                    iss |= 1 << h;
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // the records buffered during the last interval, after the fills: exactly kSB stores a point
+        // (a lane without a record j writes a dummy word), so that the next point's vmcnt(kSB) waits
+        // for the fills and not for these
+#pragma unroll
+        for (int j = 0; j < kSB; j++) *(j < nbuf ? seqs + sfl + j : dummy + lane) = recv[j];
+        sfl += nbuf;
+        nbuf = 0;
+        // the lowest position a step may start from: the ready blocks below the reader + 90 bits
+        lowok = (rdy == 3 ? 1024 * min(hb0, hb1) : (rdy == 1 ? 1024 * hb0 : (rdy == 2 ? 1024 * hb1 : (1 << 30)))) + 90;
+        if (phase != 2) lowok = 1 << 30;
+        if (LZH_ZSTD_STATS) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            sst[0] += t - tmark;
+            tmark = t;
+        }
+        if (!ballot(phase != 3)) break;
+        if (ival > (smax + 64 * (int)Z.bmax) / 2) {   // (a bound every lane meets: a stuck lane's frame goes to
+            if (phase != 3) { res = kLegacy; phase = 3; }   // the one-wave decoder)
+            lowok = 1 << 30;
+        }
+        // ---- kSB steps
+        for (int k = 0; k < kSB; k++) {
+            if (P < lowok) continue;
+            const uint32_t eL = *(const LDSA uint32_t*)(S + sLL * kRow + lo4);
+            const uint32_t eM = *(const LDSA uint32_t*)(S + kLdsML + sML * kRow + lo4);
+            const uint32_t eO = *(const LDSA uint16_t*)(S + kLdsOF + (sOF >> 1) * kRow + lo4 + (sOF & 1) * 2);
+            const int ofc = (int)(eO >> 9);
+            const uint32_t eOx = eO & 511u;
+            const int no = (int)__builtin_ctz(eOx);
+            const int am = (int)__builtin_amdgcn_ubfe(eM, 13u, 5u), al = (int)__builtin_amdgcn_ubfe(eL, 13u, 5u);
+            const int nl = (int)__builtin_amdgcn_ubfe(eL, 9u, 4u), nm = (int)__builtin_amdgcn_ubfe(eM, 9u, 4u);
+            const int ns = nl + nm + no;
+            const bool lastq = i + 1 == nseq;
+            // the fields: offset extra bits, ML extra bits, LL extra bits, LL / ML / OF state bits
+            const int P1 = P - ofc, P2 = P1 - am, P3 = P2 - al, P4 = P3 - (lastq ? 0 : ns);
+            // (the eight ring loads issued together, then used: the scheduler would wait after each pair)
+            const LDSA uint8_t* a1 = S + kLdsRing + ((P1 >> 5) & 63) * kRow + lo4;
+            const LDSA uint8_t* a2 = S + kLdsRing + ((P2 >> 5) & 63) * kRow + lo4;
+            const LDSA uint8_t* a3 = S + kLdsRing + ((P3 >> 5) & 63) * kRow + lo4;
+            const LDSA uint8_t* a4 = S + kLdsRing + ((P4 >> 5) & 63) * kRow + lo4;
+            const uint32_t w1l = *(const LDSA uint32_t*)a1, w1h = *(const LDSA uint32_t*)(a1 + kRow);
+            const uint32_t w2l = *(const LDSA uint32_t*)a2, w2h = *(const LDSA uint32_t*)(a2 + kRow);
+            const uint32_t w3l = *(const LDSA uint32_t*)a3, w3h = *(const LDSA uint32_t*)(a3 + kRow);
+            const uint32_t w4l = *(const LDSA uint32_t*)a4, w4h = *(const LDSA uint32_t*)(a4 + kRow);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t ob = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w1h, w1l, (uint32_t)P1 & 31u), 0u, (uint32_t)ofc);
+            const uint32_t mb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w2h, w2l, (uint32_t)P2 & 31u), 0u, (uint32_t)am);
+            const uint32_t lb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w3h, w3l, (uint32_t)P3 & 31u), 0u, (uint32_t)al);
+            const uint32_t sb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w4h, w4l, (uint32_t)P4 & 31u), 0u,
+                                                      (uint32_t)(lastq ? 0 : ns));
+            const int ml = (int)(eM >> 19) + (((eM >> 18) & 1u) ? (1 << am) : 0) + (int)mb;
+            const int ll = (int)(eL >> 19) + (((eL >> 18) & 1u) ? (1 << al) : 0) + (int)lb;
+            // repcodes (ZSTD_decodeSequence): ofc > 1 a new offset; else repcode j = ofc + ll0 + bit
+            // (selects on lane masks: the compiler would branch on them)
+            const bool big = ofc > 1;
+            const int j = ofc + (int)((eL >> 18) == 0) + (int)ob;
+            int t = vsel(j == 0, rep0, vsel(j == 1, rep1, vsel(j == 2, rep2, rep0 - 1)));
+            t += t == 0;
+            const int off = vsel(big, (int)((1u << ofc) - 3u + ob), t);
+            const int nrep1 = vsel(big | (j >= 1), rep0, rep1);
+            rep2 = vsel(big | (j >= 2), rep1, rep2);
+            rep1 = nrep1;
+            rep0 = off;
+            sLL = (eL & 511u) + (sb >> (nm + no));
+            sML = (eM & 511u) + __builtin_amdgcn_ubfe(sb, (uint32_t)no, (uint32_t)nm);
+            sOF = ((eOx - (1u << no)) >> 1) + __builtin_amdgcn_ubfe(sb, 0u, (uint32_t)no);
+            P = P4;
+            // the reference updates the states after the last sequence too and accepts an exhausted
+            // or overrun stream there (ZSTD_decompressSequences_body: reload >= completed); then the
+            // checks of ZSTD_execSequence, and the layout's limits (else the one-wave decoder decodes)
+            const int lrem = rs - lp;
+            const bool bad = (P < lo) | (lastq & (P - lo > ns)) | (ll > lrem) | ((uint32_t)off > (uint32_t)(op + ll)) |
+                             (op + ll + ml > n - (lrem - ll));
+            const bool lim17 = ((ll | ml) >= (1 << kLenBits)) | (sfl + nbuf >= smax);
+            {
+                volatile LDSA uint32_t* q = (volatile LDSA uint32_t*)(S + kLdsSB + (nbuf * kFPW + lane) * 8);
+                q[0] = (uint32_t)ll | ((uint32_t)ml << kLenBits);
+                q[1] = ((uint32_t)ml >> (32 - kLenBits)) | ((uint32_t)off << (2 * kLenBits - 32));
+            }
+            nbuf++;
+            lp += ll;
+            op += ll + ml;
+            i++;
+            if (bad | lim17 | lastq) {   // an error, a limit, or the block's end (its last literals)
+                const int rem = rs - lp;
+                if (!(bad | lim17) && rem > n - op) res = ZC;
+                if (bad | lim17) {
+                    res = bad ? ZC : kLegacy;
+                    phase = 3;
+                } else {
+                    op += rem;
+                    phase = 0;
+                }
+                lowok = 1 << 30;
+            }
+            if (LZH_ZSTD_STATS) sst[4]++;
+        }
+    }
+    if (LZH_ZSTD_STATS && stats && lane == 0)
+        for (int k = 0; k < 6; k++) atomicAdd(&stats[k], (unsigned long long)sst[k]);
+    if (live) {
+        if (res == kLegacy) {
+            zst[f] = kLegacy;
+        } else if (res != kGo) {
+            status[f] = res;
+            zst[f] = kDone;
+        }
+    }
 }
+
+namespace zsplit {
 
 // one frame's output from its blocks and sequences (one wave)
 __device__ __forceinline__ int exec_frame(const Bytes& rin, const Bytes& rout, const Bytes& lout, ZSink& O, LDSA uint8_t* mark,
@@ -2293,7 +2667,7 @@ __device__ __forceinline__ int exec_frame(const Bytes& rin, const Bytes& rout, c
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_hdr_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, const uint32_t* csizes,
                     uint64_t n_total, uint64_t chunk_size, uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst,
-                    zsplit::ZFrame* zfr) {
+                    zsplit::ZFrame* zfr, unsigned long long* stats, zsplit::ZHuf* jobs, uint32_t* njobs) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_raw[(zstdd::kLdsHdr + 3) / 4];
     LDSA zstdd::Lds& L = *(LDSA zstdd::Lds*)lds_raw;
     const int lane = threadIdx.x;
@@ -2317,7 +2691,8 @@ lzh_zstd_hdr_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     }
     const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
     zsplit::ZFrame fr{0, 0, -1, 0};
-    const int r = zsplit::hdr_frame(rin, rout, cs, L, part, zt + chunk * Z.stride, Z, fr, lane);
+    const int r = zsplit::hdr_frame(rin, rout, cs, L, part, zt + chunk * Z.stride, Z, fr, lane, stats, jobs, njobs,
+                                    (uint32_t)chunk);
     if (lane == 0) {
         if (r == zsplit::kGo) zfr[chunk] = fr;
         zst[chunk] = r == zsplit::kGo ? zsplit::kGo : (r == zsplit::kLegacy ? zsplit::kLegacy : zsplit::kDone);
@@ -2325,24 +2700,194 @@ lzh_zstd_hdr_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     }
 }
 
+// Huffman literal streams, one stream per lane: 4 sections a wave (lanes 4q + j: section q, stream
+// j), 8 waves per CU.  LDS: the sections' tables (2^11 cells each, rows of 16 lanes x 4 bytes as an
+// LDS-DMA writes them: section q's dword d at row d / 4, lane 4q + d mod 4), the streams' bit rings
+// (32 rows: stream dword d at row d mod 32, two halves of 16-dword blocks, + a mirror of row 0), the
+// decoded bytes staged between flush points.  One symbol per lane per step (HUF_decodeSymbolX1: a
+// tl-bit lookup, bits below the stream start read as zero); uniform points every kHB steps as in the
+// sequence kernel.  A stream not consumed exactly (huf_streams' verdict 1) sends its frame to the
+// one-wave decoder when the reference would use the double-symbol decoder there, else it is corrupt.
+namespace zsplit {
+constexpr int kHJ = 4, kHL = 4 * kHJ;            // sections a wave, lanes in use
+constexpr int kHRow = 4 * kHL;                   // 64 bytes
+constexpr int kHB = 16;                          // steps between uniform points (= bytes staged per lane)
+constexpr int kHLdsRing = 256 * kHRow, kHLdsStage = kHLdsRing + 33 * kHRow, kHLds = kHLdsStage + kHL * kHB;
+}  // namespace zsplit
+
 extern "C" __global__ void __launch_bounds__(64)
-lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t chunk_size,
-                    uint32_t nchunks, int32_t* status, uint8_t* zt, int32_t* zst, const zsplit::ZFrame* zfr) {
-    __shared__ __attribute__((aligned(16))) uint32_t tabs[zsplit::kFPW * zsplit::kCells];
-    __shared__ uint32_t base[36 + 53];
+lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t n_total,
+                    uint64_t chunk_size, uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst,
+                    const zsplit::ZHuf* jobs, const uint32_t* njobs) {
+    using namespace zsplit;
+    using namespace zstdd;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kHLds];
+    LDSA uint8_t* const S = (LDSA uint8_t*)lds;
     const int lane = threadIdx.x;
-    for (int i = lane; i < 36 + 53; i += LZH_WAVE) base[i] = i < 36 ? zstdd::kLLBase[i] : zstdd::kMLBase[i - 36];
-    __syncthreads();
-    const uint32_t f = blockIdx.x * zsplit::kFPW + (uint32_t)lane;
-    if (lane >= zsplit::kFPW || f >= nchunks || zst[f] != zsplit::kGo) return;
-    const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
-    const int r = zsplit::seq_frame(packed, packed_readable, (int64_t)offsets[f], zt + (uint64_t)f * Z.stride, Z, zfr[f],
-                                    (LDSA uint32_t*)tabs + lane * zsplit::kCells, (const LDSA uint32_t*)base);
-    if (r == zsplit::kLegacy) {
-        zst[f] = zsplit::kLegacy;
-    } else if (r != zsplit::kGo) {
-        status[f] = r;
-        zst[f] = zsplit::kDone;
+    const int q = lane >> 2, j = lane & 3;
+    const uint32_t jid = blockIdx.x * kHJ + (uint32_t)q;
+    const bool jlive = lane < kHL && jid < *njobs;
+    uint32_t jf = 0, jtblk = 0, jtl = 0, jx2 = 0, jns = 0, jdst = 0, jseg = 0, jlast = 0, js0 = 0, jsz = 0;
+    if (jlive) {
+        const ZHuf* J = jobs + jid;
+        jf = J->frame; jtblk = J->tblk; jtl = J->tl; jx2 = J->x2; jns = J->ns; jdst = J->dst; jseg = J->seg;
+        jlast = J->last; js0 = J->s0[j]; jsz = J->sz[j];
+    }
+    bool slive = jlive && zst[jf] == kGo && (uint32_t)j < jns;
+    const ZLayout Z = zlayout(chunk_size);
+    // resources from the wave's lowest frame: the packed streams and the table slots (per-lane 32-bit
+    // offsets; a section whose offsets would not fit goes to the one-wave decoder)
+    uint32_t fmin = jlive ? jf : 0xffffffffu;
+    for (int k = 1; k < 64; k <<= 1) fmin = min(fmin, (uint32_t)__shfl_xor((int)fmin, k));
+    fmin = uni(fmin == 0xffffffffu ? 0u : fmin);
+    const uint64_t pbase = offsets[fmin] & ~3ull;
+    const rsrc_t rp = rsrc_over(packed + pbase, packed_readable > pbase ? packed_readable - pbase : 0);
+    const uint8_t* zb0 = zt + (uint64_t)fmin * Z.stride;
+    const rsrc_t rz = rsrc_over(zb0, (uint64_t)0xffffffffull);
+    const uint64_t toff = (uint64_t)(jf - fmin) * Z.stride + Z.hufs() + (uint64_t)jtblk * kHufSlot;
+    bool far_ = jlive && toff + kHufSlot > 0xffffffffull;
+    uint8_t* const dummy = zt + (uint64_t)(chunk_size ? (n_total + chunk_size - 1) / chunk_size : 0) * Z.stride;
+    const int l4 = lane * 4;
+    const int tl = (int)jtl;
+    // this lane's stream
+    int P = 0, lo = 0, nsym = 0, done = 0, flushed = 0;
+    int64_t A = 0;
+    uint8_t* dst = out;
+    if (slive) {
+        const int64_t s0 = (int64_t)offsets[jf] + (int64_t)js0;
+        A = s0 & ~3ll;
+        far_ |= A - (int64_t)pbase + (int64_t)jsz + 256 > 0xffffffffll;
+        const int x0 = (int)(s0 & 3), X = x0 + (int)jsz - 1;
+        lo = 8 * x0;
+        P = 8 * X + hb32((uint32_t)packed[A + X]);   // (the end mark: checked non-zero by the header kernel)
+        nsym = j == 3 ? (int)jlast : (int)jseg;
+        dst = out + (uint64_t)jf * chunk_size + jdst + (uint64_t)j * jseg;
+    }
+    int hb0 = 0, hb1 = 0, rdy = 0, req = 0, iss = 0;
+    {
+        const int bt = (P - 1) >> 9;
+        hb0 = (bt & 1) ? bt - 1 : bt;
+        hb1 = (bt & 1) ? bt : bt - 1;
+        req = slive ? 3 : 0;
+    }
+    {   // (a section whose offsets do not fit: its frame goes to the one-wave decoder)
+        const uint64_t fm = ballot(far_);
+        if (fm) {
+            const bool qfar = ((fm >> (4 * q)) & 15ull) != 0;
+            if (qfar && j == 0 && jlive) atomicMax(&zst[jf], kLegacy);
+            slive = slive && !qfar;
+        }
+    }
+    bool tdone = false;
+    int res = 0;                                  // 0 going, 1 exact, 2 not exact
+    auto fld = [&](int bq, int w) -> uint32_t {
+        const LDSA uint8_t* a = S + kHLdsRing + ((bq >> 5) & 31) * kHRow + l4;
+        const uint32_t v = __builtin_amdgcn_alignbit(*(const volatile LDSA uint32_t*)(a + kHRow),
+                                                     *(const volatile LDSA uint32_t*)a, (uint32_t)bq & 31u);
+        return __builtin_amdgcn_ubfe(v, 0u, (uint32_t)w);
+    };
+    if (!slive) req = 0;
+    bool going = slive;
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    for (int step = 0;; step++) {
+        if ((step & (kHB - 1)) == 0) {
+            // every memory operation but the previous point's kHB byte stores (issued after its fills) is done
+            __builtin_amdgcn_s_waitcnt(vmcnt_imm(kHB));
+            const int nb = done - flushed;
+            const uint32_t w0 = *(const LDSA uint32_t*)(S + kHLdsStage + lane * kHB),
+                           w1 = *(const LDSA uint32_t*)(S + kHLdsStage + lane * kHB + 4),
+                           w2 = *(const LDSA uint32_t*)(S + kHLdsStage + lane * kHB + 8),
+                           w3 = *(const LDSA uint32_t*)(S + kHLdsStage + lane * kHB + 12);
+            rdy |= iss;
+            iss = 0;
+            if (!tdone && ballot(jlive)) {   // (step 0) the sections' tables: row r = dwords 4r .. 4r+3
+                if (jlive) {
+                    const uint32_t o = (uint32_t)toff + 4 * j;
+                    for (int r = 0; r < 256; r += 16) {
+                        LDSA uint8_t* d = S + r * kHRow;
+                        const uint32_t orr = o + 16 * r;
+                        dma_rs(rz, d, orr); dma_rs(rz, d + kHRow, orr + 16); dma_rs(rz, d + 2 * kHRow, orr + 32);
+                        dma_rs(rz, d + 3 * kHRow, orr + 48); dma_rs(rz, d + 4 * kHRow, orr + 64);
+                        dma_rs(rz, d + 5 * kHRow, orr + 80); dma_rs(rz, d + 6 * kHRow, orr + 96);
+                        dma_rs(rz, d + 7 * kHRow, orr + 112); dma_rs(rz, d + 8 * kHRow, orr + 128);
+                        dma_rs(rz, d + 9 * kHRow, orr + 144); dma_rs(rz, d + 10 * kHRow, orr + 160);
+                        dma_rs(rz, d + 11 * kHRow, orr + 176); dma_rs(rz, d + 12 * kHRow, orr + 192);
+                        dma_rs(rz, d + 13 * kHRow, orr + 208); dma_rs(rz, d + 14 * kHRow, orr + 224);
+                        dma_rs(rz, d + 15 * kHRow, orr + 240);
+                    }
+                }
+                tdone = true;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                if (ballot(req & (1 << h))) {
+                    if (req & (1 << h)) {   // the block's 16 dwords (offsets below the resource read 0)
+                        const uint32_t o = (uint32_t)(A - (int64_t)pbase + 64ll * (h ? hb1 : hb0));
+                        LDSA uint8_t* d = S + kHLdsRing + h * 16 * kHRow;
+                        dma_rs(rp, d, o); dma_rs(rp, d + kHRow, o + 4); dma_rs(rp, d + 2 * kHRow, o + 8);
+                        dma_rs(rp, d + 3 * kHRow, o + 12); dma_rs(rp, d + 4 * kHRow, o + 16);
+                        dma_rs(rp, d + 5 * kHRow, o + 20); dma_rs(rp, d + 6 * kHRow, o + 24);
+                        dma_rs(rp, d + 7 * kHRow, o + 28); dma_rs(rp, d + 8 * kHRow, o + 32);
+                        dma_rs(rp, d + 9 * kHRow, o + 36); dma_rs(rp, d + 10 * kHRow, o + 40);
+                        dma_rs(rp, d + 11 * kHRow, o + 44); dma_rs(rp, d + 12 * kHRow, o + 48);
+                        dma_rs(rp, d + 13 * kHRow, o + 52); dma_rs(rp, d + 14 * kHRow, o + 56);
+                        dma_rs(rp, d + 15 * kHRow, o + 60);
+                        if (h == 0) dma_rs(rp, S + kHLdsRing + 32 * kHRow, o);   // (the mirror of row 0)
+                        req &= ~(1 << h);
+                        iss |= 1 << h;
+                    }
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            {   // the staged bytes out, after the fills: exactly kHB byte stores a point (a lane without a
+                // byte t writes a dummy one), so that the next point's vmcnt(kHB) waits for the fills only
+                const int r = flushed & (kHB - 1);
+#pragma unroll
+                for (int k = 0; k < kHB; k++) {
+                    const int sl = (r + k) & (kHB - 1);
+                    const uint32_t w = sl < 4 ? w0 : (sl < 8 ? w1 : (sl < 12 ? w2 : w3));
+                    *(k < nb ? dst + flushed + k : dummy + lane) = (uint8_t)(w >> (8 * (sl & 3)));
+                }
+                flushed = done;
+            }
+            if (!ballot(going || done != flushed)) break;
+            if (step > 16 * kBlockMax) {   // (a bound every stream meets)
+                if (going) { going = false; res = 2; }
+            }
+        }
+        if (!going || step < kHB) continue;      // (tables and rings land at the first point after step 0)
+        {   // skip the step while the lowest bit of the lookup is in a block not ready
+            const int bm = (P - 12) >> 9;
+            const bool ok = (bm & 1) ? (hb1 == bm && (rdy & 2)) : (hb0 == bm && (rdy & 1));
+            if (!ok) continue;
+        }
+        if (done == nsym) {                      // huf_streams' verdict: exactly consumed
+            res = P == lo ? 1 : 2;
+            going = false;
+            continue;
+        }
+        const int bq = P - tl;
+        uint32_t v = fld(bq, tl);
+        if (bq < lo) v &= lo - bq >= 32 ? 0u : (~0u << (lo - bq));   // (zero-padded below the start)
+        const uint32_t e = *(const volatile LDSA uint16_t*)(S + ((v >> 3) << 6) + (q << 4) + (v & 7) * 2);
+        P -= (int)(e >> 8);
+        *(volatile LDSA uint8_t*)(S + kHLdsStage + lane * kHB + (done & (kHB - 1))) = (uint8_t)e;
+        done++;
+        {   // the upper block, once the reader is below it, takes the block under the lower one
+            const int top = (P - 1) >> 9;
+            const bool r0 = (rdy & 1) != 0 && hb0 > top && hb0 > hb1, r1 = (rdy & 2) != 0 && hb1 > top && hb1 > hb0;
+            hb0 = vsel(r0, hb1 - 1, hb0);
+            hb1 = vsel(r1, hb0 - 1, hb1);
+            rdy &= ~(int)(r0 | ((int)r1 << 1));
+            req |= (int)r0 | ((int)r1 << 1);
+        }
+    }
+    if (slive && res == 2) {   // not consumed exactly: X2's verdict (the one-wave decoder) or corrupt
+        if (jx2) {
+            atomicMax(&zst[jf], kLegacy);
+        } else if (atomicMax(&zst[jf], kDone) != kDone) {
+            status[jf] = ZC;
+        }
     }
 }
 
@@ -2459,19 +3004,6 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
                                       const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                       int32_t* status, uint32_t nchunks, uint8_t* zt, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
-    const int32_t* zsel = nullptr;
-    if (zt && !g_zstd_legacy) {   // the split kernels; frames they leave go to the one-wave decoder below
-        const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
-        int32_t* zst = (int32_t*)(zt + (uint64_t)nchunks * Z.stride);
-        zsplit::ZFrame* zfr = (zsplit::ZFrame*)((uint8_t*)zst + (((uint64_t)nchunks * 4 + 255) & ~255ull));
-        hipLaunchKernelGGL(lzh_zstd_hdr_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
-                           n_total, chunk_size, out, status, zt, zst, zfr);
-        hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3((nchunks + zsplit::kFPW - 1) / zsplit::kFPW), dim3(64), 0, s, packed,
-                           packed_readable, offsets, chunk_size, nchunks, status, zt, zst, zfr);
-        hipLaunchKernelGGL(lzh_zstd_exec_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
-                           n_total, chunk_size, out, status, zt, zst, zfr);
-        zsel = zst;
-    }
     unsigned long long* stats = nullptr;
 #if LZH_ZSTD_STATS
     static unsigned long long* d_stats = nullptr;
@@ -2479,6 +3011,44 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
     (void)hipMemsetAsync(d_stats, 0, zstdd::kZClk * sizeof(unsigned long long), s);
     stats = d_stats;
 #endif
+    const int32_t* zsel = nullptr;
+    if (zt && !g_zstd_legacy) {   // the split kernels; frames they leave go to the one-wave decoder below
+        const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
+        int32_t* zst = (int32_t*)(zt + (uint64_t)nchunks * Z.stride + 512);   // (512 bytes: the dummy words)
+        zsplit::ZFrame* zfr = (zsplit::ZFrame*)((uint8_t*)zst + (((uint64_t)nchunks * 4 + 255) & ~255ull));
+        uint32_t* njobs = (uint32_t*)((uint8_t*)zfr + (((uint64_t)nchunks * sizeof(zsplit::ZFrame) + 255) & ~255ull));
+        zsplit::ZHuf* jobs = (zsplit::ZHuf*)((uint8_t*)njobs + 256);
+        (void)hipMemsetAsync(njobs, 0, 4, s);
+        hipLaunchKernelGGL(lzh_zstd_hdr_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
+                           n_total, chunk_size, out, status, zt, zst, zfr, stats, jobs, njobs);
+        const uint64_t maxjobs = (uint64_t)nchunks * Z.bmax;
+        hipLaunchKernelGGL(lzh_zstd_huf_kernel, dim3((unsigned)((maxjobs + zsplit::kHJ - 1) / zsplit::kHJ)), dim3(64), 0, s,
+                           packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst,
+                           (const zsplit::ZHuf*)jobs, (const uint32_t*)njobs);
+        unsigned long long* sstats = nullptr;
+#if LZH_ZSTD_STATS
+        static unsigned long long* d_sst = nullptr;
+        if (!d_sst) (void)hipMalloc(&d_sst, 8 * sizeof(unsigned long long));
+        (void)hipMemsetAsync(d_sst, 0, 8 * sizeof(unsigned long long), s);
+        sstats = d_sst;
+#endif
+        hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3((nchunks + zsplit::kFPW - 1) / zsplit::kFPW), dim3(64), 0, s, packed,
+                           packed_readable, offsets, chunk_size, nchunks, status, zt, zst, zfr, sstats);
+#if LZH_ZSTD_STATS
+        {
+            unsigned long long h[8];
+            (void)hipMemcpyAsync(h, d_sst, sizeof(h), hipMemcpyDeviceToHost, s);
+            (void)hipStreamSynchronize(s);
+            const double w = (double)((nchunks + zsplit::kFPW - 1) / zsplit::kFPW);
+            fprintf(stderr, "zstd seq kernel per wave: intervals %.0f (with block starts %.0f), steps %.0f; clocks per "
+                            "interval: uniform point %.0f, steps %.0f\n",
+                    h[2] / w, h[3] / w, h[4] / w, (double)h[0] / h[2], (double)h[1] / h[2]);
+        }
+#endif
+        hipLaunchKernelGGL(lzh_zstd_exec_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
+                           n_total, chunk_size, out, status, zt, zst, zfr);
+        zsel = zst;
+    }
     hipLaunchKernelGGL(lzh_zstd_decompress_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets,
                        csizes, n_total, chunk_size, out, status, 0u, stats, zsel);
 #if LZH_ZSTD_STATS
@@ -2502,5 +3072,6 @@ size_t lzh_zstd_decode_temp(uint64_t n, uint64_t chunk_size) {
     if (!chunk_size) return 0;
     const uint64_t k = (n + chunk_size - 1) / chunk_size;
     const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
-    return k * Z.stride + ((k * 4 + 255) & ~255ull) + k * sizeof(zsplit::ZFrame) + 256;
+    return k * Z.stride + 512 + ((k * 4 + 255) & ~255ull) + ((k * sizeof(zsplit::ZFrame) + 255) & ~255ull) + 256 +
+           k * Z.bmax * sizeof(zsplit::ZHuf) + 256;
 }
