@@ -2226,7 +2226,7 @@ __device__ __forceinline__ int hdr_frame(const Bytes& rin, const Bytes& rout, in
 constexpr int kRow = 4 * kFPW;
 constexpr int kSB = 16;                         // steps between flush / fill points
 constexpr int kLdsML = 512 * kRow, kLdsOF = 1024 * kRow, kLdsRing = 1152 * kRow, kLdsSB = 1217 * kRow;
-constexpr int kLdsSeq = kLdsSB + kSB * kFPW * 8;
+constexpr int kLdsSeq = kLdsSB;
 
 __device__ __forceinline__ void dma_row(const uint8_t* src, LDSA uint8_t* row) {
     __builtin_amdgcn_global_load_lds((const void*)src, (LDSA void*)row, 4, 0, 0);
@@ -2292,20 +2292,16 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
         n = fr.n;
         ioff = (int64_t)offsets[f];
     }
-    // the wave's frames are consecutive: one resource over the packed stream from the first one's
-    // offset (stream fills), one over their temp (table fills); per-lane 32-bit offsets into them
-    const uint32_t f0 = min(blockIdx.x * kFPW, nchunks - 1);
-    const uint64_t pbase = offsets[f0] & ~3ull;
-    const rsrc_t rp = rsrc_over(packed + pbase, packed_readable > pbase ? packed_readable - pbase : 0);
-    uint8_t* const zb0 = zt + (uint64_t)f0 * Z.stride;
-    const rsrc_t rz = rsrc_over(zb0, (uint64_t)kFPW * Z.stride);
+    // (fills are global_load_lds rows from per-lane addresses: with a buffer resource the kernel's
+    // scalar-register pressure moved it to vector registers and every fill became a waterfall loop)
+    const int64_t readable = (int64_t)packed_readable;
     uint64_t* const dummy = (uint64_t*)(zt + (uint64_t)nchunks * Z.stride);   // (512 bytes: see the flush)
     const int lo4 = lane * 4;
     int phase = live ? 0 : 3, res = kGo;   // 0 block start, 1 waiting for fills, 2 sequences, 3 finished
-    int b = 0, op = 0, sfl = 0, nbuf = 0, rep0 = 1, rep1 = 4, rep2 = 8;
+    int b = 0, op = 0, sfl = 0, rep0 = 1, rep1 = 4, rep2 = 8;   // (sfl: sequences stored)
     int rs = 0, lp = 0, nseq = 0, i = 0, lA = 0, oA = 0, mA = 0;
     uint32_t sLL = 0, sOF = 0, sML = 0;
-    uint32_t tLL = 0, tOF = 0, tML = 0;   // the block's table slots (offsets in rz)
+    const uint8_t *tLL = zb, *tOF = zb, *tML = zb;   // the block's table slots
     int64_t A = 0;                       // the stream's first byte rounded down to a dword (absolute)
     int P = 0, lo = 0;                   // bits [lo, P) of the stream are unread (positions from A)
     int hb0 = 0, hb1 = 0;                // the 32-dword stream blocks in ring halves 0 / 1
@@ -2324,7 +2320,6 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     };
 
     uint64_t sst[6] = {0, 0, 0, 0, 0, 0}, tmark = 0;   // (LZH_ZSTD_STATS: uniform points, steps, ...)
-    uint64_t recv[kSB];
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the compiler's own wait tracking sees it
     for (int ival = 0;; ival++) {
         if (LZH_ZSTD_STATS) {
@@ -2336,10 +2331,7 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
         // ---- uniform point
         // every memory operation but the previous point's kSB flush stores (issued after its fills) is done
         __builtin_amdgcn_s_waitcnt(vmcnt_imm(kSB));
-        {   // (the buffered records read now, stored at the end of the point)
-#pragma unroll
-            for (int j = 0; j < kSB; j++) recv[j] = *(const LDSA uint64_t*)(S + kLdsSB + (j * kFPW + lane) * 8);
-        }
+        if (LZH_ZSTD_STATS) sst[5] += __builtin_amdgcn_s_memtime() - tmark;
         rdy |= iss;
         iss = 0;
         if (tiss) { tiss = false; trdy = true; }
@@ -2358,7 +2350,7 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 break;
             }
             const ZBlk B = blk[b];
-            const int si = sfl + nbuf;
+            const int si = sfl;
             if (B.type != 2) {
                 if ((int)B.size > n - op) { res = ZC; phase = 3; break; }
                 ex[b] = ZExe{(uint32_t)op, (uint32_t)si};
@@ -2381,10 +2373,10 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
             lA = (int)(B.logs & 255u);
             oA = (int)((B.logs >> 8) & 255u);
             mA = (int)(B.logs >> 16);
-            const uint32_t zoff = (uint32_t)(zb - zb0 + Z.cells());
-            tLL = zoff + B.tll * kSlot;
-            tML = zoff + B.tml * kSlot + 2048;
-            tOF = zoff + B.tof * kSlot + 4096;
+            const uint8_t* cz = zb + Z.cells();
+            tLL = cz + (size_t)B.tll * kSlot;
+            tML = cz + (size_t)B.tml * kSlot + 2048;
+            tOF = cz + (size_t)B.tof * kSlot + 4096;
             treq = true;
             trdy = false;
             // the stream's end mark (BIT_initDStream) and the two blocks below it
@@ -2413,38 +2405,12 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
         }
         if (ballot(treq)) {
             if (treq) {
-#pragma unroll 16
-                for (int r = 0; r < 512; r += 16) {
-                    const uint32_t o = tLL + 4 * r;
-                    dma_rs(rz, S + (r + 0) * kRow, o); dma_rs(rz, S + (r + 1) * kRow, o + 4);
-                    dma_rs(rz, S + (r + 2) * kRow, o + 8); dma_rs(rz, S + (r + 3) * kRow, o + 12);
-                    dma_rs(rz, S + (r + 4) * kRow, o + 16); dma_rs(rz, S + (r + 5) * kRow, o + 20);
-                    dma_rs(rz, S + (r + 6) * kRow, o + 24); dma_rs(rz, S + (r + 7) * kRow, o + 28);
-                    dma_rs(rz, S + (r + 8) * kRow, o + 32); dma_rs(rz, S + (r + 9) * kRow, o + 36);
-                    dma_rs(rz, S + (r + 10) * kRow, o + 40); dma_rs(rz, S + (r + 11) * kRow, o + 44);
-                    dma_rs(rz, S + (r + 12) * kRow, o + 48); dma_rs(rz, S + (r + 13) * kRow, o + 52);
-                    dma_rs(rz, S + (r + 14) * kRow, o + 56); dma_rs(rz, S + (r + 15) * kRow, o + 60);
-                }
-                for (int r = 0; r < 512; r += 16) {
-                    const uint32_t o = tML + 4 * r;
-                    LDSA uint8_t* d = S + kLdsML + r * kRow;
-                    dma_rs(rz, d, o); dma_rs(rz, d + kRow, o + 4); dma_rs(rz, d + 2 * kRow, o + 8);
-                    dma_rs(rz, d + 3 * kRow, o + 12); dma_rs(rz, d + 4 * kRow, o + 16); dma_rs(rz, d + 5 * kRow, o + 20);
-                    dma_rs(rz, d + 6 * kRow, o + 24); dma_rs(rz, d + 7 * kRow, o + 28); dma_rs(rz, d + 8 * kRow, o + 32);
-                    dma_rs(rz, d + 9 * kRow, o + 36); dma_rs(rz, d + 10 * kRow, o + 40); dma_rs(rz, d + 11 * kRow, o + 44);
-                    dma_rs(rz, d + 12 * kRow, o + 48); dma_rs(rz, d + 13 * kRow, o + 52); dma_rs(rz, d + 14 * kRow, o + 56);
-                    dma_rs(rz, d + 15 * kRow, o + 60);
-                }
-                for (int r = 0; r < 128; r += 16) {
-                    const uint32_t o = tOF + 4 * r;
-                    LDSA uint8_t* d = S + kLdsOF + r * kRow;
-                    dma_rs(rz, d, o); dma_rs(rz, d + kRow, o + 4); dma_rs(rz, d + 2 * kRow, o + 8);
-                    dma_rs(rz, d + 3 * kRow, o + 12); dma_rs(rz, d + 4 * kRow, o + 16); dma_rs(rz, d + 5 * kRow, o + 20);
-                    dma_rs(rz, d + 6 * kRow, o + 24); dma_rs(rz, d + 7 * kRow, o + 28); dma_rs(rz, d + 8 * kRow, o + 32);
-                    dma_rs(rz, d + 9 * kRow, o + 36); dma_rs(rz, d + 10 * kRow, o + 40); dma_rs(rz, d + 11 * kRow, o + 44);
-                    dma_rs(rz, d + 12 * kRow, o + 48); dma_rs(rz, d + 13 * kRow, o + 52); dma_rs(rz, d + 14 * kRow, o + 56);
-                    dma_rs(rz, d + 15 * kRow, o + 60);
-                }
+#pragma unroll 8
+                for (int r = 0; r < 512; r++) dma_row(tLL + 4 * r, S + r * kRow);
+#pragma unroll 8
+                for (int r = 0; r < 512; r++) dma_row(tML + 4 * r, S + kLdsML + r * kRow);
+#pragma unroll 8
+                for (int r = 0; r < 128; r++) dma_row(tOF + 4 * r, S + kLdsOF + r * kRow);
                 treq = false;
                 tiss = true;
             }
@@ -2452,34 +2418,29 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             if (ballot(req & (1 << h))) {
-                if (req & (1 << h)) {   // the block's 32 dwords (offsets below the resource read 0)
-                    const uint32_t o = (uint32_t)(A - (int64_t)pbase + 128ll * (h ? hb1 : hb0));
-                    LDSA uint8_t* d = S + kLdsRing + h * 32 * kRow;
-                    dma_rs(rp, d, o); dma_rs(rp, d + kRow, o + 4); dma_rs(rp, d + 2 * kRow, o + 8);
-                    dma_rs(rp, d + 3 * kRow, o + 12); dma_rs(rp, d + 4 * kRow, o + 16); dma_rs(rp, d + 5 * kRow, o + 20);
-                    dma_rs(rp, d + 6 * kRow, o + 24); dma_rs(rp, d + 7 * kRow, o + 28); dma_rs(rp, d + 8 * kRow, o + 32);
-                    dma_rs(rp, d + 9 * kRow, o + 36); dma_rs(rp, d + 10 * kRow, o + 40); dma_rs(rp, d + 11 * kRow, o + 44);
-                    dma_rs(rp, d + 12 * kRow, o + 48); dma_rs(rp, d + 13 * kRow, o + 52); dma_rs(rp, d + 14 * kRow, o + 56);
-                    dma_rs(rp, d + 15 * kRow, o + 60); dma_rs(rp, d + 16 * kRow, o + 64); dma_rs(rp, d + 17 * kRow, o + 68);
-                    dma_rs(rp, d + 18 * kRow, o + 72); dma_rs(rp, d + 19 * kRow, o + 76); dma_rs(rp, d + 20 * kRow, o + 80);
-                    dma_rs(rp, d + 21 * kRow, o + 84); dma_rs(rp, d + 22 * kRow, o + 88); dma_rs(rp, d + 23 * kRow, o + 92);
-                    dma_rs(rp, d + 24 * kRow, o + 96); dma_rs(rp, d + 25 * kRow, o + 100); dma_rs(rp, d + 26 * kRow, o + 104);
-                    dma_rs(rp, d + 27 * kRow, o + 108); dma_rs(rp, d + 28 * kRow, o + 112); dma_rs(rp, d + 29 * kRow, o + 116);
-                    dma_rs(rp, d + 30 * kRow, o + 120); dma_rs(rp, d + 31 * kRow, o + 124);
-                    if (h == 0) dma_rs(rp, S + kLdsRing + 64 * kRow, o);   // (the mirror of row 0)
+                const int64_t x0 = A + 128ll * (h ? hb1 : hb0);
+                // a block wholly outside the packed bytes holds no stream data: any readable bytes will do
+                const bool part = x0 >= 0 && x0 < readable && x0 + 128 > readable;
+                const uint8_t* g = packed + (x0 < 0 || x0 >= readable ? 0 : x0);
+                if ((req & (1 << h)) && !part) {
+#pragma unroll
+                    for (int k = 0; k < 32; k++) dma_row(g + 4 * k, S + kLdsRing + (h * 32 + k) * kRow);
+                    if (h == 0) dma_row(g, S + kLdsRing + 64 * kRow);   // (the mirror of row 0)
+                }
+                if (ballot((req & (1 << h)) && part)) {   // (the packed bytes end inside the block)
+                    if ((req & (1 << h)) && part) {
+                        for (int k = 0; k < 32; k++)
+                            dma_row(packed + (x0 + 4 * k < readable - 4 ? x0 + 4 * k : ((readable - 4) & ~3ll)), S + kLdsRing + (h * 32 + k) * kRow);
+                        if (h == 0) dma_row(packed + x0, S + kLdsRing + 64 * kRow);
+                    }
+                }
+                if (req & (1 << h)) {
                     req &= ~(1 << h);
                     iss |= 1 << h;
                 }
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        // the records buffered during the last interval, after the fills: exactly kSB stores a point
-        // (a lane without a record j writes a dummy word), so that the next point's vmcnt(kSB) waits
-        // for the fills and not for these
-#pragma unroll
-        for (int j = 0; j < kSB; j++) *(j < nbuf ? seqs + sfl + j : dummy + lane) = recv[j];
-        sfl += nbuf;
-        nbuf = 0;
         // the lowest position a step may start from: the ready blocks below the reader + 90 bits
         lowok = (rdy == 3 ? 1024 * min(hb0, hb1) : (rdy == 1 ? 1024 * hb0 : (rdy == 2 ? 1024 * hb1 : (1 << 30)))) + 90;
         if (phase != 2) lowok = 1 << 30;
@@ -2493,86 +2454,91 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
             if (phase != 3) { res = kLegacy; phase = 3; }   // the one-wave decoder)
             lowok = 1 << 30;
         }
-        // ---- kSB steps
+        // ---- kSB steps: each stores exactly one record per lane (a dummy word for a lane without one),
+        // so that the next point's vmcnt(kSB) waits for this point's fills and not for these stores
         for (int k = 0; k < kSB; k++) {
-            if (P < lowok) continue;
-            const uint32_t eL = *(const LDSA uint32_t*)(S + sLL * kRow + lo4);
-            const uint32_t eM = *(const LDSA uint32_t*)(S + kLdsML + sML * kRow + lo4);
-            const uint32_t eO = *(const LDSA uint16_t*)(S + kLdsOF + (sOF >> 1) * kRow + lo4 + (sOF & 1) * 2);
-            const int ofc = (int)(eO >> 9);
-            const uint32_t eOx = eO & 511u;
-            const int no = (int)__builtin_ctz(eOx);
-            const int am = (int)__builtin_amdgcn_ubfe(eM, 13u, 5u), al = (int)__builtin_amdgcn_ubfe(eL, 13u, 5u);
-            const int nl = (int)__builtin_amdgcn_ubfe(eL, 9u, 4u), nm = (int)__builtin_amdgcn_ubfe(eM, 9u, 4u);
-            const int ns = nl + nm + no;
-            const bool lastq = i + 1 == nseq;
-            // the fields: offset extra bits, ML extra bits, LL extra bits, LL / ML / OF state bits
-            const int P1 = P - ofc, P2 = P1 - am, P3 = P2 - al, P4 = P3 - (lastq ? 0 : ns);
-            // (the eight ring loads issued together, then used: the scheduler would wait after each pair)
-            const LDSA uint8_t* a1 = S + kLdsRing + ((P1 >> 5) & 63) * kRow + lo4;
-            const LDSA uint8_t* a2 = S + kLdsRing + ((P2 >> 5) & 63) * kRow + lo4;
-            const LDSA uint8_t* a3 = S + kLdsRing + ((P3 >> 5) & 63) * kRow + lo4;
-            const LDSA uint8_t* a4 = S + kLdsRing + ((P4 >> 5) & 63) * kRow + lo4;
-            const uint32_t w1l = *(const LDSA uint32_t*)a1, w1h = *(const LDSA uint32_t*)(a1 + kRow);
-            const uint32_t w2l = *(const LDSA uint32_t*)a2, w2h = *(const LDSA uint32_t*)(a2 + kRow);
-            const uint32_t w3l = *(const LDSA uint32_t*)a3, w3h = *(const LDSA uint32_t*)(a3 + kRow);
-            const uint32_t w4l = *(const LDSA uint32_t*)a4, w4h = *(const LDSA uint32_t*)(a4 + kRow);
-            __builtin_amdgcn_sched_barrier(0);
-            const uint32_t ob = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w1h, w1l, (uint32_t)P1 & 31u), 0u, (uint32_t)ofc);
-            const uint32_t mb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w2h, w2l, (uint32_t)P2 & 31u), 0u, (uint32_t)am);
-            const uint32_t lb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w3h, w3l, (uint32_t)P3 & 31u), 0u, (uint32_t)al);
-            const uint32_t sb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w4h, w4l, (uint32_t)P4 & 31u), 0u,
-                                                      (uint32_t)(lastq ? 0 : ns));
-            const int ml = (int)(eM >> 19) + (((eM >> 18) & 1u) ? (1 << am) : 0) + (int)mb;
-            const int ll = (int)(eL >> 19) + (((eL >> 18) & 1u) ? (1 << al) : 0) + (int)lb;
-            // repcodes (ZSTD_decodeSequence): ofc > 1 a new offset; else repcode j = ofc + ll0 + bit
-            // (selects on lane masks: the compiler would branch on them)
-            const bool big = ofc > 1;
-            const int j = ofc + (int)((eL >> 18) == 0) + (int)ob;
-            int t = vsel(j == 0, rep0, vsel(j == 1, rep1, vsel(j == 2, rep2, rep0 - 1)));
-            t += t == 0;
-            const int off = vsel(big, (int)((1u << ofc) - 3u + ob), t);
-            const int nrep1 = vsel(big | (j >= 1), rep0, rep1);
-            rep2 = vsel(big | (j >= 2), rep1, rep2);
-            rep1 = nrep1;
-            rep0 = off;
-            sLL = (eL & 511u) + (sb >> (nm + no));
-            sML = (eM & 511u) + __builtin_amdgcn_ubfe(sb, (uint32_t)no, (uint32_t)nm);
-            sOF = ((eOx - (1u << no)) >> 1) + __builtin_amdgcn_ubfe(sb, 0u, (uint32_t)no);
-            P = P4;
-            // the reference updates the states after the last sequence too and accepts an exhausted
-            // or overrun stream there (ZSTD_decompressSequences_body: reload >= completed); then the
-            // checks of ZSTD_execSequence, and the layout's limits (else the one-wave decoder decodes)
-            const int lrem = rs - lp;
-            const bool bad = (P < lo) | (lastq & (P - lo > ns)) | (ll > lrem) | ((uint32_t)off > (uint32_t)(op + ll)) |
-                             (op + ll + ml > n - (lrem - ll));
-            const bool lim17 = ((ll | ml) >= (1 << kLenBits)) | (sfl + nbuf >= smax);
-            {
-                volatile LDSA uint32_t* q = (volatile LDSA uint32_t*)(S + kLdsSB + (nbuf * kFPW + lane) * 8);
-                q[0] = (uint32_t)ll | ((uint32_t)ml << kLenBits);
-                q[1] = ((uint32_t)ml >> (32 - kLenBits)) | ((uint32_t)off << (2 * kLenBits - 32));
-            }
-            nbuf++;
-            lp += ll;
-            op += ll + ml;
-            i++;
-            if (bad | lim17 | lastq) {   // an error, a limit, or the block's end (its last literals)
-                const int rem = rs - lp;
-                if (!(bad | lim17) && rem > n - op) res = ZC;
-                if (bad | lim17) {
-                    res = bad ? ZC : kLegacy;
-                    phase = 3;
-                } else {
-                    op += rem;
-                    phase = 0;
+            const bool act = P >= lowok;
+            uint32_t r0 = 0, r1 = 0;
+            bool keep = false;
+            if (act) {
+                const uint32_t eL = *(const LDSA uint32_t*)(S + sLL * kRow + lo4);
+                const uint32_t eM = *(const LDSA uint32_t*)(S + kLdsML + sML * kRow + lo4);
+                const uint32_t eO = *(const LDSA uint16_t*)(S + kLdsOF + (sOF >> 1) * kRow + lo4 + (sOF & 1) * 2);
+                const int ofc = (int)(eO >> 9);
+                const uint32_t eOx = eO & 511u;
+                const int no = (int)__builtin_ctz(eOx);
+                const int am = (int)__builtin_amdgcn_ubfe(eM, 13u, 5u), al = (int)__builtin_amdgcn_ubfe(eL, 13u, 5u);
+                const int nl = (int)__builtin_amdgcn_ubfe(eL, 9u, 4u), nm = (int)__builtin_amdgcn_ubfe(eM, 9u, 4u);
+                const int ns = nl + nm + no;
+                const bool lastq = i + 1 == nseq;
+                // the fields: offset extra bits, ML extra bits, LL extra bits, LL / ML / OF state bits
+                const int P1 = P - ofc, P2 = P1 - am, P3 = P2 - al, P4 = P3 - (lastq ? 0 : ns);
+                // (the eight ring loads issued together, then used: the scheduler would wait after each pair)
+                const LDSA uint8_t* a1 = S + kLdsRing + ((P1 >> 5) & 63) * kRow + lo4;
+                const LDSA uint8_t* a2 = S + kLdsRing + ((P2 >> 5) & 63) * kRow + lo4;
+                const LDSA uint8_t* a3 = S + kLdsRing + ((P3 >> 5) & 63) * kRow + lo4;
+                const LDSA uint8_t* a4 = S + kLdsRing + ((P4 >> 5) & 63) * kRow + lo4;
+                const uint32_t w1l = *(const LDSA uint32_t*)a1, w1h = *(const LDSA uint32_t*)(a1 + kRow);
+                const uint32_t w2l = *(const LDSA uint32_t*)a2, w2h = *(const LDSA uint32_t*)(a2 + kRow);
+                const uint32_t w3l = *(const LDSA uint32_t*)a3, w3h = *(const LDSA uint32_t*)(a3 + kRow);
+                const uint32_t w4l = *(const LDSA uint32_t*)a4, w4h = *(const LDSA uint32_t*)(a4 + kRow);
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t ob = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w1h, w1l, (uint32_t)P1 & 31u), 0u, (uint32_t)ofc);
+                const uint32_t mb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w2h, w2l, (uint32_t)P2 & 31u), 0u, (uint32_t)am);
+                const uint32_t lb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w3h, w3l, (uint32_t)P3 & 31u), 0u, (uint32_t)al);
+                const uint32_t sb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w4h, w4l, (uint32_t)P4 & 31u), 0u,
+                                                          (uint32_t)(lastq ? 0 : ns));
+                const int ml = (int)(eM >> 19) + (((eM >> 18) & 1u) ? (1 << am) : 0) + (int)mb;
+                const int ll = (int)(eL >> 19) + (((eL >> 18) & 1u) ? (1 << al) : 0) + (int)lb;
+                // repcodes (ZSTD_decodeSequence): ofc > 1 a new offset; else repcode j = ofc + ll0 + bit
+                // (selects on lane masks: the compiler would branch on them)
+                const bool big = ofc > 1;
+                const int j = ofc + (int)((eL >> 18) == 0) + (int)ob;
+                int t = vsel(j == 0, rep0, vsel(j == 1, rep1, vsel(j == 2, rep2, rep0 - 1)));
+                t += t == 0;
+                const int off = vsel(big, (int)((1u << ofc) - 3u + ob), t);
+                const int nrep1 = vsel(big | (j >= 1), rep0, rep1);
+                rep2 = vsel(big | (j >= 2), rep1, rep2);
+                rep1 = nrep1;
+                rep0 = off;
+                sLL = (eL & 511u) + (sb >> (nm + no));
+                sML = (eM & 511u) + __builtin_amdgcn_ubfe(sb, (uint32_t)no, (uint32_t)nm);
+                sOF = ((eOx - (1u << no)) >> 1) + __builtin_amdgcn_ubfe(sb, 0u, (uint32_t)no);
+                P = P4;
+                // the reference updates the states after the last sequence too and accepts an exhausted
+                // or overrun stream there (ZSTD_decompressSequences_body: reload >= completed); then the
+                // checks of ZSTD_execSequence, and the layout's limits (else the one-wave decoder decodes)
+                const int lrem = rs - lp;
+                const bool bad = (P < lo) | (lastq & (P - lo > ns)) | (ll > lrem) | ((uint32_t)off > (uint32_t)(op + ll)) |
+                                 (op + ll + ml > n - (lrem - ll));
+                const bool lim17 = ((ll | ml) >= (1 << kLenBits)) | (sfl >= smax);
+                r0 = (uint32_t)ll | ((uint32_t)ml << kLenBits);
+                r1 = ((uint32_t)ml >> (32 - kLenBits)) | ((uint32_t)off << (2 * kLenBits - 32));
+                keep = !(bad | lim17);
+                lp += ll;
+                op += ll + ml;
+                i++;
+                if (bad | lim17 | lastq) {   // an error, a limit, or the block's end (its last literals)
+                    const int rem = rs - lp;
+                    if (!(bad | lim17) && rem > n - op) res = ZC;
+                    if (bad | lim17) {
+                        res = bad ? ZC : kLegacy;
+                        phase = 3;
+                    } else {
+                        op += rem;
+                        phase = 0;
+                    }
+                    lowok = 1 << 30;
                 }
-                lowok = 1 << 30;
+                if (LZH_ZSTD_STATS) sst[4]++;
             }
-            if (LZH_ZSTD_STATS) sst[4]++;
+            *(keep ? seqs + sfl : dummy + lane) = (uint64_t)r0 | ((uint64_t)r1 << 32);
+            sfl += keep;
         }
     }
     if (LZH_ZSTD_STATS && stats && lane == 0)
         for (int k = 0; k < 6; k++) atomicAdd(&stats[k], (unsigned long long)sst[k]);
+    if (LZH_ZSTD_STATS && stats && live && res == kLegacy) atomicAdd(&stats[6], 1ull);
     if (live) {
         if (res == kLegacy) {
             zst[f] = kLegacy;
@@ -2712,13 +2678,13 @@ namespace zsplit {
 constexpr int kHJ = 4, kHL = 4 * kHJ;            // sections a wave, lanes in use
 constexpr int kHRow = 4 * kHL;                   // 64 bytes
 constexpr int kHB = 16;                          // steps between uniform points (= bytes staged per lane)
-constexpr int kHLdsRing = 256 * kHRow, kHLdsStage = kHLdsRing + 33 * kHRow, kHLds = kHLdsStage + kHL * kHB;
+constexpr int kHLdsRing = 256 * kHRow, kHLds = kHLdsRing + 33 * kHRow;
 }  // namespace zsplit
 
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t n_total,
                     uint64_t chunk_size, uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst,
-                    const zsplit::ZHuf* jobs, const uint32_t* njobs) {
+                    const zsplit::ZHuf* jobs, const uint32_t* njobs, unsigned long long* stats) {
     using namespace zsplit;
     using namespace zstdd;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kHLds];
@@ -2750,7 +2716,7 @@ lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     const int l4 = lane * 4;
     const int tl = (int)jtl;
     // this lane's stream
-    int P = 0, lo = 0, nsym = 0, done = 0, flushed = 0;
+    int P = 0, lo = 0, nsym = 0, done = 0;
     int64_t A = 0;
     uint8_t* dst = out;
     if (slive) {
@@ -2778,110 +2744,104 @@ lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
             slive = slive && !qfar;
         }
     }
-    bool tdone = false;
     int res = 0;                                  // 0 going, 1 exact, 2 not exact
     auto fld = [&](int bq, int w) -> uint32_t {
         const LDSA uint8_t* a = S + kHLdsRing + ((bq >> 5) & 31) * kHRow + l4;
-        const uint32_t v = __builtin_amdgcn_alignbit(*(const volatile LDSA uint32_t*)(a + kHRow),
-                                                     *(const volatile LDSA uint32_t*)a, (uint32_t)bq & 31u);
+        const uint32_t v = __builtin_amdgcn_alignbit(*(const LDSA uint32_t*)(a + kHRow), *(const LDSA uint32_t*)a,
+                                                     (uint32_t)bq & 31u);
         return __builtin_amdgcn_ubfe(v, 0u, (uint32_t)w);
     };
     if (!slive) req = 0;
     bool going = slive;
+    int lowok = 1 << 30;                         // a step runs while P >= lowok (the ready blocks + tl bits)
+    uint64_t hst[5] = {0, 0, 0, 0, 0}, tmark = 0;   // (LZH_ZSTD_STATS: points, steps, intervals, waits, symbols)
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-    for (int step = 0;; step++) {
-        if ((step & (kHB - 1)) == 0) {
-            // every memory operation but the previous point's kHB byte stores (issued after its fills) is done
-            __builtin_amdgcn_s_waitcnt(vmcnt_imm(kHB));
-            const int nb = done - flushed;
-            const uint32_t w0 = *(const LDSA uint32_t*)(S + kHLdsStage + lane * kHB),
-                           w1 = *(const LDSA uint32_t*)(S + kHLdsStage + lane * kHB + 4),
-                           w2 = *(const LDSA uint32_t*)(S + kHLdsStage + lane * kHB + 8),
-                           w3 = *(const LDSA uint32_t*)(S + kHLdsStage + lane * kHB + 12);
-            rdy |= iss;
-            iss = 0;
-            if (!tdone && ballot(jlive)) {   // (step 0) the sections' tables: row r = dwords 4r .. 4r+3
-                if (jlive) {
-                    const uint32_t o = (uint32_t)toff + 4 * j;
-                    for (int r = 0; r < 256; r += 16) {
-                        LDSA uint8_t* d = S + r * kHRow;
-                        const uint32_t orr = o + 16 * r;
-                        dma_rs(rz, d, orr); dma_rs(rz, d + kHRow, orr + 16); dma_rs(rz, d + 2 * kHRow, orr + 32);
-                        dma_rs(rz, d + 3 * kHRow, orr + 48); dma_rs(rz, d + 4 * kHRow, orr + 64);
-                        dma_rs(rz, d + 5 * kHRow, orr + 80); dma_rs(rz, d + 6 * kHRow, orr + 96);
-                        dma_rs(rz, d + 7 * kHRow, orr + 112); dma_rs(rz, d + 8 * kHRow, orr + 128);
-                        dma_rs(rz, d + 9 * kHRow, orr + 144); dma_rs(rz, d + 10 * kHRow, orr + 160);
-                        dma_rs(rz, d + 11 * kHRow, orr + 176); dma_rs(rz, d + 12 * kHRow, orr + 192);
-                        dma_rs(rz, d + 13 * kHRow, orr + 208); dma_rs(rz, d + 14 * kHRow, orr + 224);
-                        dma_rs(rz, d + 15 * kHRow, orr + 240);
-                    }
-                }
-                tdone = true;
-            }
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                if (ballot(req & (1 << h))) {
-                    if (req & (1 << h)) {   // the block's 16 dwords (offsets below the resource read 0)
-                        const uint32_t o = (uint32_t)(A - (int64_t)pbase + 64ll * (h ? hb1 : hb0));
-                        LDSA uint8_t* d = S + kHLdsRing + h * 16 * kHRow;
-                        dma_rs(rp, d, o); dma_rs(rp, d + kHRow, o + 4); dma_rs(rp, d + 2 * kHRow, o + 8);
-                        dma_rs(rp, d + 3 * kHRow, o + 12); dma_rs(rp, d + 4 * kHRow, o + 16);
-                        dma_rs(rp, d + 5 * kHRow, o + 20); dma_rs(rp, d + 6 * kHRow, o + 24);
-                        dma_rs(rp, d + 7 * kHRow, o + 28); dma_rs(rp, d + 8 * kHRow, o + 32);
-                        dma_rs(rp, d + 9 * kHRow, o + 36); dma_rs(rp, d + 10 * kHRow, o + 40);
-                        dma_rs(rp, d + 11 * kHRow, o + 44); dma_rs(rp, d + 12 * kHRow, o + 48);
-                        dma_rs(rp, d + 13 * kHRow, o + 52); dma_rs(rp, d + 14 * kHRow, o + 56);
-                        dma_rs(rp, d + 15 * kHRow, o + 60);
-                        if (h == 0) dma_rs(rp, S + kHLdsRing + 32 * kHRow, o);   // (the mirror of row 0)
-                        req &= ~(1 << h);
-                        iss |= 1 << h;
-                    }
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            {   // the staged bytes out, after the fills: exactly kHB byte stores a point (a lane without a
-                // byte t writes a dummy one), so that the next point's vmcnt(kHB) waits for the fills only
-                const int r = flushed & (kHB - 1);
-#pragma unroll
-                for (int k = 0; k < kHB; k++) {
-                    const int sl = (r + k) & (kHB - 1);
-                    const uint32_t w = sl < 4 ? w0 : (sl < 8 ? w1 : (sl < 12 ? w2 : w3));
-                    *(k < nb ? dst + flushed + k : dummy + lane) = (uint8_t)(w >> (8 * (sl & 3)));
-                }
-                flushed = done;
-            }
-            if (!ballot(going || done != flushed)) break;
-            if (step > 16 * kBlockMax) {   // (a bound every stream meets)
-                if (going) { going = false; res = 2; }
-            }
+    for (int ival = 0;; ival++) {
+        if (LZH_ZSTD_STATS) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (ival) hst[1] += t - tmark;
+            tmark = t;
+            hst[2]++;
         }
-        if (!going || step < kHB) continue;      // (tables and rings land at the first point after step 0)
-        {   // skip the step while the lowest bit of the lookup is in a block not ready
-            const int bm = (P - 12) >> 9;
-            const bool ok = (bm & 1) ? (hb1 == bm && (rdy & 2)) : (hb0 == bm && (rdy & 1));
-            if (!ok) continue;
-        }
-        if (done == nsym) {                      // huf_streams' verdict: exactly consumed
+        // ---- uniform point: every memory operation but the last interval's kHB byte stores is done
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(kHB));
+        if (LZH_ZSTD_STATS) hst[3] += __builtin_amdgcn_s_memtime() - tmark;
+        rdy |= iss;
+        iss = 0;
+        if (going && done == nsym) {             // huf_streams' verdict: exactly consumed
             res = P == lo ? 1 : 2;
             going = false;
-            continue;
         }
-        const int bq = P - tl;
-        uint32_t v = fld(bq, tl);
-        if (bq < lo) v &= lo - bq >= 32 ? 0u : (~0u << (lo - bq));   // (zero-padded below the start)
-        const uint32_t e = *(const volatile LDSA uint16_t*)(S + ((v >> 3) << 6) + (q << 4) + (v & 7) * 2);
-        P -= (int)(e >> 8);
-        *(volatile LDSA uint8_t*)(S + kHLdsStage + lane * kHB + (done & (kHB - 1))) = (uint8_t)e;
-        done++;
-        {   // the upper block, once the reader is below it, takes the block under the lower one
+        if (going) {   // the upper block, once the reader is below it, takes the block under the lower one
             const int top = (P - 1) >> 9;
-            const bool r0 = (rdy & 1) != 0 && hb0 > top && hb0 > hb1, r1 = (rdy & 2) != 0 && hb1 > top && hb1 > hb0;
-            hb0 = vsel(r0, hb1 - 1, hb0);
-            hb1 = vsel(r1, hb0 - 1, hb1);
-            rdy &= ~(int)(r0 | ((int)r1 << 1));
-            req |= (int)r0 | ((int)r1 << 1);
+            if ((rdy & 1) && hb0 > top && hb0 > hb1) { hb0 = hb1 - 1; rdy &= ~1; req |= 1; }
+            if ((rdy & 2) && hb1 > top && hb1 > hb0) { hb1 = hb0 - 1; rdy &= ~2; req |= 2; }
+        }
+        if (ival == 0 && ballot(jlive)) {   // the sections' tables: row r = dwords 4r .. 4r+3
+            if (jlive) {
+                const uint32_t o = (uint32_t)toff + 4 * j;
+#pragma unroll 1
+                for (int r = 0; r < 256; r += 16) {
+                    LDSA uint8_t* d = S + r * kHRow;
+                    const uint32_t orr = o + 16 * r;
+                    dma_rs(rz, d, orr); dma_rs(rz, d + kHRow, orr + 16); dma_rs(rz, d + 2 * kHRow, orr + 32);
+                    dma_rs(rz, d + 3 * kHRow, orr + 48); dma_rs(rz, d + 4 * kHRow, orr + 64);
+                    dma_rs(rz, d + 5 * kHRow, orr + 80); dma_rs(rz, d + 6 * kHRow, orr + 96);
+                    dma_rs(rz, d + 7 * kHRow, orr + 112); dma_rs(rz, d + 8 * kHRow, orr + 128);
+                    dma_rs(rz, d + 9 * kHRow, orr + 144); dma_rs(rz, d + 10 * kHRow, orr + 160);
+                    dma_rs(rz, d + 11 * kHRow, orr + 176); dma_rs(rz, d + 12 * kHRow, orr + 192);
+                    dma_rs(rz, d + 13 * kHRow, orr + 208); dma_rs(rz, d + 14 * kHRow, orr + 224);
+                    dma_rs(rz, d + 15 * kHRow, orr + 240);
+                }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            if (ballot(req & (1 << h))) {
+                if (req & (1 << h)) {   // the block's 16 dwords (offsets below the resource read 0)
+                    const uint32_t o = (uint32_t)(A - (int64_t)pbase + 64ll * (h ? hb1 : hb0));
+                    LDSA uint8_t* d = S + kHLdsRing + h * 16 * kHRow;
+#pragma unroll
+                    for (int k = 0; k < 16; k++) dma_rs(rp, d + k * kHRow, o + 4 * k);
+                    if (h == 0) dma_rs(rp, S + kHLdsRing + 32 * kHRow, o);   // (the mirror of row 0)
+                    req &= ~(1 << h);
+                    iss |= 1 << h;
+                }
+            }
+        }
+        lowok = (rdy == 3 ? 512 * min(hb0, hb1) : (rdy == 1 ? 512 * hb0 : (rdy == 2 ? 512 * hb1 : (1 << 30)))) + 12;
+        if (!going) lowok = 1 << 30;
+        if (LZH_ZSTD_STATS) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            hst[0] += t - tmark;
+            tmark = t;
+        }
+        if (!ballot(going)) break;
+        if (ival > 2 * kBlockMax) {   // (a bound every stream meets)
+            if (going) { going = false; res = 2; }
+            lowok = 1 << 30;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- kHB steps, one symbol each (HUF_decodeSymbolX1) and exactly one byte store per lane (a dummy
+        // byte for a lane without a symbol), so that the next point's vmcnt(kHB) waits for the fills only
+#pragma unroll 2
+        for (int k = 0; k < kHB; k++) {
+            const bool act = P >= lowok && done < nsym;
+            const int bq = P - tl;
+            uint32_t v = fld(bq, tl);
+            if (bq < lo) v &= lo - bq >= 32 ? 0u : (~0u << (lo - bq));   // (zero-padded below the start)
+            const uint32_t e = *(const LDSA uint16_t*)(S + ((v >> 3) << 6) + (q << 4) + (v & 7) * 2);
+            *(act ? dst + done : dummy + lane) = (uint8_t)e;
+            P -= act ? (int)(e >> 8) : 0;
+            done += act;
         }
     }
+    if (LZH_ZSTD_STATS && stats && lane == 0) {
+        for (int k = 0; k < 4; k++) atomicAdd(&stats[k], (unsigned long long)hst[k]);
+    }
+    if (LZH_ZSTD_STATS && stats && slive) atomicAdd(&stats[4], (unsigned long long)nsym);
+    if (LZH_ZSTD_STATS && stats && slive && res == 2) atomicAdd(&stats[5 + (int)jx2], 1ull);
+    if (LZH_ZSTD_STATS && stats && far_) atomicAdd(&stats[7], 1ull);
     if (slive && res == 2) {   // not consumed exactly: X2's verdict (the one-wave decoder) or corrupt
         if (jx2) {
             atomicMax(&zst[jf], kLegacy);
@@ -3022,9 +2982,31 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         hipLaunchKernelGGL(lzh_zstd_hdr_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
                            n_total, chunk_size, out, status, zt, zst, zfr, stats, jobs, njobs);
         const uint64_t maxjobs = (uint64_t)nchunks * Z.bmax;
+        unsigned long long* hstats = nullptr;
+#if LZH_ZSTD_STATS
+        static unsigned long long* d_hst = nullptr;
+        if (!d_hst) (void)hipMalloc(&d_hst, 8 * sizeof(unsigned long long));
+        (void)hipMemsetAsync(d_hst, 0, 8 * sizeof(unsigned long long), s);
+        hstats = d_hst;
+#endif
         hipLaunchKernelGGL(lzh_zstd_huf_kernel, dim3((unsigned)((maxjobs + zsplit::kHJ - 1) / zsplit::kHJ)), dim3(64), 0, s,
                            packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst,
-                           (const zsplit::ZHuf*)jobs, (const uint32_t*)njobs);
+                           (const zsplit::ZHuf*)jobs, (const uint32_t*)njobs, hstats);
+#if LZH_ZSTD_STATS
+        {
+            unsigned long long h[8];
+            uint32_t nj = 0;
+            (void)hipMemcpyAsync(h, d_hst, sizeof(h), hipMemcpyDeviceToHost, s);
+            (void)hipMemcpyAsync(&nj, njobs, 4, hipMemcpyDeviceToHost, s);
+            (void)hipStreamSynchronize(s);
+            const double w = (double)((nj + zsplit::kHJ - 1) / zsplit::kHJ);
+            fprintf(stderr, "zstd huf kernel: %u sections, %.0f symbols a stream; per wave: intervals %.0f; clocks per "
+                            "interval: uniform point %.0f (its wait %.0f), steps %.0f; inexact streams %llu (x1) %llu (x2), "
+                            "far %llu\n",
+                    nj, (double)h[4] / (nj ? 4.0 * nj : 1.0), h[2] / (w ? w : 1), (double)h[0] / (h[2] ? h[2] : 1),
+                    (double)h[3] / (h[2] ? h[2] : 1), (double)h[1] / (h[2] ? h[2] : 1), h[5], h[6], h[7]);
+        }
+#endif
         unsigned long long* sstats = nullptr;
 #if LZH_ZSTD_STATS
         static unsigned long long* d_sst = nullptr;
@@ -3041,8 +3023,8 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
             (void)hipStreamSynchronize(s);
             const double w = (double)((nchunks + zsplit::kFPW - 1) / zsplit::kFPW);
             fprintf(stderr, "zstd seq kernel per wave: intervals %.0f (with block starts %.0f), steps %.0f; clocks per "
-                            "interval: uniform point %.0f, steps %.0f\n",
-                    h[2] / w, h[3] / w, h[4] / w, (double)h[0] / h[2], (double)h[1] / h[2]);
+                            "interval: uniform point %.0f (its wait %.0f), steps %.0f; frames to the one-wave decoder %llu\n",
+                    h[2] / w, h[3] / w, h[4] / w, (double)h[0] / h[2], (double)h[5] / h[2], (double)h[1] / h[2], h[6]);
         }
 #endif
         hipLaunchKernelGGL(lzh_zstd_exec_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
