@@ -2706,8 +2706,7 @@ lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     uint32_t fmin = jlive ? jf : 0xffffffffu;
     for (int k = 1; k < 64; k <<= 1) fmin = min(fmin, (uint32_t)__shfl_xor((int)fmin, k));
     fmin = uni(fmin == 0xffffffffu ? 0u : fmin);
-    const uint64_t pbase = offsets[fmin] & ~3ull;
-    const rsrc_t rp = rsrc_over(packed + pbase, packed_readable > pbase ? packed_readable - pbase : 0);
+    const int64_t readable = (int64_t)packed_readable;
     const uint8_t* zb0 = zt + (uint64_t)fmin * Z.stride;
     const rsrc_t rz = rsrc_over(zb0, (uint64_t)0xffffffffull);
     const uint64_t toff = (uint64_t)(jf - fmin) * Z.stride + Z.hufs() + (uint64_t)jtblk * kHufSlot;
@@ -2722,7 +2721,7 @@ lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     if (slive) {
         const int64_t s0 = (int64_t)offsets[jf] + (int64_t)js0;
         A = s0 & ~3ll;
-        far_ |= A - (int64_t)pbase + (int64_t)jsz + 256 > 0xffffffffll;
+
         const int x0 = (int)(s0 & 3), X = x0 + (int)jsz - 1;
         lo = 8 * x0;
         P = 8 * X + hb32((uint32_t)packed[A + X]);   // (the end mark: checked non-zero by the header kernel)
@@ -2797,13 +2796,25 @@ lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
         }
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-            if (ballot(req & (1 << h))) {
-                if (req & (1 << h)) {   // the block's 16 dwords (offsets below the resource read 0)
-                    const uint32_t o = (uint32_t)(A - (int64_t)pbase + 64ll * (h ? hb1 : hb0));
-                    LDSA uint8_t* d = S + kHLdsRing + h * 16 * kHRow;
+            if (ballot(req & (1 << h))) {   // the block's 16 dwords (global_load_lds rows: see the sequence kernel)
+                const int64_t x0 = A + 64ll * (h ? hb1 : hb0);
+                // a block wholly outside the packed bytes holds no stream data: any readable bytes will do
+                const bool part = x0 >= 0 && x0 < readable && x0 + 64 > readable;
+                const uint8_t* g = packed + (x0 < 0 || x0 >= readable ? 0 : x0);
+                LDSA uint8_t* d = S + kHLdsRing + h * 16 * kHRow;
+                if ((req & (1 << h)) && !part) {
 #pragma unroll
-                    for (int k = 0; k < 16; k++) dma_rs(rp, d + k * kHRow, o + 4 * k);
-                    if (h == 0) dma_rs(rp, S + kHLdsRing + 32 * kHRow, o);   // (the mirror of row 0)
+                    for (int k = 0; k < 16; k++) dma_row(g + 4 * k, d + k * kHRow);
+                    if (h == 0) dma_row(g, S + kHLdsRing + 32 * kHRow);   // (the mirror of row 0)
+                }
+                if (ballot((req & (1 << h)) && part)) {   // (the packed bytes end inside the block)
+                    if ((req & (1 << h)) && part) {
+                        for (int k = 0; k < 16; k++)
+                            dma_row(packed + (x0 + 4 * k < readable - 4 ? x0 + 4 * k : ((readable - 4) & ~3ll)), d + k * kHRow);
+                        if (h == 0) dma_row(packed + x0, S + kHLdsRing + 32 * kHRow);
+                    }
+                }
+                if (req & (1 << h)) {
                     req &= ~(1 << h);
                     iss |= 1 << h;
                 }
