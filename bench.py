@@ -50,7 +50,9 @@ BASELINE_METRIC = "comp+decomp MB/s, lz4 -b64 on 1 GiB; ratio + bit-exact vs CPU
 COMPRESS_KERNEL = {"lz4": "lzh_lz4_parse_kernel", "lz4fast": "lzh_lz4_parse_kernel",
                    "snappy": "lzh_snappy_parse_kernel",
                    "zstd": "lzh_zstd_match_kernel+lzh_zstd_entropy_kernel"}
-DECOMPRESS_KERNEL = {"zstd": "lzh_zstd_decompress_kernel"}
+# (zstd decodes in four kernels, and frames the split layout does not fit in a fifth: the stage)
+DECOMPRESS_KERNEL = {"zstd": "lzh_zstd_hdr_kernel+lzh_zstd_huf_kernel+lzh_zstd_seq_kernel+lzh_zstd_exec_kernel"
+                             "+lzh_zstd_decompress_kernel"}
 
 
 def log(*a):
@@ -140,8 +142,12 @@ def traffic_for(kernel, workload):
                 t = json.load(f)
             if t.get("workload_key") != workload:
                 continue
-            k = t["kernels"].get(kernel)
-            return None if k is None else int(k["traffic_bytes_per_dispatch"])
+            # a stage of several kernels ("a+b"): the sum over the kernels the profile holds (a kernel
+            # no dispatch of which ran in the profiled pass has no entry and contributes nothing)
+            parts = [t["kernels"].get(k) for k in kernel.split("+")]
+            if all(p is None for p in parts):
+                return None
+            return int(sum(p["traffic_bytes_per_dispatch"] for p in parts if p is not None))
         except (OSError, KeyError, ValueError):
             continue
     return None
