@@ -1279,6 +1279,49 @@ struct OutR {
     }
 };
 
+// One group of 64 records: its header (sequences before catch-up; the literals of a record run from
+// the previous record's match end, lane-1 by a wave shift, the previous group's end for lane 0).
+// Its loads -- the dwords under the catch-up words before the match and its candidate, and the
+// group's input span [ia, ia + Lt) -- go into the caller's registers, issued a group ahead of use,
+// unconditionally (out-of-range buffer reads return 0): a load under a branch merges with the old
+// register value, and that copy would wait for the load.
+constexpr int kSpanW = kSpan / 256;     // span dwords per lane
+struct Grp {
+    int Pm = 0, mlx = 0, o = 0, anc = 0, lit = 0, ia = 0, Lt = 0, X0 = 0, nd = 0;
+    bool v = false, span = false;
+    __device__ __forceinline__ void head(uint32_t w0, uint32_t w1, int ia_, int g, int nrec, const Bytes& in, int lane) {
+        v = g + lane < nrec;
+        Pm = (int)(w0 & 0xFFFFFFu);
+        mlx = (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8));
+        o = (int)(w1 >> 16);
+        const int end = Pm + 4 + mlx;
+        ia = ia_;
+        anc = __builtin_amdgcn_update_dpp(ia_, end, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        lit = Pm - anc;
+        const int nv = max(min(64, nrec - g), 1);
+        Lt = __builtin_amdgcn_readlane(end, nv - 1) - ia_;
+        span = Lt + 8 <= kSpan;
+        X0 = (ia_ + in.sh) & ~3;
+        nd = (ia_ + in.sh + Lt - X0 + 3) >> 2;
+    }
+    // raw dwords: c[0..1] under bytes [Pm-4, Pm), c[2..3] under [M-4, M) (M = Pm - o), span words
+    __device__ __forceinline__ void issue(const Bytes& in, int lane, uint32_t* c, uint32_t* sp) const {
+        // (words nobody needs re-read the group's first span dword: no extra memory traffic)
+        const int a0 = X0 + 4 * lane;
+        const bool cu = v && min(lit, Pm - o) > 0;
+        const int xp = cu ? (max(Pm - 4, 0) + in.sh) & ~3 : a0, xm = cu ? (max(Pm - o - 4, 0) + in.sh) & ~3 : a0;
+        c[0] = ld_b32(in.r, xp); c[1] = ld_b32(in.r, xp + 4);
+        c[2] = ld_b32(in.r, xm); c[3] = ld_b32(in.r, xm + 4);
+#pragma unroll
+        for (int k = 0; k < kSpanW; k++) sp[k] = ld_b32(in.r, span && 64 * k < nd ? a0 + 256 * k : a0);
+    }
+    // the dword of bytes [p-4, p), byte p-1 most significant, bytes before 0 as 0 (u32_before)
+    __device__ __forceinline__ static uint32_t before(uint32_t lo, uint32_t hi, int p, int sh) {
+        const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(max(p - 4, 0) + sh) & 3u);
+        return p >= 4 ? w : (p <= 0 ? 0u : w << (8 * (4 - p)));
+    }
+};
+
 // bytes of one sequence (or the last literals: ml < 0) written by the whole wave through the ring
 __device__ void put_seq_wave(OutR& R, const Bytes& in, int op, int anchor, int lit, int off, int mlx, int lane) {
     const bool hm = mlx >= 0;
@@ -1314,7 +1357,12 @@ __device__ void put_seq_wave(OutR& R, const Bytes& in, int op, int anchor, int l
 
 }  // namespace lz4e
 
-extern "C" __global__ void __launch_bounds__(64)
+// (8 waves per SIMD: the group pipeline's registers fit 64 VGPRs without spills; left to itself the
+// compiler takes 66 and 7 waves)
+#ifndef LZH_EMIT_WAVES
+#define LZH_EMIT_WAVES 8
+#endif
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZH_EMIT_WAVES, 8)))
 lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                     const uint8_t* recs, uint64_t rec_stride, const uint32_t* rec_hdr, uint8_t* stage, uint64_t stride,
                     uint32_t* csizes, uint64_t frame_size, uint32_t bpf) {
@@ -1330,39 +1378,45 @@ lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, u
     const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
     const int nrec = (int)uni(rec_hdr[2 * chunk]);
     lz4e::OutR R{(LDSA uint8_t*)ring, make_rsrc(stage + chunk * stride, (uint32_t)stride), 0};
-    int op = 0, ia = 0;
-    uint32_t nw0 = 0, nw1 = 0;                 // records of the next group (loaded one group ahead)
-    if (lane < nrec) { nw0 = ld_b32(rr, 8 * lane); nw1 = ld_b32(rr, 8 * lane + 4); }
-    for (int g = 0; g < nrec; g += 64) {
-        const int r = g + lane;
-        const bool v = r < nrec;
-        const uint32_t w0 = nw0, w1 = nw1;
-        if (r + 64 < nrec) { nw0 = ld_b32(rr, 8 * (r + 64)); nw1 = ld_b32(rr, 8 * (r + 64) + 4); }
-        // records carry the sequence before catch-up (the parse kernel defers it): the match start
-        // P found by the search and the match length past P+4; the literals run from the previous
-        // record's match end (lane-1 by a wave shift; the previous group's end for lane 0)
-        const int Pm = (int)(w0 & 0xFFFFFFu);
-        int mlx = (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8));
-        const int o = (int)(w1 >> 16);
-        const int end = Pm + 4 + mlx;
-        const int anc = __builtin_amdgcn_update_dpp(ia, end, 0x138, 0xf, 0xf, false);   // wave_shr:1
-        int lit = Pm - anc;
-        const int nv = min(64, nrec - g);
-        const int Lt = rdlanei(end, nv - 1) - ia;
-        int T;
-        // the catch-up operands and the group's input span [ia, ia + Lt) (literal bytes are read
-        // from LDS) are loaded together: one memory wait per group
-        const int M = Pm - o;
-        const int maxb = min(lit, M);
-        uint32_t xp = 0, xm = 0;
-        if (v && maxb > 0) { xp = lz4e::u32_before(in_b, Pm); xm = lz4e::u32_before(in_b, M); }
-        const bool span = Lt + 8 <= lz4e::kSpan;
-        const int X0 = (ia + in_b.sh) & ~3;
-        if (span) {
-            const int nd = (ia + in_b.sh + Lt - X0 + 3) >> 2;
-            for (int d = lane; d < nd; d += 64) ibuf[d] = ld_b32(in_b.r, X0 + 4 * d);
+    // Software pipeline over groups of 64 records: while group g is laid out, the loads of group g+1
+    // (its input span and catch-up words) and the records of group g+2 are in flight, so a group's one
+    // memory wait comes a whole group after its loads were issued.
+    int op = 0, ia_end = 0;
+    lz4e::Grp GA, GB;                           // headers of groups g and g+1 (alternating roles)
+    uint32_t sp[lz4e::kSpanW], cw[4];           // group g's span and catch-up dwords (in flight)
+    // records of group g+1 (in flight), per lane; past nrec the offsets are out of range (0)
+    uint32_t nw0 = ld_b32(rr, 8 * (64 + lane)), nw1 = ld_b32(rr, 8 * (64 + lane) + 4);
+    {
+        const uint32_t w0 = ld_b32(rr, 8 * lane), w1 = ld_b32(rr, 8 * lane + 4);
+        GA.head(w0, w1, 0, 0, nrec, in_b, lane);
+        GA.issue(in_b, lane, cw, sp);
+    }
+    auto step = [&](lz4e::Grp& G, lz4e::Grp& Gn, int g) {
+        // group g's input span into LDS (literal bytes are read from it), its catch-up words
+        if (G.span) {
+#pragma unroll
+            for (int k = 0; k < lz4e::kSpanW; k++)
+                if (64 * k < G.nd && lane + 64 * k < G.nd) ibuf[lane + 64 * k] = sp[k];
             wave_lds_fence();
         }
+        const uint32_t xp = lz4e::Grp::before(cw[0], cw[1], G.Pm, in_b.sh);
+        const uint32_t xm = lz4e::Grp::before(cw[2], cw[3], G.Pm - G.o, in_b.sh);
+        // group g+1: header from its records; its loads and the records of group g+2 go out now
+        {
+            const uint32_t w0 = nw0, w1 = nw1;
+            nw0 = ld_b32(rr, 8 * (g + 128 + lane));
+            nw1 = ld_b32(rr, 8 * (g + 128 + lane) + 4);
+            Gn.head(w0, w1, G.ia + G.Lt, g + 64, nrec, in_b, lane);
+            Gn.issue(in_b, lane, cw, sp);
+        }
+        const bool v = G.v;
+        int lit = G.lit, mlx = G.mlx;
+        const int Pm = G.Pm, o = G.o, anc = G.anc, ia = G.ia, Lt = G.Lt;
+        const bool span = G.span;
+        const int X0 = G.X0;
+        int T;
+        const int M = Pm - o;
+        const int maxb = min(lit, M);
         if (v && maxb > 0) {   // catch-up (lz4.c:1017-1020): extend the match backwards while ip > anchor, match > start
             const uint32_t x = xp ^ xm;
             int bk = x ? (int)((uint32_t)__builtin_clz(x) >> 3) : 4;
@@ -1411,8 +1465,13 @@ lzh_lz4_emit_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, u
                 op += 3 + kl + lz4e::ext_len(kl) + lz4e::ext_len(km);
             }
         }
-        ia += Lt;
+        ia_end = ia + Lt;
+    };
+    for (int g = 0; g < nrec; g += 128) {
+        step(GA, GB, g);
+        if (g + 64 < nrec) step(GB, GA, g + 64);
     }
+    const int ia = ia_end;
     // last literals (lz4.c:1204-1231): everything after the last match, the whole chunk if none
     const int last = n - ia;
     if (op + 256 - R.flushed > lz4e::kRingB) R.flush(op, false, lane);

@@ -9,8 +9,14 @@ mkdir -p $out
 cd $root/lzbench_amd/csrc
 objs=""
 for f in lz4c_hip snappyc_hip decode_hip pack_hip zstdc_hip frame_hip; do
-  sf=""; { [ $f = lz4c_hip ] || [ $f = snappyc_hip ]; } && sf="${SCHED_LZ4C--mllvm -amdgpu-sched-strategy=max-memory-clause}"
-  [ $f = zstdc_hip ] && sf="-mllvm -amdgpu-atomic-optimizer-strategy=None"
+  # per-file flags as in the Makefile; SCHED_<file> (e.g. SCHED_decode_hip) overrides one file's
+  case $f in
+    lz4c_hip) sf="-mllvm -amdgpu-sched-strategy=max-ilp" ;;
+    snappyc_hip) sf="-mllvm -amdgpu-sched-strategy=max-memory-clause" ;;
+    zstdc_hip) sf="-mllvm -amdgpu-atomic-optimizer-strategy=None" ;;
+    *) sf="" ;;
+  esac
+  v=SCHED_$f; [ -n "${!v+x}" ] && sf="${!v}"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 $sf $flags -c $f.hip -o $out/$f.o &
   objs="$objs $out/$f.o"
 done
