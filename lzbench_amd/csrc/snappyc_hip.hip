@@ -1014,36 +1014,74 @@ __device__ int frag_bytes(rsrc_t rr, int r0, int r1, int ia, int lane) {
 }
 
 // lay out the records [r0, r1) at op (the first literal run starts at ia); returns the end
+// One group of 64 records (lzh_snappy_emit_kernel's pipeline): header from the records (the literal
+// run of a record starts at the previous record's end: lane-1 by a wave shift, the previous group's
+// end for lane 0) and its input span's dwords, loaded unconditionally into the caller's registers
+// (unneeded lanes re-read the span's first dword): a load under a branch merges with the old register
+// value, and that copy would wait for the load.
+constexpr int kSpanW = kSpan / 256;
+struct SGrp {
+    int Pc = 0, ml = 0, anc = 0, lit = 0, ia = 0, Lt = 0, X0 = 0, nd = 0;
+    uint32_t o = 0;
+    bool v = false, span = false;
+    __device__ __forceinline__ void head(uint32_t w0, uint32_t w1, int ia_, int g, int r1, const Bytes& in, int lane) {
+        v = g + lane < r1;
+        Pc = (int)(w0 & 0xFFFFFFu);
+        ml = v ? (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8)) : 0;
+        o = w1 >> 16;
+        const int end = Pc + ml;
+        ia = ia_;
+        anc = __builtin_amdgcn_update_dpp(ia_, end, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        lit = v ? Pc - anc : 0;
+        Lt = __builtin_amdgcn_readlane(end, max(min(64, r1 - g), 1) - 1) - ia_;
+        span = Lt + 8 <= kSpan;
+        X0 = (ia_ + in.sh) & ~3;
+        nd = (ia_ + in.sh + Lt - X0 + 3) >> 2;
+    }
+    __device__ __forceinline__ void issue(const Bytes& in, int lane, uint32_t* sp) const {
+        const int a0 = X0 + 4 * lane;
+#pragma unroll
+        for (int k = 0; k < kSpanW; k++) sp[k] = ld_b32(in.r, span && 64 * k < nd ? a0 + 256 * k : a0);
+    }
+};
+
 template <class OutR>
 __device__ __forceinline__ int emit_records(OutR& R, const Bytes& in_b, rsrc_t rr, int r0, int r1, int ia, int op,
                             LDSA uint32_t* ibuf, int lane) {
-    uint32_t nw0 = 0, nw1 = 0;                 // records of the next group (loaded one group ahead)
-    if (r0 + lane < r1) { nw0 = ld_b32(rr, 8 * (r0 + lane)); nw1 = ld_b32(rr, 8 * (r0 + lane) + 4); }
-    for (int g = r0; g < r1; g += 64) {
-        const int r = g + lane;
-        const bool v = r < r1;
-        const uint32_t w0 = nw0, w1 = nw1;
-        if (r + 64 < r1) { nw0 = ld_b32(rr, 8 * (r + 64)); nw1 = ld_b32(rr, 8 * (r + 64) + 4); }
-        // the literal run of a record starts at the previous record's end (lane-1 by a wave shift;
-        // the previous group's end for lane 0)
-        const int Pc = (int)(w0 & 0xFFFFFFu);
-        const int ml = v ? (int)((w0 >> 24) | ((w1 & 0xFFFFu) << 8)) : 0;
-        const uint32_t o = w1 >> 16;
-        const int end = Pc + ml;
-        const int anc = __builtin_amdgcn_update_dpp(ia, end, 0x138, 0xf, 0xf, false);   // wave_shr:1
-        const int lit = v ? Pc - anc : 0;
+    // Software pipeline over groups of 64 records (as lzh_lz4_emit_kernel): while group g is laid
+    // out, group g+1's input span and the records of group g+2 are in flight.
+    SGrp GA, GB;                                  // headers of groups g and g+1 (alternating roles)
+    uint32_t sp[kSpanW];                          // group g's span dwords (in flight)
+    // records of group g+1 (in flight); offsets past the chunk's records are out of range (0)
+    uint32_t nw0 = ld_b32(rr, 8 * (r0 + 64 + lane)), nw1 = ld_b32(rr, 8 * (r0 + 64 + lane) + 4);
+    {
+        const uint32_t w0 = ld_b32(rr, 8 * (r0 + lane)), w1 = ld_b32(rr, 8 * (r0 + lane) + 4);
+        GA.head(w0, w1, ia, r0, r1, in_b, lane);
+        GA.issue(in_b, lane, sp);
+    }
+    auto step = [&](SGrp& G, SGrp& Gn, int g) {
+        if (G.span) {   // group g's input span [ia, ia + Lt) into LDS (literal bytes are read from there)
+#pragma unroll
+            for (int k = 0; k < kSpanW; k++)
+                if (64 * k < G.nd && lane + 64 * k < G.nd) ibuf[lane + 64 * k] = sp[k];
+            wave_lds_fence();
+        }
+        {   // group g+1: header from its records; its span and the records of group g+2 go out now
+            const uint32_t w0 = nw0, w1 = nw1;
+            nw0 = ld_b32(rr, 8 * (g + 128 + lane));
+            nw1 = ld_b32(rr, 8 * (g + 128 + lane) + 4);
+            Gn.head(w0, w1, G.ia + G.Lt, g + 64, r1, in_b, lane);
+            Gn.issue(in_b, lane, sp);
+        }
+        const bool v = G.v;
+        const int ml = G.ml, anc = G.anc, lit = G.lit, X0 = G.X0;
+        const uint32_t o = G.o;
         const snv2::SnapSeq Q(lit, o, ml);
         const int S = v ? Q.total : 0;
-        const int Lt = rdlanei(end, min(64, r1 - g) - 1) - ia;
         int T;
         const int pos = op + sne::wave_excl_scan(S, T);
         const int litmax = (int)uni((uint32_t)sne::wave_max(lit));
-        if (T <= sne::kRingB / 2 && litmax <= LZH_SNE_LITMAX && Lt + 8 <= sne::kSpan) {
-            // the group's input span [ia, ia + Lt) into LDS (literal bytes are read from there)
-            const int X0 = (ia + in_b.sh) & ~3;
-            const int nd = (ia + in_b.sh + Lt - X0 + 3) >> 2;
-            for (int d = lane; d < nd; d += 64) ibuf[d] = ld_b32(in_b.r, X0 + 4 * d);
-            wave_lds_fence();
+        if (T <= sne::kRingB / 2 && litmax <= LZH_SNE_LITMAX && G.span) {
             const LDSA uint8_t* ib = (const LDSA uint8_t*)ibuf;
             const int ioff = in_b.sh - X0;            // input position p lives at ib[p + ioff]
             if (op + T - R.flushed > sne::kRingB - 8) R.flush(op, false, lane);
@@ -1102,7 +1140,10 @@ __device__ __forceinline__ int emit_records(OutR& R, const Bytes& in_b, rsrc_t r
                 op += K.total;
             }
         }
-        ia += Lt;
+    };
+    for (int g = r0; g < r1; g += 128) {
+        step(GA, GB, g);
+        if (g + 64 < r1) step(GB, GA, g + 64);
     }
     return op;
 }
