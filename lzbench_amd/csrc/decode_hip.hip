@@ -2454,6 +2454,14 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
             if (phase != 3) { res = kLegacy; phase = 3; }   // the one-wave decoder)
             lowok = 1 << 30;
         }
+        // the cells of the states (read one step ahead from here on: a step reads the next step's cells
+        // as soon as its states are known, under its checks and record)
+        uint32_t cL = 0, cM = 0, cO = 0;
+        if (phase == 2) {
+            cL = *(const LDSA uint32_t*)(S + sLL * kRow + lo4);
+            cM = *(const LDSA uint32_t*)(S + kLdsML + sML * kRow + lo4);
+            cO = *(const LDSA uint16_t*)(S + kLdsOF + (sOF >> 1) * kRow + lo4 + (sOF & 1) * 2);
+        }
         // ---- kSB steps: each stores exactly one record per lane (a dummy word for a lane without one),
         // so that the next point's vmcnt(kSB) waits for this point's fills and not for these stores
         for (int k = 0; k < kSB; k++) {
@@ -2461,9 +2469,7 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
             uint32_t r0 = 0, r1 = 0;
             bool keep = false;
             if (act) {
-                const uint32_t eL = *(const LDSA uint32_t*)(S + sLL * kRow + lo4);
-                const uint32_t eM = *(const LDSA uint32_t*)(S + kLdsML + sML * kRow + lo4);
-                const uint32_t eO = *(const LDSA uint16_t*)(S + kLdsOF + (sOF >> 1) * kRow + lo4 + (sOF & 1) * 2);
+                const uint32_t eL = cL, eM = cM, eO = cO;
                 const int ofc = (int)(eO >> 9);
                 const uint32_t eOx = eO & 511u;
                 const int no = (int)__builtin_ctz(eOx);
@@ -2505,6 +2511,9 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 sML = (eM & 511u) + __builtin_amdgcn_ubfe(sb, (uint32_t)no, (uint32_t)nm);
                 sOF = ((eOx - (1u << no)) >> 1) + __builtin_amdgcn_ubfe(sb, 0u, (uint32_t)no);
                 P = P4;
+                cL = *(const LDSA uint32_t*)(S + sLL * kRow + lo4);
+                cM = *(const LDSA uint32_t*)(S + kLdsML + sML * kRow + lo4);
+                cO = *(const LDSA uint16_t*)(S + kLdsOF + (sOF >> 1) * kRow + lo4 + (sOF & 1) * 2);
                 // the reference updates the states after the last sequence too and accepts an exhausted
                 // or overrun stream there (ZSTD_decompressSequences_body: reload >= completed); then the
                 // checks of ZSTD_execSequence, and the layout's limits (else the one-wave decoder decodes)
