@@ -434,6 +434,7 @@ static void usage(params_t* P) {
     fprintf(stderr, " -tX,Y set min. time in seconds for compression and decompression (default = %.0f, %.0f)\n",
             P->cmintime / 1000.0, P->dmintime / 1000.0);
     fprintf(stderr, " -v    disable progress information\n -x    disable real-time process priority\n -z    show (de)compression times instead of speed\n");
+    fprintf(stderr, "\ndebug (environment): LZH_DUMP_DIR=dir writes each GPU row's packed buffer and compressed sizes there\n");
 }
 
 static int read_file(const char* fn, std::vector<uint8_t>& out) {

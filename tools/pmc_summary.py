@@ -1,4 +1,5 @@
-"""tools/pmc_summary.py OUTDIR -- fold tools/pmc_sq.sh passes into per-dispatch averages per kernel."""
+"""tools/pmc_summary.py OUTDIR -- fold the rocprofv3 --pmc passes of tools/pmc_inst.sh / tools/pmc_zstd.sh into
+per-dispatch averages per kernel."""
 import csv, glob, os, sys, collections
 out = sys.argv[1]
 avg = collections.defaultdict(dict)
