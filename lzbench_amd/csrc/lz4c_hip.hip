@@ -833,6 +833,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 // ================= run batch: resolve every sequence that starts in the batch
                 // ("colliders" are re-evaluated per step against the in-batch candidate)
                 LZ_CLK(4);                                             // eval + slot groups
+                // the resolve (a serial chain of dependent scalar / lane reads) issues ahead of the other
+                // waves' independent work: s_setprio 1 until the table restore (-0.6 %, profiles/r04_d)
+                __builtin_amdgcn_s_setprio(1);
                 const int fv = __builtin_popcountll(vmask);           // first lane past mflimit
                 const uint64_t I0 = pins >= 0 ? (1ull << (pins - base)) : 0ull;
                 const int lo = q - base, hi0 = min(qlim - base, LZH_WAVE - 1);
@@ -1026,6 +1029,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         base = pins >= 0 ? pins : q;
                     }
                 }
+                __builtin_amdgcn_s_setprio(0);
                 LZ_CLK(8);                                             // table restore
                 continue;
             }
