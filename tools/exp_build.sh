@@ -14,6 +14,7 @@ for f in lz4c_hip snappyc_hip decode_hip pack_hip zstdc_hip frame_hip; do
     lz4c_hip) sf="-mllvm -amdgpu-sched-strategy=max-ilp" ;;
     snappyc_hip) sf="-mllvm -amdgpu-sched-strategy=max-memory-clause" ;;
     zstdc_hip) sf="-mllvm -amdgpu-atomic-optimizer-strategy=None" ;;
+    decode_hip) sf="-mllvm -amdgpu-sched-strategy=max-ilp" ;;
     *) sf="" ;;
   esac
   v=SCHED_$f; [ -n "${!v+x}" ] && sf="${!v}"
