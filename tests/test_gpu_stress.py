@@ -92,3 +92,33 @@ def test_stress_vs_oracle(torch_cuda, gen, seed, cfg):
     assert len(packed) == len(exp_packed) and (packed == exp_packed).all(), "packed bytes differ"
     out = L.decompress_chunks(packed, cs, len(data), codec, chunk)
     assert (out == data).all()
+
+
+def _copies_chunks():
+    """64 KiB chunks of random bytes, each with k copies of earlier 16-byte blocks (about one sequence per
+    copy: no other 4-byte repeats) spaced s bytes apart: record counts around the emission kernels' 64-record
+    groups and their one-group-ahead loads (k = 0 .. 300), input spans that fit the group's LDS copy (s = 20)
+    and spans that do not (s = 200: the record-by-record path)."""
+    rng = np.random.default_rng(4242)
+    chunks = []
+    for s in (20, 200):
+        for k in (0, 1, 2, 63, 64, 65, 127, 128, 129, 191, 192, 193, 256, 300):
+            c = rng.integers(0, 256, 65536).astype(np.uint8)
+            for i in range(k):
+                pos = 1024 + i * s
+                src = int(rng.integers(0, pos - 32))
+                c[pos:pos + 16] = c[src:src + 16]
+            chunks.append(c)
+    return np.concatenate(chunks)
+
+
+@pytest.mark.parametrize("codec", ["lz4", "snappy"])
+def test_emission_group_boundaries(torch_cuda, codec):
+    data = _copies_chunks()
+    packed, cs = L.compress_chunks(data, codec, 65536, 1 if codec == "lz4" else 0)
+    exp_packed, exp_cs = O.compress_chunks(data, codec, 65536, 1 if codec == "lz4" else 0)
+    bad = np.nonzero(cs != exp_cs)[0]
+    assert len(bad) == 0, f"chunk sizes differ first at chunk {bad[:4]}: {cs[bad[:4]]} vs {exp_cs[bad[:4]]}"
+    assert len(packed) == len(exp_packed) and (packed == exp_packed).all(), "packed bytes differ"
+    out = L.decompress_chunks(packed, cs, len(data), codec, 65536)
+    assert (out == data).all()
