@@ -265,7 +265,16 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group(backend=args.backend)
+        # (gloo prints "[Gloo] Rank r is connected to ..." on the process's stdout while it connects:
+        # send it to stderr, so that rank 0's stdout is the one JSON line)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend=args.backend)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
 
     import lzbench_amd as L
 
