@@ -40,12 +40,6 @@ constexpr int kMinLength = 13;
 constexpr int kRing = 1024;           // bytes of LDS input ring per wave
 constexpr int kAhead = 704;           // keep the ring filled this far past the batch front
 constexpr int kOut = 512;             // bytes of LDS output ring per wave
-#ifndef LZH_BRFREE
-#define LZH_BRFREE 1
-#endif
-#ifndef LZH_PACKOS
-#define LZH_PACKOS 1
-#endif
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -291,7 +285,7 @@ __device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const B
         int carry = first;
         // offset (< 2^16) and output start (< 256 on this path) in one gathered word (packing
         // lit | mlx << 8 as well measured 0.3 % slower)
-        const uint32_t os = LZH_PACKOS ? (off | (st << 16)) : 0u;
+        const uint32_t os = off | (st << 16);
         for (int pass = 0; pass * LZH_WAVE < tot; pass++) {
             const int ob = pass * LZH_WAVE + lane;
             // owner of output byte ob: the last member starting at or before it.  Start marks go
@@ -312,14 +306,9 @@ __device__ __forceinline__ int emit_recs(const Bytes& in, const Ring& R, const B
             const int a = (int)lane_gather(anc, k), l = (int)lane_gather(lit, k);
             const int m = (int)lane_gather(mlx, k);
             int o, t;
-            if (LZH_PACKOS) {
-                const uint32_t osk = lane_gather(os, k);
-                o = (int)(osk & 0xffffu);
-                t = ob - (int)(osk >> 16);
-            } else {
-                o = (int)lane_gather(off, k);
-                t = ob - (int)lane_gather(st, k);
-            }
+            const uint32_t osk = lane_gather(os, k);
+            o = (int)(osk & 0xffffu);
+            t = ob - (int)(osk >> 16);
             const SeqLayout S(l, true, m);
             const uint32_t lb = R.byte(a + t - S.lit0);
             if (ob < tot) O.put(op + ob, S.byte(t, lb, o));
@@ -407,12 +396,7 @@ struct MWin {
         const int X = (valid ? (int)c : 0) + in.sh;
         const int A = (X & ~3) - 4;
         sm = X & 3;
-#if LZH_BRFREE
         {   // (idle lanes load the chunk's first bytes: in range, and their evaluation is masked)
-#else
-        d0 = d1 = d2 = d3 = d4 = d5 = d6 = d7 = 0;
-        if (valid) {
-#endif
             // d0 (bytes before the candidate) matters only when A >= 0: clamped, separate load
             // (a merged wide load starting at offset -4 would fail its range check as a whole)
             d0 = ld_b32(in.r, max(A, 0)); d1 = ld_b32(in.r, A + 4); d2 = ld_b32(in.r, A + 8); d3 = ld_b32(in.r, A + 12);
@@ -755,7 +739,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             uint32_t cand = old;
             MWin W;
             W.load(in, cand, valid);                                   // (issued before the claim round trip)
-            if (LZH_BRFREE && vmask == ~0ull) T.put(h, (uint32_t)p);   // (no exec-mask juggling)
+            if (vmask == ~0ull) T.put(h, (uint32_t)p);   // (no exec-mask juggling)
             else if (valid) T.put(h, (uint32_t)p);
             wave_lds_fence();
             const uint32_t back = T.get(h);
@@ -965,7 +949,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 // (kLinked) the table restore at the end of a block (as in the else branch below)
                 auto restore = [&](uint64_t Iw) {
                     const bool inI = lane_on(Iw);
-                    if (LZH_BRFREE && vmask == ~0ull) {
+                    if (vmask == ~0ull) {
                         // every lane stores its slot's final value (all lanes of a slot agree):
                         // the slot's last inserted lane, else its old value
                         const uint64_t gi = grp & Iw;
@@ -1007,7 +991,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     }
                     // table: the last inserted lane of each slot, or the slot's old value
                     const bool inI = lane_on(I);
-                    if (LZH_BRFREE && vmask == ~0ull) {
+                    if (vmask == ~0ull) {
                         // every lane stores its slot's final value (all lanes of a slot agree):
                         // the slot's last inserted lane, else its old value
                         const uint64_t gi = grp & I;

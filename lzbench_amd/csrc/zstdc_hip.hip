@@ -156,9 +156,6 @@ struct LdsTab24 {
     static constexpr uint32_t kBackMask = ~0u;
     __device__ __forceinline__ void fence() const { wave_lds_fence(); }
 };
-#ifndef LZH_ZSTD_MSKOR
-#define LZH_ZSTD_MSKOR 1
-#endif
 // 17-bit entries for frames of at most 128 KiB (positions + 1 < 2^17): 16-bit low halves + a bitmap
 // of bit 16 -- 17 KiB at hashLog 13, 9 waves per CU instead of 6.  A put writes the low half and
 // clears / sets the bit with LDS atomics (lanes of one bitmap dword touch different bits).  When lanes
@@ -174,14 +171,9 @@ struct LdsTab17 {
     }
     __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
         ((volatile LDSA uint16_t*)lo)[h] = (uint16_t)v;
-#if LZH_ZSTD_MSKOR
         // bit h & 31 of the bitmap dword := bit 16 of v in one atomic (ds_mskor_b32: M = (M & ~mask) | data)
         const uint32_t a = (uint32_t)(uintptr_t)(bm + (h >> 5));
         asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(a), "v"(1u << (h & 31u)), "v"(((v >> 16) & 1u) << (h & 31u)) : "memory");
-#else
-        __atomic_fetch_and(bm + (h >> 5), ~(1u << (h & 31u)), __ATOMIC_RELAXED);
-        __atomic_fetch_or(bm + (h >> 5), ((v >> 16) & 1u) << (h & 31u), __ATOMIC_RELAXED);
-#endif
     }
     // the claim writes whole entries (an uncontested slot keeps it); its readback reads the low half
     __device__ __forceinline__ void claim(uint32_t h, uint32_t v) const { put(h, v); }
