@@ -51,8 +51,9 @@ COMPRESS_KERNEL = {"lz4": "lzh_lz4_parse_kernel", "lz4fast": "lzh_lz4_parse_kern
                    "snappy": "lzh_snappy_parse_kernel",
                    "zstd": "lzh_zstd_match_kernel+lzh_zstd_entropy_kernel"}
 # (zstd decodes in four kernels, and frames the split layout does not fit in a fifth: the stage)
-DECOMPRESS_KERNEL = {"zstd": "lzh_zstd_hdr_kernel+lzh_zstd_huf_kernel+lzh_zstd_seq_kernel+lzh_zstd_exec_kernel"
-                             "+lzh_zstd_decompress_kernel"}
+# (the literal kernel comes in two widths, lzh_zstd_huf_kernel / lzh_zstd_huf8_kernel, picked by frame count)
+DECOMPRESS_KERNEL = {"zstd": "lzh_zstd_hdr_kernel+lzh_zstd_huf_kernel+lzh_zstd_huf8_kernel+lzh_zstd_seq_kernel"
+                             "+lzh_zstd_exec_kernel+lzh_zstd_decompress_kernel"}
 
 
 def log(*a):

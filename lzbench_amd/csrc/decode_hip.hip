@@ -2684,18 +2684,23 @@ lzh_zstd_hdr_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
 // sequence kernel.  A stream not consumed exactly (huf_streams' verdict 1) sends its frame to the
 // one-wave decoder when the reference would use the double-symbol decoder there, else it is corrupt.
 namespace zsplit {
-constexpr int kHJ = 4, kHL = 4 * kHJ;            // sections a wave, lanes in use
-constexpr int kHRow = 4 * kHL;                   // 64 bytes
 constexpr int kHB = 16;                          // steps between uniform points (= bytes staged per lane)
-constexpr int kHLdsRing = 256 * kHRow, kHLds = kHLdsRing + 33 * kHRow;
 }  // namespace zsplit
 
-extern "C" __global__ void __launch_bounds__(64)
-lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t n_total,
-                    uint64_t chunk_size, uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst,
-                    const zsplit::ZHuf* jobs, const uint32_t* njobs, unsigned long long* stats) {
+// HJ sections a wave (4 HJ lanes in use).  The kernel is bound by instruction issue, not by its LDS round
+// trips: 8 sections a wave (36 KiB of LDS, one wave per SIMD) issue half the instructions per section of
+// 4 a wave (two waves per SIMD) -- 1 GiB -b128: mixed 5.3 -> 4.9 ms, text 2.0 -> 1.6 ms; 2 a wave 6.5 /
+// 3.2 ms -- but need 32 sections per CU to keep every SIMD busy, so launches with fewer frames keep 4.
+template <int HJ>
+__device__ __forceinline__ void zstd_huf(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                                         uint64_t n_total, uint64_t chunk_size, uint8_t* out, int32_t* status,
+                                         uint8_t* zt, int32_t* zst, const zsplit::ZHuf* jobs, const uint32_t* njobs,
+                                         unsigned long long* stats) {
     using namespace zsplit;
     using namespace zstdd;
+    constexpr int kHJ = HJ, kHL = 4 * kHJ;          // sections a wave, lanes in use
+    constexpr int kHRow = 4 * kHL;                   // bytes per LDS row (one dword per lane in use)
+    constexpr int kHLdsRing = 256 * kHRow, kHLds = kHLdsRing + 33 * kHRow;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kHLds];
     LDSA uint8_t* const S = (LDSA uint8_t*)lds;
     const int lane = threadIdx.x;
@@ -2850,7 +2855,7 @@ lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
             const int bq = P - tl;
             uint32_t v = fld(bq, tl);
             if (bq < lo) v &= lo - bq >= 32 ? 0u : (~0u << (lo - bq));   // (zero-padded below the start)
-            const uint32_t e = *(const LDSA uint16_t*)(S + ((v >> 3) << 6) + (q << 4) + (v & 7) * 2);
+            const uint32_t e = *(const LDSA uint16_t*)(S + (v >> 3) * kHRow + (q << 4) + (v & 7) * 2);
             *(act ? dst + done : dummy + lane) = (uint8_t)e;
             P -= act ? (int)(e >> 8) : 0;
             done += act;
@@ -2869,6 +2874,19 @@ lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
             status[jf] = ZC;
         }
     }
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t n_total,
+                    uint64_t chunk_size, uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst,
+                    const zsplit::ZHuf* jobs, const uint32_t* njobs, unsigned long long* stats) {
+    zstd_huf<4>(packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst, jobs, njobs, stats);
+}
+extern "C" __global__ void __launch_bounds__(64)
+lzh_zstd_huf8_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t n_total,
+                     uint64_t chunk_size, uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst,
+                     const zsplit::ZHuf* jobs, const uint32_t* njobs, unsigned long long* stats) {
+    zstd_huf<8>(packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst, jobs, njobs, stats);
 }
 
 extern "C" __global__ void __launch_bounds__(64)
@@ -2943,6 +2961,13 @@ extern "C" int lzh_debug_zstd_legacy(int on) {
     g_zstd_legacy = on ? 1 : 0;
     return 0;
 }
+// Test hook: force the zstd literal kernel's sections per wave (4 or 8; 0 = by frame count)
+static int g_zstd_huf_sections = 0;
+extern "C" int lzh_debug_zstd_huf_sections(int hj) {
+    if (hj != 0 && hj != 4 && hj != 8) return -1;
+    g_zstd_huf_sections = hj;
+    return 0;
+}
 extern "C" int lzh_debug_force_decode_window(int kw) {
     if (kw != 0 && kw != 4096 && kw != 8192 && kw != 16384) return -1;
     g_force_window = kw;
@@ -3009,8 +3034,17 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         (void)hipMemsetAsync(d_hst, 0, 8 * sizeof(unsigned long long), s);
         hstats = d_hst;
 #endif
-        hipLaunchKernelGGL(lzh_zstd_huf_kernel, dim3((unsigned)((maxjobs + zsplit::kHJ - 1) / zsplit::kHJ)), dim3(64), 0, s,
-                           packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst,
+        // (8 sections a wave once the frames -- about one Huffman job each -- fill 8 x 4 waves per CU)
+        static int hcus[64];
+        int hdev = 0;
+        (void)hipGetDevice(&hdev);
+        if (hdev < 0 || hdev >= 64) hdev = 0;
+        if (!hcus[hdev] && hipDeviceGetAttribute(&hcus[hdev], hipDeviceAttributeMultiprocessorCount, hdev) != hipSuccess)
+            hcus[hdev] = 0;
+        const int hj = (g_zstd_huf_sections ? g_zstd_huf_sections == 8
+                                            : hcus[hdev] > 0 && (uint64_t)nchunks >= 32ull * (uint64_t)hcus[hdev]) ? 8 : 4;
+        hipLaunchKernelGGL(hj == 8 ? lzh_zstd_huf8_kernel : lzh_zstd_huf_kernel, dim3((unsigned)((maxjobs + hj - 1) / hj)),
+                           dim3(64), 0, s, packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst,
                            (const zsplit::ZHuf*)jobs, (const uint32_t*)njobs, hstats);
 #if LZH_ZSTD_STATS
         {
@@ -3019,7 +3053,7 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
             (void)hipMemcpyAsync(h, d_hst, sizeof(h), hipMemcpyDeviceToHost, s);
             (void)hipMemcpyAsync(&nj, njobs, 4, hipMemcpyDeviceToHost, s);
             (void)hipStreamSynchronize(s);
-            const double w = (double)((nj + zsplit::kHJ - 1) / zsplit::kHJ);
+            const double w = (double)((nj + hj - 1) / hj);
             fprintf(stderr, "zstd huf kernel: %u sections, %.0f symbols a stream; per wave: intervals %.0f; clocks per "
                             "interval: uniform point %.0f (its wait %.0f), steps %.0f; inexact streams %llu (x1) %llu (x2), "
                             "far %llu\n",

@@ -28,7 +28,9 @@ def torch_cuda():
     return torch
 
 
-PATHS = ["split", "legacy"]
+# split: the four kernels (the literal kernel's sections per wave by frame count: 4 for these sizes);
+# split8: the same with 8 sections a wave forced (lzh_debug_zstd_huf_sections); legacy: the one-wave decoder
+PATHS = ["split", "split8", "legacy"]
 
 
 def _legacy(on):
@@ -36,6 +38,13 @@ def _legacy(on):
     f.restype = C.c_int
     f.argtypes = [C.c_int]
     assert f(1 if on else 0) == 0
+
+
+def _huf_sections(hj):
+    f = L.lib().lzh_debug_zstd_huf_sections
+    f.restype = C.c_int
+    f.argtypes = [C.c_int]
+    assert f(hj) == 0
 
 
 def gpu_decode(torch, packed, cs, n, chunk, path="split"):
@@ -47,10 +56,12 @@ def gpu_decode(torch, packed, cs, n, chunk, path="split"):
     dc.out.fill_(0xA5)
     try:
         _legacy(path == "legacy")
+        _huf_sections(8 if path == "split8" else 0)
         dc.decompress(packed=d_packed, csizes=d_cs)
         torch.cuda.synchronize()
     finally:
         _legacy(False)
+        _huf_sections(0)
     return dc.status[:dc.k].cpu().numpy(), dc.out[:n].cpu().numpy()
 
 
@@ -327,6 +338,10 @@ def test_split_and_legacy_statuses_equal(torch_cuda, corpus_kind, chunk):
     assert (st1 == st2).all(), np.nonzero(st1 != st2)[0][:10]
     for i in np.nonzero(st1 == chunk)[0]:
         assert (out1[i * chunk:(i + 1) * chunk] == out2[i * chunk:(i + 1) * chunk]).all(), i
+    st3, out3 = gpu_decode(torch_cuda, blob, cs, len(streams) * chunk, chunk, "split8")
+    assert (st3 == st2).all(), np.nonzero(st3 != st2)[0][:10]
+    for i in np.nonzero(st3 == chunk)[0]:
+        assert (out3[i * chunk:(i + 1) * chunk] == out2[i * chunk:(i + 1) * chunk]).all(), i
 
 
 def _raw_block_frame(data: bytes, block: int) -> bytes:
