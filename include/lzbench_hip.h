@@ -52,9 +52,10 @@ extern "C" {
  * other levels return LZH_EARG.  Decoding: any frame of that shape, also with the XXH64 content
  * checksum (verified); dictionary ids, a missing content size or windows over 2^27 report -2. */
 /* LZH_CODEC_LZ4F: one LZ4 frame per chunk as LZ4F_compressFrame writes it (lz4/lz4frame.c:429-470)
- * with independent blocks; level = LZH_LZ4F_PARAMS(blockSizeID 0|4..7, flags, acceleration).
- * Decoding: frames with independent blocks (or one block), every block but the last full, no
- * dictionary id; other frames report -2.
+ * with independent blocks, or linked blocks with LZH_LZ4F_LINKED (LZ4_compress_fast_continue in prefix
+ * mode, lz4.c:1565-1628); level = LZH_LZ4F_PARAMS(blockSizeID 0|4..7, flags, acceleration).
+ * Decoding: frames with independent or linked blocks, every block but the last full, no dictionary id;
+ * other frames report -2.
  * LZH_CODEC_NVLZ4: one nvcomp LZ4 container per chunk (the format of the reference's nvcomp_lz4
  * row, nvcomp/LZ4Metadata.h), LZ4 blocks of 1 << (15 + level) bytes, level 0..5 (compressors.cpp:1863).
  * Both: lzh_compress_async / lzh_decompress_async and the rows below; not lzh_compress_kernel_only /
@@ -136,7 +137,10 @@ int lzh_debug_gather_order(size_t nsb, const uint64_t* order, const uint64_t* si
 int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t in_readable, size_t chunk_size,
                        void* d_packed, size_t packed_cap, uint32_t* d_csizes, uint64_t* d_offsets,
                        void* d_temp, size_t temp_bytes, void* hip_stream);
-/* d_offsets may be NULL (then derived from d_csizes into d_temp).  d_status: nchunks i32,
+/* d_offsets may be NULL (then derived from d_csizes into d_temp).  d_temp / temp_bytes: LZ4 and snappy use
+ * temp only for those derived offsets; LZ4 frames / nvcomp need lzh_decompress_temp_bytes; zstd runs its
+ * four-kernel decoder in temp when temp_bytes >= lzh_decompress_temp_bytes (chunks of 16 KiB and more),
+ * else every frame in the one-wave decoder (same results, slower).  d_status: nchunks i32,
  * decoded size per chunk or negative on malformed input (zstd / LZ4 frame / nvcomp container:
  * -1 corrupt, -2 unsupported frame feature).  A chunk whose compressed size equals its size is stored raw (all codecs).
  * Replaces (zstd): lzbench_zstd_decompress, compressors.cpp:1767-1773 (ZSTD_decompressDCtx). */

@@ -315,9 +315,15 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
     if (n == 0) return LZH_OK;
     Range range("lzh:decompress");
     const uint64_t* offs = d_offsets;
-    if (!offs || is_frame(codec) || codec == LZH_CODEC_ZSTD) {
-        if (!d_temp || temp_bytes < lzh_decompress_temp_bytes(codec, n, chunk_size)) return LZH_ESPACE;
-    }
+    const size_t scan_bytes = align_up((k + 1) * sizeof(uint64_t), 256);
+    if (is_frame(codec) && (!d_temp || temp_bytes < lzh_decompress_temp_bytes(codec, n, chunk_size))) return LZH_ESPACE;
+    if (!offs && (!d_temp || temp_bytes < scan_bytes + 256)) return LZH_ESPACE;
+    // zstd: the split decoder's per-frame layout lives in temp after the offsets; without room for it
+    // (or for chunks below lzh_zstd_split_min) every frame takes the one-wave decoder
+    uint8_t* zt = nullptr;
+    if (codec == LZH_CODEC_ZSTD && d_temp && temp_bytes >= lzh_decompress_temp_bytes(codec, n, chunk_size) &&
+        lzh_zstd_decode_temp(n, chunk_size) > 0)
+        zt = (uint8_t*)d_temp + scan_bytes;
     if (!offs) {
         LZH_CHECK(lzh_launch_scan(d_csizes, k, (uint64_t*)d_temp, nullptr, s));
         offs = (const uint64_t*)d_temp;
@@ -341,8 +347,7 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
     }
     if (codec == LZH_CODEC_ZSTD)
         LZH_CHECK(lzh_launch_zstd_decompress((const uint8_t*)d_packed, packed_readable, offs, d_csizes, n, chunk_size,
-                                             (uint8_t*)d_out, d_status, (uint32_t)k,
-                                             (uint8_t*)d_temp + align_up((k + 1) * sizeof(uint64_t), 256), s));
+                                             (uint8_t*)d_out, d_status, (uint32_t)k, zt, s));
     else
         LZH_CHECK(lzh_launch_decompress(codec, (const uint8_t*)d_packed, packed_readable, offs, d_csizes, n,
                                         chunk_size, (uint8_t*)d_out, d_status, (uint32_t)k, s));
@@ -602,8 +607,9 @@ int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t c
         LZH_CHECK(hipMemcpyAsync(d.h_cs + l * P.sbk, dcs, ck * 4, hipMemcpyDeviceToHost, ks));
         LZH_CHECK(hipEventRecord(e_k, ks));
     }
-    // host-side gather: poll every pending sub-batch (any shard, any order); each one's sizes are
-    // read when its kernels are done, and copies leave as soon as their chunk-order offset is known
+    // host-side gather: block on the next sub-batch in chunk order (its offset needs every earlier
+    // one), then take any later sub-batch that has already finished on another shard without
+    // waiting; copies leave as soon as their chunk-order offset is known
     bool fits = true;
     GatherOrder go(P.nsb);
     auto place = [&](size_t j, size_t base) -> int {
@@ -615,26 +621,32 @@ int64_t run_compress(LzhCtx* c, int level, const uint8_t* in, size_t n, size_t c
         LZH_CHECK(hipMemcpyAsync(out + base, (uint8_t*)d.packed.p + l * sb_packed, tot, hipMemcpyDeviceToHost, d.sout));
         return 0;
     };
-    for (unsigned spin = 0; !go.finished(); spin++) {
-        bool progress = false;
+    auto take = [&](size_t j) -> int {   // j's kernels and size copy are done: record its sizes
+        Dev& d = c->devs[P.shard(j)];
+        const size_t l = P.slot(j), ck = P.c_count(j), c0 = P.c_begin(j);
+        size_t tot = 0;
+        const uint32_t* hs = d.h_cs + l * P.sbk;
+        for (size_t i = 0; i < ck; i++) { compr_sizes[c0 + i] = hs[i]; tot += hs[i]; }
+        return go.complete(j, tot, place);
+    };
+    while (!go.finished()) {
+        const size_t j0 = go.next;
+        hipError_t q = hipEventSynchronize(evk.get(j0));
+        if (q != hipSuccess) {
+            fprintf(stderr, "lzbench_hip: sub-batch %zu failed: %s\n", j0, hipGetErrorString(q));
+            return LZH_EHIP;
+        }
+        if (const int rc = take(j0)) return rc;
         for (size_t j = go.next; j < P.nsb; j++) {
             if (go.done[j]) continue;
-            const hipError_t q = hipEventQuery(evk.get(j));
+            q = hipEventQuery(evk.get(j));
             if (q == hipErrorNotReady) continue;
             if (q != hipSuccess) {
                 fprintf(stderr, "lzbench_hip: sub-batch %zu failed: %s\n", j, hipGetErrorString(q));
                 return LZH_EHIP;
             }
-            Dev& d = c->devs[P.shard(j)];
-            const size_t l = P.slot(j), ck = P.c_count(j), c0 = P.c_begin(j);
-            size_t tot = 0;
-            const uint32_t* hs = d.h_cs + l * P.sbk;
-            for (size_t i = 0; i < ck; i++) { compr_sizes[c0 + i] = hs[i]; tot += hs[i]; }
-            const int rc = go.complete(j, tot, place);
-            if (rc) return rc;
-            progress = true;
+            if (const int rc = take(j)) return rc;
         }
-        if (!progress && (spin & 63) == 63) std::this_thread::yield();
     }
     const size_t base = go.base;
     for (size_t g = 0; g < P.G; g++) {

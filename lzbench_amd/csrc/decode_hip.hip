@@ -3104,8 +3104,10 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
 
 // bytes of the split decoder's temp for n bytes in chunks of chunk_size (per frame: blocks, block
 // positions, sequence tables, sequences; then the frame states and frame fields)
+// (0 below lzh_zstd_split_min: the layout reserves two block slots (~17 KiB) and 2 x chunk of sequence
+// records per frame, 20x the input at 1 KiB chunks; small frames decode in the one-wave kernel)
 size_t lzh_zstd_decode_temp(uint64_t n, uint64_t chunk_size) {
-    if (!chunk_size) return 0;
+    if (chunk_size < lzh_zstd_split_min) return 0;
     const uint64_t k = (n + chunk_size - 1) / chunk_size;
     const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
     return k * Z.stride + 512 + ((k * 4 + 255) & ~255ull) + ((k * sizeof(zsplit::ZFrame) + 255) & ~255ull) + 256 +

@@ -18,6 +18,8 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
                                       const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                       int32_t* status, uint32_t nchunks, uint8_t* zt, hipStream_t s);
 size_t lzh_zstd_decode_temp(uint64_t n, uint64_t chunk_size);
+// smallest chunk the zstd split decoder takes (below it: the one-wave decoder, no temp)
+constexpr uint64_t lzh_zstd_split_min = 16384;
 hipError_t lzh_launch_scan(const uint32_t* csizes, uint64_t nchunks, uint64_t* offsets, uint64_t* total,
                            hipStream_t s);
 hipError_t lzh_launch_pack(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,

@@ -7,7 +7,7 @@ gather: the ranks all-gather their packed totals and chunk counts (a few bytes, 
 then every rank copies its packed slab and its compr_sizes straight into one shared host buffer
 (a /dev/shm mapping) at its chunk-order offset -- the layout of lzbench's compbuf
 (lzbench.cpp:266-298: chunk i at sum(clen[<i])).  No collective moves codec bytes -- unless the
-ranks span hosts or /dev/shm lacks the room, where a dist.gather to rank 0 takes over.  The result is
+ranks span hosts or /dev/shm lacks the room, where point-to-point sends to rank 0 take over.  The result is
 byte-identical to the single-process chunk loop.  bench.py times the same gather on HBM-resident
 slabs.
 """
@@ -63,31 +63,49 @@ def _shm_usable(nbytes: int, world: int, group) -> Tuple[bool, str]:
 
 
 def _gather_collective(p, c, sizes, counts, rank, world, group, keep):
-    """Fallback: rank 0 receives every slab by dist.gather (padded to the largest slab; CUDA tensors
-    under nccl, host tensors under gloo) and lays them out in chunk order."""
+    """Fallback: rank 0 receives the slabs one by one (point-to-point; CUDA tensors under nccl, host
+    tensors under gloo) and writes each straight into one preallocated host buffer at its chunk-order
+    offset: the device holds at most one received slab at a time, never world x the largest."""
     import torch
     import torch.distributed as dist
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
-    mx, mc = max(max(sizes), 1), max(max(counts), 1)
-    pb = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    pb[:p.numel()].copy_(p)
-    cb = torch.zeros(mc, dtype=torch.int64, device=dev)
-    cb[:c.numel()].copy_(c)
-    dst = 0 if group is None else dist.get_global_rank(group, 0)
-    if p.is_cuda:
+    nccl = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+    glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
+    if p.is_cuda or nccl:
         torch.cuda.synchronize()
     dist.barrier(group=group)
     t = time.perf_counter()
-    gp = [torch.empty_like(pb) for _ in range(world)] if rank == 0 else None
-    gc = [torch.empty_like(cb) for _ in range(world)] if rank == 0 else None
-    dist.gather(pb, gp, dst=dst, group=group)
-    dist.gather(cb, gc, dst=dst, group=group)
     res = None
     if rank == 0:
-        allp = torch.cat([gp[r][:sizes[r]] for r in range(world)]).cpu().numpy()
-        allc = torch.cat([gc[r][:counts[r]] for r in range(world)]).cpu().numpy().astype(np.uint64)
+        hp = torch.empty(sum(sizes), dtype=torch.uint8)
+        hc = torch.empty(sum(counts), dtype=torch.int64)
+        hp[:sizes[0]].copy_(p)
+        hc[:counts[0]].copy_(c)
+        rb = torch.empty(max(sizes[1:] + [1]), dtype=torch.uint8, device=dev) if nccl else None
+        rc = torch.empty(max(counts[1:] + [1]), dtype=torch.int64, device=dev) if nccl else None
+        pb, cb = sizes[0], counts[0]
+        for r in range(1, world):
+            if sizes[r]:
+                if nccl:
+                    dist.recv(rb[:sizes[r]], src=glob(r), group=group)
+                    hp[pb:pb + sizes[r]].copy_(rb[:sizes[r]])
+                else:
+                    dist.recv(hp[pb:pb + sizes[r]], src=glob(r), group=group)
+            if counts[r]:
+                if nccl:
+                    dist.recv(rc[:counts[r]], src=glob(r), group=group)
+                    hc[cb:cb + counts[r]].copy_(rc[:counts[r]])
+                else:
+                    dist.recv(hc[cb:cb + counts[r]], src=glob(r), group=group)
+            pb += sizes[r]
+            cb += counts[r]
         if keep:
-            res = (allp, allc)
+            res = (hp.numpy(), hc.numpy().astype(np.uint64))
+    else:
+        if sizes[rank]:
+            dist.send(p.to(dev).contiguous(), dst=glob(0), group=group)
+        if counts[rank]:
+            dist.send(c.to(dev).contiguous(), dst=glob(0), group=group)
     el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=dev)
     dist.all_reduce(el, op=dist.ReduceOp.MAX, group=group)
     return float(el.item()), res
@@ -100,8 +118,8 @@ def gather_slabs(packed, csizes, rank: int, world: int, group=None, keep: bool =
     csizes: its per-chunk compressed sizes (numpy / torch, any integer type).  Returns
     ({"ms", "bytes", "GBps", "path"} of the slab copies, max over ranks; (packed_all, csizes_all) on
     rank 0 when keep, else None).  "path" is "shm" (every rank copies its slab into one /dev/shm
-    mapping) or "collective" (dist.gather to rank 0: ranks on several hosts, too little /dev/shm, or
-    LZH_GATHER=collective)."""
+    mapping) or "collective" (slabs sent to rank 0 one by one: ranks on several hosts, too little
+    /dev/shm, or LZH_GATHER=collective)."""
     import torch
     import torch.distributed as dist
 

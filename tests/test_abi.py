@@ -52,6 +52,21 @@ def test_size_helpers():
     assert lib.lzh_max_packed_bytes(0, 1 << 20, 65536) >= 16 * (65536 + 65536 // 255 + 16)
 
 
+@pytest.mark.parametrize("chunk", [1024, 4096, 16384, 131072])
+def test_zstd_decode_temp_stays_proportionate(chunk):
+    """zstd decode temp per GiB: below 16 KiB chunks the split decoder's per-frame layout (two block slots
+    and 2 x chunk of sequence records, ~20x the input at -b1) is not reserved -- those frames decode in
+    the one-wave kernel -- so -b1 / -b4 need only the offsets; from 16 KiB on the layout costs a few x."""
+    lib = L.lib()
+    n = 1 << 30
+    t = lib.lzh_decompress_temp_bytes(3, n, chunk)
+    k = lib.lzh_num_chunks(n, chunk)
+    if chunk < 16384:
+        assert t <= 8 * (k + 1) + 1024
+    else:
+        assert t <= 4 * n
+
+
 def test_comp_desc_table_mirrors_lzbench():
     assert L.COMP_DESC[0].name == "memcpy"                   # lzbench.cpp:609, :695
     assert L.find_compressor("lz4").name == "hip_lz4"
