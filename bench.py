@@ -8,8 +8,10 @@ HBM when the timed region starts.  value = comp+decomp MB/s (MB = 1e6 B, lzbench
 = bytes processed by all ranks / (max over ranks of the timed wall time).
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, each owns a contiguous 1 GiB shard of the chunk list (weak scaling; every shard is the same
-seed-12345 input, so every rank's output is checked against the one reference digest).  The only
+GPU; rank r owns share r -- bytes [r x 1 GiB, (r+1) x 1 GiB) -- of ONE N GiB seed-12345 corpus, i.e.
+its contiguous range of that corpus's lzbench chunk list (lzbench.cpp:366-373; weak scaling: 1 GiB
+per GPU).  Every share, and the gathered whole, is checked against the reference chunk loop's digest
+of exactly those bytes (tests/golden/fullsize.json, make_fullsize.py SHARED).  The only
 exchange is the host-side gather of SURVEY.md 8(e): after the timed region the ranks all-gather
 their packed totals (a few bytes, control plane), and each copies its packed slab straight into
 one shared host buffer at its chunk-order offset (lzbench_amd/shard.py gather_slabs); that gather
@@ -26,7 +28,7 @@ Also reported (rank 0):
   cpu_baseline_all_cores          the same on every host core this process may use
   e2e                             host-to-host through the batched lzbench rows
                                   (lzbench_hip_compress_batch / _decompress_batch, ngpus = N) on
-                                  the same input (N copies at N > 1), beside the hipMemcpy
+                                  the whole N-share corpus, beside the hipMemcpy
                                   round-trip bound (PCIe; never value)
   roofline_compress_stage         the whole compress stage (parse + emit + scan + pack) against
                                   the same N + C algorithmic bytes
@@ -154,12 +156,14 @@ def traffic_for(kernel, workload):
     return None
 
 
-def fullsize_digest(corpus, codec, chunk, level, n, seed):
+def fullsize_digest(corpus, codec, chunk, level, n, seed, offset=0):
+    """the reference chunk loop's digest of corpus bytes [offset, offset + n) (tests/golden/fullsize.json)"""
     path = os.path.join(ROOT, "tests", "golden", "fullsize.json")
     try:
         for e in json.load(open(path)):
             lvl = level if codec in ("lz4fast", "zstd") else (1 if codec == "lz4" else 0)
-            if (e["corpus"], e["codec"], e["chunk"], e["level"], e["size"], e["seed"]) == (corpus, codec, chunk, lvl, n, seed):
+            if (e["corpus"], e["codec"], e["chunk"], e["level"], e["size"], e["seed"], e.get("offset", 0)) == \
+                    (corpus, codec, chunk, lvl, n, seed, offset):
                 return e
     except (OSError, ValueError):
         pass
@@ -177,9 +181,8 @@ def e2e_rows(L, host, codec, chunk, level, ngpus, iters, dig=None):
     """Host-to-host through the batched lzbench rows (what lzbench_hip -b -g<ngpus> runs): best of
     `iters` compress_batch and decompress_batch passes over `host` (its chunk list sharded over
     ngpus devices, api.cpp make_plan), and the hipMemcpy round trip (H2D + D2H of the same bytes,
-    pinned, one device) as the PCIe bound beside them.  dig: the reference digest of one copy of
-    the per-GPU input (host = ngpus copies of it): every copy's slab of the packed output and of
-    compr_sizes must hash to it."""
+    pinned, one device) as the PCIe bound beside them.  dig: the reference digest of `host` itself:
+    the whole packed output and compr_sizes must hash to it."""
     import torch
     n = len(host)
     cs = L.chunk_sizes_for(n, chunk)
@@ -203,15 +206,9 @@ def e2e_rows(L, host, codec, chunk, level, ngpus, iters, dig=None):
             best_d = min(best_d, time.perf_counter() - t)
     ok = tot > 0 and r == n and bool((back[:n] == host).all())
     exact = None
-    # (each copy's slab lines up with whole chunks only when the per-copy size is a multiple of the
-    # chunk size; otherwise a copy's chunks straddle two copies and no per-copy digest applies)
-    if dig is not None and tot > 0 and dig["size"] % chunk == 0:
-        reps, per = n // dig["size"], len(cs) // (n // dig["size"])
-        c64 = comp.astype("<u8")
-        offs = np.concatenate([[0], np.cumsum(comp.astype(np.int64))])
-        exact = reps * dig["size"] == n and all(
-            sha(c64[i * per:(i + 1) * per]) == dig["csizes_sha256"] and
-            sha(out[offs[i * per]:offs[(i + 1) * per]]) == dig["packed_sha256"] for i in range(reps))
+    if dig is not None and tot > 0 and dig["size"] == n:
+        exact = tot == dig["packed_bytes"] and sha(comp.astype("<u8")) == dig["csizes_sha256"] and \
+            sha(out[:tot]) == dig["packed_sha256"]
     del back
     pin = torch.from_numpy(host[:min(n, 1 << 30)]).pin_memory()
     n1 = len(pin)
@@ -281,10 +278,14 @@ def main():
 
     n = args.size_mib << 20
     chunk = args.chunk_kib << 10
-    seed = 12345                       # every rank's shard is the digest-pinned input (see docstring)
+    seed = 12345                       # the digest-pinned corpus (see docstring)
+    if world > 1 and (n % (16 << 20) or n % chunk):
+        raise SystemExit("bench.py: at N > 1 the per-GPU size must be a multiple of 16 MiB and of the chunk size "
+                         "(rank r owns bytes [r n, (r+1) n) of one corpus)")
     t = time.perf_counter()
-    host = L.datagen(args.corpus, n, seed=seed)
-    log(f"[rank {rank}] generated {n >> 20} MiB {args.corpus} in {time.perf_counter() - t:.1f}s")
+    host = L.datagen(args.corpus, n, seed=seed, offset=rank * n)   # share `rank` of one world x n corpus
+    log(f"[rank {rank}] generated share {rank} ({n >> 20} MiB) of {world * n >> 20} MiB {args.corpus} "
+        f"in {time.perf_counter() - t:.1f}s")
     d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda")
     d_in[:n].copy_(torch.from_numpy(host))
     codec = L.DeviceCodec(args.codec, n, chunk, level=args.level)
@@ -335,16 +336,23 @@ def main():
     ratio = comp_total / n
 
     result_extra = {}
+    whole = fullsize_digest(args.corpus, args.codec, chunk, args.level, world * n, seed) if world > 1 else None
     if dist:
         from lzbench_amd.shard import gather_slabs
-        g, _ = gather_slabs(codec.packed[:comp_total], codec.csizes[:codec.k], rank, world, keep=False)
+        g, res = gather_slabs(codec.packed[:comp_total], codec.csizes[:codec.k], rank, world, keep=whole is not None)
         g["how"] = ("all_gather of packed totals, then each rank copies its HBM slab (and its compr_sizes) into one "
                     "shared host buffer at its chunk-order offset (lzbench_amd/shard.py gather_slabs); timed after "
                     "the timed region, max over ranks")
+        if rank == 0 and res is not None:
+            # the gathered whole (every share in chunk order) against the digest of the whole corpus
+            g["bit_exact_whole"] = bool(len(res[0]) == whole["packed_bytes"] and sha(res[0]) == whole["packed_sha256"]
+                                        and sha(res[1].astype("<u8")) == whole["csizes_sha256"])
+            g["whole_bytes"] = world * n
+        del res
         result_extra["gather"] = g
 
-    # bit-exactness of the WHOLE output vs the reference chunk loop's digest, on every rank
-    dig = fullsize_digest(args.corpus, args.codec, chunk, args.level, n, seed)
+    # bit-exactness of the WHOLE output vs the reference chunk loop's digest of this rank's share
+    dig = fullsize_digest(args.corpus, args.codec, chunk, args.level, n, seed, offset=rank * n)
     exact = None
     if dig is not None:
         cs64 = codec.csizes.cpu().numpy().astype("<u8")
@@ -356,14 +364,16 @@ def main():
         flags = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
         dist.all_gather(flags, flag)
         ranks_exact = [None if int(f.item()) < 0 else bool(f.item()) for f in flags]
-    if dig is not None:
+    if all(x is not None for x in ranks_exact):
         result_extra["bit_exact"] = all(ranks_exact)
         result_extra["bit_exact_ranks"] = ranks_exact
         result_extra["bit_exact_bytes"] = n * world
-        result_extra["bit_exact_against"] = "tests/golden/fullsize.json (reference chunk loop, oracle/_ref)"
+        result_extra["bit_exact_against"] = ("tests/golden/fullsize.json (reference chunk loop, oracle/_ref): "
+                                             "each rank's share, offset r x size")
     else:
         result_extra["bit_exact"] = None
-        result_extra["bit_exact_against"] = "no committed reference digest for this workload"
+        result_extra["bit_exact_ranks"] = ranks_exact
+        result_extra["bit_exact_against"] = "no committed reference digest for this workload (or for some share)"
 
     cpu = None
     usable, cpuinfo = host_cpus()
@@ -381,8 +391,8 @@ def main():
         if dist:
             dist.barrier()
         if rank == 0:
-            big = host if world == 1 else np.tile(host, world)
-            result_extra["e2e"] = e2e_rows(L, big, args.codec, chunk, args.level, world, 3, dig)
+            big = host if world == 1 else L.datagen(args.corpus, world * n, seed=seed)
+            result_extra["e2e"] = e2e_rows(L, big, args.codec, chunk, args.level, world, 3, dig if world == 1 else whole)
             del big
         if dist:
             dist.barrier()
@@ -407,8 +417,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": f"synthetic {args.corpus} corpus (SURVEY.md 8(d) stand-in; enwik8/Silesia unavailable offline), "
-                f"the same seed-12345 shard on every rank, resident in HBM",
+        "data": f"synthetic {args.corpus} corpus (SURVEY.md 8(d) stand-in; enwik8/Silesia unavailable offline): "
+                f"rank r owns share r ({size_label(n)}) of one {size_label(world * n)} seed-12345 corpus, resident in HBM",
         "config": {
             "workload": f"{args.codec}{',' + str(args.level) if args.codec in ('lz4fast', 'zstd') else ''} "
                         f"-b{args.chunk_kib} on {size_label(n)} {args.corpus} per GPU, comp+decomp pass",

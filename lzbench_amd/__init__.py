@@ -120,8 +120,10 @@ def lib():
     return _lib
 
 
-def datagen(kind: str | int, n: int, seed: int = 12345) -> np.ndarray:
-    """Synthetic corpus: random / text / json / mixed / binary."""
+def datagen(kind: str | int, n: int, seed: int = 12345, offset: int = 0) -> np.ndarray:
+    """Synthetic corpus: random / text / json / mixed / binary.  offset (a multiple
+    of 16 MiB): bytes [offset, offset + n) of the same corpus -- a rank's share of a multi-GiB input
+    (the corpus is generated in independent 16 MiB segments, so a share needs no prefix)."""
     global _dg
     kinds = {"random": 0, "text": 1, "json": 2, "mixed": 3, "binary": 4}
     k = kinds[kind] if isinstance(kind, str) else int(kind)
@@ -131,8 +133,12 @@ def datagen(kind: str | int, n: int, seed: int = 12345) -> np.ndarray:
         _dg = C.CDLL(DATAGEN_PATH)
         _dg.lzb_datagen.restype = _SZ
         _dg.lzb_datagen.argtypes = [C.c_int, C.c_uint64, _P, _SZ]
+        _dg.lzb_datagen_at.restype = _SZ
+        _dg.lzb_datagen_at.argtypes = [C.c_int, C.c_uint64, _P, _SZ, _SZ]
+    if offset % (16 << 20):
+        raise ValueError("datagen offset must be a multiple of 16 MiB")
     buf = np.empty(max(n, 1), dtype=np.uint8)
-    if _dg.lzb_datagen(k, C.c_uint64(seed), buf.ctypes.data, n) != n:
+    if _dg.lzb_datagen_at(k, C.c_uint64(seed), buf.ctypes.data, offset, n) != n:
         raise ValueError(f"bad corpus kind {kind}")
     return buf[:n]
 

@@ -149,7 +149,7 @@ static size_t gen_one(int kind, uint64_t seed, uint8_t* buf, size_t n) {
 /* Corpora are generated in independent 16 MiB segments (segment s seeded with
  * seed * 1000003 + s), so the bytes do not depend on how many threads produce them. */
 #define SEG ((size_t)16 << 20)
-typedef struct { int kind; uint64_t seed; uint8_t* buf; size_t n, s0, s1; } seg_job;
+typedef struct { int kind; uint64_t seed; uint8_t* buf; size_t off, end, s0, s1; } seg_job;
 
 static int kind_of_segment(int kind, size_t s) {
     static const int order[4] = { LZB_DATA_TEXT, LZB_DATA_JSON, LZB_DATA_BINARY, LZB_DATA_RANDOM };
@@ -157,32 +157,40 @@ static int kind_of_segment(int kind, size_t s) {
     return order[(s * SEG / ((size_t)64 << 20)) % 4];     /* 64 MiB stripes */
 }
 
+/* segments [s0, s1) of the corpus into buf, which holds corpus bytes [off, end) */
 static void* seg_worker(void* a) {
     seg_job* j = (seg_job*)a;
     for (size_t s = j->s0; s < j->s1; s++) {
-        size_t off = s * SEG, len = j->n - off < SEG ? j->n - off : SEG;
-        gen_one(kind_of_segment(j->kind, s), j->seed * 1000003ull + s, j->buf + off, len);
+        size_t pos = s * SEG, len = j->end - pos < SEG ? j->end - pos : SEG;
+        gen_one(kind_of_segment(j->kind, s), j->seed * 1000003ull + s, j->buf + (pos - j->off), len);
     }
     return NULL;
 }
 
-/* Fill buf[0..n) with corpus `kind`. Returns n, or 0 on bad kind. */
-size_t lzb_datagen(int kind, uint64_t seed, uint8_t* buf, size_t n) {
-    if (kind < 0 || kind > LZB_DATA_BINARY) return 0;
+/* Corpus bytes [off, off + n) of `kind` (off a multiple of 16 MiB: a rank's share of a multi-GiB
+ * corpus without generating the bytes before it).  Returns n, or 0 on bad kind / offset. */
+size_t lzb_datagen_at(int kind, uint64_t seed, uint8_t* buf, size_t off, size_t n) {
+    if (kind < 0 || kind > LZB_DATA_BINARY || off % SEG) return 0;
     pthread_once(&g_vocab_once, vocab_once);
-    size_t nseg = (n + SEG - 1) / SEG;
+    size_t s0 = off / SEG, nseg = (n + SEG - 1) / SEG;
     int threads = nseg < 16 ? (int)nseg : 16;
     if (threads <= 1) {
-        seg_job j = { kind, seed, buf, n, 0, nseg };
+        seg_job j = { kind, seed, buf, off, off + n, s0, s0 + nseg };
         seg_worker(&j);
         return n;
     }
     pthread_t th[16];
     seg_job jobs[16];
     for (int t = 0; t < threads; t++) {
-        jobs[t] = (seg_job){ kind, seed, buf, n, nseg * (size_t)t / (size_t)threads, nseg * (size_t)(t + 1) / (size_t)threads };
+        jobs[t] = (seg_job){ kind, seed, buf, off, off + n, s0 + nseg * (size_t)t / (size_t)threads,
+                             s0 + nseg * (size_t)(t + 1) / (size_t)threads };
         pthread_create(&th[t], NULL, seg_worker, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     return n;
+}
+
+/* Fill buf[0..n) with corpus `kind`. Returns n, or 0 on bad kind. */
+size_t lzb_datagen(int kind, uint64_t seed, uint8_t* buf, size_t n) {
+    return lzb_datagen_at(kind, seed, buf, 0, n);
 }

@@ -42,6 +42,18 @@ WORKLOADS = [
     ("text", "lz4fast", 65536, 3, 1 << 30),
 ]
 SEED = 12345
+# multi-GPU workloads as one corpus cut into contiguous per-GPU shares (lzbench.cpp:366-373 cuts ONE
+# file into one chunk list; rank r of N owns share r): (corpus, codec, chunk, level, share bytes,
+# shares).  Each share is pinned on its own (offset = r x share: what rank r of bench.py compresses)
+# and the whole corpus by the digest of the shares' packed streams / compr_sizes concatenated (what
+# the host gather assembles): the north star at 1/2/4/8 GPUs (1 GiB of text per GPU), config 4
+# (8 GiB JSON, lz4 and snappy -b64) and config 5 (4 GiB mixed, zstd-1 -b128, 512 MiB per GPU).
+SHARED = [
+    ("text", "lz4", 65536, 1, 1 << 30, 8),
+    ("json", "lz4", 65536, 1, 1 << 30, 8),
+    ("json", "snappy", 65536, 0, 1 << 30, 8),
+    ("mixed", "zstd", 131072, 1, 512 << 20, 8),
+]
 
 
 def sha(*arrays) -> str:
@@ -49,6 +61,52 @@ def sha(*arrays) -> str:
     for a in arrays:
         h.update(np.ascontiguousarray(a).tobytes())
     return h.hexdigest()
+
+
+def entry_key(e):
+    return (e["corpus"], e["codec"], e["chunk"], e["level"], e["size"], e.get("offset", 0))
+
+
+def shared(out, path, only):
+    """share and aggregate digests of SHARED (entries carry "offset"; aggregates of the first 2, 4 and
+    all shares carry "shares": the whole corpus at 2, 4 and 8 GPUs)"""
+    have = {entry_key(e) for e in out}
+    for corpus, codec, chunk, level, share, nsh in SHARED:
+        if only and codec not in only:
+            continue
+        prefixes = [m for m in (2, 4, 8) if m <= nsh]
+        need = [(corpus, codec, chunk, level, share, r * share) for r in range(nsh)] + \
+               [(corpus, codec, chunk, level, share * m, 0) for m in prefixes]
+        if all(k in have for k in need):
+            continue
+        hp, hc, hin, tot = hashlib.sha256(), hashlib.sha256(), hashlib.sha256(), 0
+        for r in range(nsh):
+            data = L.datagen(corpus, share, seed=SEED, offset=r * share)
+            packed, cs = O.compress_chunks(data, codec, chunk, level, use_ref=True, threads=8)
+            hin.update(data.tobytes())
+            hp.update(packed.tobytes())
+            hc.update(cs.astype("<u8").tobytes())
+            tot += len(packed)
+            if (corpus, codec, chunk, level, share, r * share) not in have:
+                e = {"corpus": corpus, "size": share, "offset": r * share, "seed": SEED, "codec": codec,
+                     "chunk": chunk, "level": level, "input_sha256": sha(data), "packed_sha256": sha(packed),
+                     "csizes_sha256": sha(cs.astype("<u8")), "packed_bytes": int(len(packed)),
+                     "ratio_pct": round(100 * len(packed) / share, 3)}
+                print(e, flush=True)
+                out.append(e)
+                have.add(entry_key(e))
+            del data, packed, cs
+            m = r + 1
+            if m in prefixes and (corpus, codec, chunk, level, share * m, 0) not in have:
+                e = {"corpus": corpus, "size": share * m, "offset": 0, "shares": m, "seed": SEED, "codec": codec,
+                     "chunk": chunk, "level": level, "input_sha256": hin.copy().hexdigest(),
+                     "packed_sha256": hp.copy().hexdigest(), "csizes_sha256": hc.copy().hexdigest(),
+                     "packed_bytes": int(tot), "ratio_pct": round(100 * tot / (share * m), 3)}
+                print(e, flush=True)
+                out.append(e)
+                have.add(entry_key(e))
+            with open(path, "w") as f:
+                json.dump(out, f, indent=1)
 
 
 def main():
@@ -73,6 +131,7 @@ def main():
         out.append(e)
         with open(path, "w") as f:
             json.dump(out, f, indent=1)
+    shared(out, path, only)
 
 
 if __name__ == "__main__":
