@@ -82,8 +82,23 @@ def _fullsize():
         return json.load(f)
 
 
-@pytest.mark.parametrize("big", _fullsize(),
-                         ids=lambda b: f"{b['corpus']}{b['size'] >> 20}m-{b['codec']}{b['level']}-b{b['chunk'] >> 10}")
+def _per_gpu_sizes():
+    """the 1-GPU workloads and, of the multi-GPU corpora, the first and the last share (offset != 0: the bytes
+    rank r compresses); whole multi-GiB corpora: test_gpu_rows.py"""
+    out = []
+    for b in _fullsize():
+        if "shares" in b:
+            continue
+        if b.get("offset", 0) and b["offset"] + b["size"] < max(e.get("offset", 0) + e["size"] for e in _fullsize()
+                                                                 if (e["corpus"], e["codec"], e["chunk"]) ==
+                                                                 (b["corpus"], b["codec"], b["chunk"]) and "shares" not in e):
+            continue
+        out.append(b)
+    return out
+
+
+@pytest.mark.parametrize("big", _per_gpu_sizes(),
+                         ids=lambda b: f"{b['corpus']}{b['size'] >> 20}m@{b.get('offset', 0) >> 20}-{b['codec']}{b['level']}-b{b['chunk'] >> 10}")
 def test_full_size_vs_reference_digest(torch_cuda, big):
     """BASELINE sizes (1 GiB per GPU): the whole packed stream and every compr_size equal the
     reference chunk loop's (sha256 from tests/golden/make_fullsize.py), plus the size-independent
@@ -91,7 +106,7 @@ def test_full_size_vs_reference_digest(torch_cuda, big):
     the codec bound."""
     torch = torch_cuda
     n, chunk = big["size"], big["chunk"]
-    data = L.datagen(big["corpus"], n, seed=big["seed"])
+    data = L.datagen(big["corpus"], n, seed=big["seed"], offset=big.get("offset", 0))
     assert G.sha(data) == big["input_sha256"]
     d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda")
     d_in[:n].copy_(torch.from_numpy(data))

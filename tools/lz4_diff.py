@@ -1,5 +1,5 @@
 """tools/lz4_diff.py -- first differing LZ4 sequence between the HIP compressor and the oracle.
-usage: python tools/lz4_diff.py [corpus] [chunk_kib] [acc]"""
+usage: python tools/lz4_diff.py [corpus] [chunk_kib] [acc] [MiB] [seed]"""
 import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -35,11 +35,17 @@ corpus = sys.argv[1] if len(sys.argv) > 1 else "text"
 chunk = (int(sys.argv[2]) if len(sys.argv) > 2 else 64) << 10
 acc = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 codec = "lz4" if acc == 1 else "lz4fast"
-d = L.datagen(corpus, 1 << 20, 7)
+mib = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+seed = int(sys.argv[5]) if len(sys.argv) > 5 else 7
+d = L.datagen(corpus, mib << 20, seed)
 p, cs = L.compress_chunks(d, codec, chunk, acc)
-op, ocs = O.compress_chunks(d, codec, chunk, acc)
+op, ocs = O.compress_chunks(d, codec, chunk, acc, threads=16)
 bad = np.nonzero(cs != ocs)[0]
-print("bad chunks", bad[:10])
+if len(bad) == 0 and not (p == op).all():   # same sizes, different bytes
+    offs = np.concatenate([[0], np.cumsum(cs.astype(np.int64))])
+    first = int(np.nonzero(p != op)[0][0])
+    bad = np.array([int(np.searchsorted(offs, first, side="right") - 1)])
+print("bad chunks", len(bad), bad[:10])
 shown = 0
 for c in bad[:3]:
     go = int(np.sum(cs[:c])); oo = int(np.sum(ocs[:c]))
