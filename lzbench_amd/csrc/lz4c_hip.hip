@@ -1222,663 +1222,6 @@ lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, 
     }
 }
 
-// ======================================================================= two-wave parse (acc 1, byU16)
-// lzh_lz4_parse2_kernel: the parse of lzh_lz4_parse_kernel for LZ4_compress_default on chunks below
-// 65 547 bytes (byU16 table, acceleration 1: every batch but a long literal run's is a run batch) by a
-// workgroup of TWO waves sharing the chunk's one table and input ring, one barrier per batch:
-//   * the LOADER wave makes every table access (claims, restores) and every candidate load.  While the
-//     resolver resolves batch k, it prepares batch k+1 at base_k + 64 -- the next batch's base whenever the
-//     chain of batch k ends before base_k + 128 -- : P side, hash, table read, claim and read-back, slot
-//     groups, collider pre-evaluation, candidate windows, load wait, evaluation, and publishes it (LDS
-//     mailbox, two dwords per lane).  After the barrier it restores batch k's slots from I_k.
-//   * the RESOLVER wave runs the chain resolve of lz4.c:954-1200 over the published batch (compress_chunk's
-//     run-batch resolve), the parse state, the records, and the stride batches of long literal runs (then
-//     the loader idles and the resolver owns the table).
-// Batch k+1 reads the table BEFORE batch k's restore.  Every table write is the loader's, in the order
-// claim(k) -> [read k+1, claim k+1] -> restore(k) -> re-claim(k+1), so a batch-(k+1) lane that read a batch-k
-// position (the claim winner w of a slot batch k also hashed to: a "hot" lane; positions only grow) finds
-// the slot's final value only with I_k: the last inserted lane of w's slot group, else the slot's old value.
-// The loader evaluates both likely outcomes -- the group's top lane g inserted (window from the ring), or
-// none (the window batch k's lane w used, gathered) -- and the resolver, which holds I_k, picks: it walks
-// w's group down from g by batch k's prev links to its last inserted lane (a third lane: evaluated from the
-// ring there).  Every other lane's read is final.  After restore(k) the hot lanes write their claim winner
-// back, so the table again holds "finals, plus the claim winners of the batch being resolved".  A batch not
-// at base_k + 64 (a match of batch k reaching past base_k + 127, a stride batch next) is undone (every
-// claiming lane writes back the value it read) and built at the real base after the restore, behind a
-// second barrier.
-namespace lz4p2 {
-using namespace lz4v3;
-
-enum { kRun = 0, kStride = 1, kEnd = 2 };
-constexpr int kAhead2 = 640;     // ring refill target past the front: a refill never overwrites the bytes at
-                                 // or after front - 128 (the two batches in use are front - 64 .. front + 91)
-
-// s_barrier after this wave's LDS operations are complete (no vmcnt: loads / stores stay in flight)
-__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// mailbox words per lane (kRec: no catch-up lengths; the emission kernel computes them)
-//   w0: ok | len << 1 | okp << 6 | lep << 7 | valid << 12 | prev6 << 13 (prev, or the lane itself: none)
-//       | hot << 19 | g << 20 | okB << 26 | lenB << 27
-//   w1: cand | candB << 16   (hot lanes: cand = base_k + g, candB = the slot's old value)
-__device__ __forceinline__ uint32_t pack0(bool ok, int len, bool okp, int lep, bool valid, int prev6, bool hot, int g,
-                                          bool okB, int lenB) {
-    return (uint32_t)ok | ((uint32_t)len << 1) | ((uint32_t)okp << 6) | ((uint32_t)lep << 7) | ((uint32_t)valid << 12) |
-           ((uint32_t)prev6 << 13) | ((uint32_t)hot << 19) | ((uint32_t)g << 20) | ((uint32_t)okB << 26) |
-           ((uint32_t)lenB << 27);
-}
-
-// the candidate window [c-4, c+28) from the mirrored ring (d0 unused without catch-up)
-__device__ __forceinline__ void ring_window(const Ring& R, uint32_t c, MWin& W) {
-    const int X = (int)c + R.sh, A = (X & ~3) - 4;
-    const volatile LDSA uint32_t* r = (const volatile LDSA uint32_t*)R.w + ((A & (kRing - 1)) >> 2);
-    W.d0 = 0; W.d1 = r[1]; W.d2 = r[2]; W.d3 = r[3]; W.d4 = r[4]; W.d5 = r[5]; W.d6 = r[6]; W.d7 = r[7];
-    W.sm = X & 3;
-}
-
-// records of kRec (lzh_lz4_emit_kernel): P | (mlx << 24), (mlx >> 8) | (offset << 16), chunk order
-__device__ __forceinline__ void put_records(rsrc_t recs, int& nrec, uint64_t mem, int p, int mlx, uint32_t off) {
-    const uint64_t m = uni64(mem);
-    if (!m) return;
-    const int ri = nrec + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (lane_on(m)) st_b64(recs, 8 * ri, (uint32_t)p | ((uint32_t)mlx << 24), ((uint32_t)mlx >> 8) | (off << 16));
-    nrec = unii(nrec + __builtin_popcountll(m));
-}
-
-// LDS: table (16 KiB) | ring 1 KiB + 32 B mirror | mailbox 64 x 2 dwords | 16 control dwords:
-//   ctl[4 (i & 1) + 0..3] the resolver's verdict of iteration i: I lo, I hi, mode, next base
-//   ctl[8], ctl[9] ring fill / ready with the published batch; ctl[10] iterations whose mailbox is read
-// (kStats: phase clocks and events per wave into stats[0..31], tools/lz4_stats.py --parse2)
-#define P2CLK(i) do { if (kStats) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); clk[i] += t_ - clk_last; clk_last = t_; } } while (0)
-#define P2CNT(i) do { if (kStats) ev[i]++; } while (0)
-template <bool kStats>
-__device__ void parse2(const Bytes& in, int n, LDSA uint32_t* tab, LDSA uint32_t* ringw, LDSA uint32_t* mail,
-                       LDSA uint32_t* ctl, rsrc_t recs, uint32_t* rec_hdr, unsigned long long* stats) {
-    const int lane = threadIdx.x & 63;
-    const int wid = unii((int)(threadIdx.x >> 6));   // 0 resolver, 1 loader
-    volatile LDSA uint32_t* const vc = (volatile LDSA uint32_t*)ctl;
-    volatile LDSA uint32_t* const vm = (volatile LDSA uint32_t*)mail;
-    uint64_t clk[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t clk_last = kStats ? __builtin_amdgcn_s_memtime() : 0;
-    auto flush_stats = [&](int w) {
-        if (kStats && lane == 0) {
-            for (int i = 0; i < 8; i++) atomicAdd(&stats[8 * w + i], (unsigned long long)clk[i]);
-            for (int i = 0; i < 8; i++) atomicAdd(&stats[16 + 8 * w + i], (unsigned long long)ev[i]);
-        }
-    };
-    Table<true> T{tab};
-    {
-        LDSA uint32_t* t4 = (LDSA uint32_t*)tab;
-#pragma unroll
-        for (int i = 0; i < 8; i++) lds_zero16(t4 + 4 * (i * 128 + (int)threadIdx.x));
-        if (threadIdx.x < 16) vc[threadIdx.x] = 0;
-    }
-    if (n < kMinLength) {   // no search: the whole chunk is the last literals
-        if (threadIdx.x == 0) { rec_hdr[0] = 0; rec_hdr[1] = 0; }
-        return;
-    }
-    const int mfl1 = n - kMfLimit + 1;
-    const int mlimit = n - kLastLiterals;
-    const int endX = n + in.sh + 8;
-    wg_barrier();   // (the zeroed table and control words)
-
-    if (wid == 1) {
-        // ================================================================= loader
-        Ring R{ringw, in.sh, 0, 0, true, true};
-        for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
-        wait_vm();
-        R.ready = R.fill;
-        wave_lds_fence();
-        {   // the first position enters the table before the first search (lz4.c:922-923)
-            const uint32_t h0 = hash_of<true>(R.u32(0), 0);
-            if (lane == 0) T.put(h0, 0u);
-            wave_lds_fence();
-        }
-        // the batch being resolved (k): slots, resolved old values (the slots' values before it), slot
-        // groups and their top lanes, the windows of the old values
-        int c_base = 0, c_top = lane;
-        uint32_t c_h = 0, c_old = 0;
-        uint64_t c_grp = 0;
-        bool c_valid = false;
-        MWin Wold;
-        Wold.d0 = Wold.d1 = Wold.d2 = Wold.d3 = Wold.d4 = Wold.d5 = Wold.d6 = Wold.d7 = 0;
-        Wold.sm = 0;
-        // the batch prepared next (k+1); hot lanes: the batch-k lane w, the old value's window
-        int n_base = 0, n_w = lane;
-        uint32_t n_h = 0, n_v = 0, n_back = 0, n_cold = 0;
-        uint64_t n_grp = 0, n_hot = 0;
-        bool n_valid = false;
-        MWin n_W, n_Wb;
-
-        // batch at nb: P side, hash, table read, claim, read back, slot groups, collider pre-evaluation,
-        // candidate windows, evaluation; publish when `it` >= 0 (after the resolver has read iteration it's)
-        auto prepare = [&](int nb, bool spec, int it) {
-            n_base = nb;
-            const int p = nb + lane;
-            n_valid = p + 1 <= mfl1;                         // forwardIp <= mflimitPlusOne (lz4.c:969)
-            const uint64_t vmask = ballot(n_valid);
-            const int pmax = vmask ? nb + 63 - __builtin_clzll(vmask) : nb;
-            PSide ps;
-            if (R.has(nb - 4, pmax + 28)) ps = p_side_ring_m<false>(R, p);
-            else ps = p_side_global(in, p);
-            n_h = hash_of<true>(ps.w, 0);
-            n_v = T.get(n_h);
-            const bool hot = spec && n_valid && n_v - (uint32_t)c_base < 64u;
-            n_hot = ballot(hot);
-            n_W.load(in, n_v, n_valid && !hot);              // (issued before the claim round trip)
-            if (vmask == ~0ull) T.put(n_h, (uint32_t)p);
-            else if (n_valid) T.put(n_h, (uint32_t)p);
-            wave_lds_fence();
-            n_back = T.get(n_h);
-            const uint64_t losers = ballot(n_valid && n_back != (uint32_t)p);
-            uint64_t grp = 1ull << lane;
-            int prev = -1;
-            bool okp = false;
-            int lep = 0;
-            if (losers) {   // slot groups by the claim winner, bit-sliced (compress_chunk's run batch)
-                const uint64_t below = (1ull << lane) - 1ull;
-                const uint32_t W = n_back - (uint32_t)nb;
-                uint32_t ne0 = 0, ne1 = 0;
-#pragma unroll
-                for (int b = 0; b < 6; b++) {
-                    const uint64_t bm = ballot((W >> b) & 1u);
-                    const uint32_t mine = (uint32_t)__builtin_amdgcn_sbfe((int)W, b, 1);
-                    ne0 |= (uint32_t)bm ^ mine;
-                    ne1 |= (uint32_t)(bm >> 32) ^ mine;
-                }
-                const uint64_t ne = ((uint64_t)ne1 << 32) | ne0;
-                grp = n_valid ? (~ne & vmask) : (1ull << lane);
-                const uint64_t eb = grp & below;
-                prev = (n_valid && eb) ? 63 - __builtin_clzll(eb) : -1;
-                const int k = prev >= 0 ? prev : lane;
-                const uint32_t gw = lane_gather(ps.w, k), g0 = lane_gather(ps.q0, k), g1 = lane_gather(ps.q1, k),
-                               g2 = lane_gather(ps.q2, k), g3 = lane_gather(ps.q3, k), g4 = lane_gather(ps.q4, k);
-                lep = first_diff20(ps.q0 ^ g0, ps.q1 ^ g1, ps.q2 ^ g2, ps.q3 ^ g3, ps.q4 ^ g4);
-                okp = n_valid && gw == ps.w;
-            }
-            n_grp = grp;
-            // hot lanes: outcome A (the group's top lane g of batch k inserted: its position, window from the
-            // ring) and outcome B (no lane of the group inserted: the slot's old value, the window batch k's
-            // lane w used)
-            int g = 0;
-            bool okB = false;
-            int lenB = 0;
-            uint32_t cand = n_v;
-            MWin WA;
-            if (n_hot) {
-                if (kStats) P2CNT(2);
-                n_w = hot ? (int)(n_v - (uint32_t)c_base) : lane;
-                g = (int)lane_gather((uint32_t)c_top, n_w);
-                n_cold = lane_gather(c_old, n_w);
-                n_Wb.d0 = 0;
-                n_Wb.d1 = lane_gather(Wold.d1, n_w); n_Wb.d2 = lane_gather(Wold.d2, n_w);
-                n_Wb.d3 = lane_gather(Wold.d3, n_w); n_Wb.d4 = lane_gather(Wold.d4, n_w);
-                n_Wb.d5 = lane_gather(Wold.d5, n_w); n_Wb.d6 = lane_gather(Wold.d6, n_w);
-                n_Wb.d7 = lane_gather(Wold.d7, n_w); n_Wb.sm = (int)lane_gather((uint32_t)Wold.sm, n_w);
-                if (R.has(c_base - 4, c_base + LZH_WAVE + 28)) {
-                    ring_window(R, (uint32_t)(c_base + g), WA);
-                } else {   // (the ring does not reach back: after a jump of the front)
-                    WA.load(in, (uint32_t)(c_base + g), hot);
-                }
-                int bk_;
-                okB = eval_lane(ps, n_Wb, n_valid, bk_, lenB);
-                if (hot) cand = (uint32_t)(c_base + g);
-            }
-            wait_vm();                                        // the candidate windows (and older refills)
-            R.ready = R.fill;
-            wave_lds_fence();
-            {
-                const int target = min(nb + in.sh + kAhead2, endX + 256);
-                for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
-            }
-            int bkr, len;
-            const bool ok = eval_lane(ps, lane_on(n_hot) ? WA : n_W, n_valid, bkr, len);
-            const uint32_t w0 = pack0(ok, len, okp, lep, n_valid, prev >= 0 ? prev : lane, lane_on(n_hot), g, okB, lenB);
-            const uint32_t w1 = (cand & 0xffffu) | (n_cold << 16);
-            if (it >= 0) {   // the resolver has read iteration it's mailbox (it does so right after the barrier)
-                P2CLK(0);
-                for (int sp = 0; sp < (1 << 20); sp++) {
-                    if (unii((int)vc[10]) > it) break;
-                    if (kStats && sp == 0) P2CNT(3);
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                P2CLK(1);
-            }
-            vm[2 * lane] = w0;
-            vm[2 * lane + 1] = w1;
-            if (lane == 0) { vc[8] = (uint32_t)R.fill; vc[9] = (uint32_t)R.ready; }
-        };
-        // batch k+1 becomes the batch being resolved (hot lanes: their old value and its window from fin, the
-        // finals of batch k's slots)
-        auto advance = [&](const uint32_t* fin) {
-            if (fin && n_hot) {
-                const bool hot = lane_on(n_hot);
-                const uint32_t fw = lane_gather(*fin, n_w);
-                const bool inr = hot && fw >= (uint32_t)c_base;
-                MWin G;
-                if (ballot(inr)) {
-                    if (R.has(c_base - 4, c_base + LZH_WAVE + 28)) ring_window(R, inr ? fw : (uint32_t)c_base, G);
-                    else { G.load(in, fw, inr); wait_vm(); }
-                }
-                if (hot) {
-                    n_W = inr ? G : n_Wb;
-                    n_v = fw;
-                }
-            }
-            c_base = n_base; c_h = n_h; c_old = n_v; c_grp = n_grp; c_valid = n_valid; Wold = n_W;
-            c_top = 63 - __builtin_clzll(c_grp | (1ull << lane));
-        };
-
-        prepare(1, false, -1);
-        advance(nullptr);
-        int mode = kRun;
-        P2CLK(7);
-        wg_barrier();                                            // the first batch published
-        for (int it = 0;; it++) {
-            const bool have_nxt = mode == kRun && c_base + 64 < mfl1;
-            if (have_nxt) {                                      // batch k+1, speculatively at base_k + 64
-                P2CNT(0);
-                prepare(c_base + 64, true, it);
-            }
-            P2CLK(2);
-            wg_barrier();                                        // the resolver's verdict on batch k
-            P2CLK(3);
-            const int cb = 4 * (it & 1);
-            const uint64_t I = uni64(((uint64_t)vc[cb + 1] << 32) | vc[cb]);
-            const int nmode = unii((int)vc[cb + 2]), nbase = unii((int)vc[cb + 3]);
-            if (nmode == kEnd) break;
-            const bool spec = have_nxt && nmode == kRun && nbase == n_base;
-            uint32_t fin = 0;
-            if (mode == kRun) {   // each slot of batch k ends with its last inserted lane, else its old value
-                const uint64_t gi = c_grp & I;
-                fin = gi ? (uint32_t)(c_base + 63 - __builtin_clzll(gi)) : c_old;
-            }
-            if (have_nxt && !spec && n_valid) T.put(n_h, n_v);   // undo the speculative claims
-            if (mode == kRun && c_valid) T.put(c_h, fin);        // restore(k)
-            if (spec) {
-                if (lane_on(n_hot)) T.put(n_h, n_back);          // the claim winners back
-                wave_lds_fence();
-                advance(&fin);
-                P2CLK(4);
-            } else {
-                wave_lds_fence();
-                if (nmode == kRun) {
-                    P2CNT(1);
-                    prepare(nbase, false, -1);                   // (the resolver read iteration it's mailbox)
-                    advance(nullptr);
-                }
-                P2CLK(5);
-                wg_barrier();                                    // the rebuilt batch / the table for a stride batch
-                P2CLK(6);
-            }
-            mode = nmode;
-            R.fill = unii(R.fill); R.ready = unii(R.ready);
-            c_base = unii(c_base); n_base = unii(n_base);
-        }
-        flush_stats(0);
-        return;
-    }
-
-    // ===================================================================== resolver
-    int base = 1, q = 1, qlim = 64, pins = -1, so = 0, anchor = 0, s = 1, k0 = 0, nrec = 0, mode = kRun;
-    bool retest = false;
-    const int64_t a64 = 64;
-    int pbase = 0, pprev = -1;       // the previous run batch: base and slot-group links (hot lanes)
-    uint64_t pI = 0;                 // and its inserted lanes
-    P2CLK(7);
-    wg_barrier();                                                // the first batch published
-#ifdef LZH_P2PRIO
-    __builtin_amdgcn_s_setprio(LZH_P2PRIO);                      // (experiment: the resolver ahead throughout)
-#endif
-    for (int it = 0;; it++) {
-        Ring R{ringw, in.sh, 0, 0, true, true};
-        int nmode = kEnd, nbase = 0;
-        uint64_t I = 0;
-        uint64_t Mm = 0;                                         // run batch: its members, counts, candidates
-        int cn = 0, prev = -1;
-        uint32_t ce = 0;
-        const int rbase = base;
-        int sP = -1, sM = 0, scnt = 0;                          // stride batch: its sequence
-        R.fill = unii((int)vc[8]);
-        R.ready = unii((int)vc[9]);
-        if (mode == kRun) {
-            const uint32_t w0 = vm[2 * lane], w1 = vm[2 * lane + 1];
-            __builtin_amdgcn_s_waitcnt(0xC07F);              // lgkmcnt(0): the mailbox is in registers
-            if (lane == 0) vc[10] = (uint32_t)(it + 1);        // ... and may be overwritten
-            const bool okp = (w0 >> 6) & 1u, valid = (w0 >> 12) & 1u;
-            const int lep = (int)((w0 >> 7) & 31u);
-            const int prev6 = (int)((w0 >> 13) & 63u);
-            prev = prev6 == lane ? -1 : prev6;
-            bool ok = w0 & 1u;
-            int len = (int)((w0 >> 1) & 31u);
-            uint32_t cand = w1 & 0xffffu;
-            const uint64_t hotm = ballot((w0 >> 19) & 1u);
-            const int p = base + lane;
-            if (hotm) {   // hot lanes: the last inserted lane of the group in the previous batch
-                if (kStats) P2CNT(2);
-                const bool hot = lane_on(hotm);
-                const int g = (int)((w0 >> 20) & 63u);
-                int x = hot ? g : -1;
-                for (int i = 0; i < LZH_WAVE; i++) {
-                    const bool m = x >= 0 && !((pI >> x) & 1ull);
-                    if (!ballot(m)) break;
-                    const int xp = (int)lane_gather((uint32_t)pprev, m ? x : lane);
-                    x = m ? xp : x;
-                }
-                const bool useB = hot && x < 0, other = hot && x >= 0 && x != g;
-                if (useB) {
-                    ok = (w0 >> 26) & 1u;
-                    len = (int)(w0 >> 27);
-                    cand = w1 >> 16;
-                }
-                if (ballot(other)) {   // (rare) another lane of the group: evaluated from the ring
-                    if (kStats) P2CNT(3);
-                    MWin W;
-                    PSide ps;
-                    if (R.has(pbase - 4, base + LZH_WAVE + 28)) {
-                        ps = p_side_ring_m<false>(R, p);
-                        ring_window(R, (uint32_t)(pbase + (other ? x : 0)), W);
-                    } else {
-                        ps = p_side_global(in, p);
-                        W.load(in, (uint32_t)(pbase + (other ? x : 0)), true);
-                        wait_vm();
-                    }
-                    int bk_, l_;
-                    const bool o_ = eval_lane(ps, W, valid, bk_, l_);
-                    if (other) {
-                        ok = o_;
-                        len = l_;
-                        cand = (uint32_t)(pbase + x);
-                    }
-                }
-            }
-            P2CLK(0);
-            // ================= run batch: resolve every sequence that starts in the batch (compress_chunk)
-#ifndef LZH_P2PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
-            const uint64_t below = (1ull << lane) - 1ull;
-            const uint64_t vmask = ballot(valid);
-            const int fv = __builtin_popcountll(vmask);
-            const uint64_t coll = ballot(prev >= 0);
-            const uint64_t I0 = pins >= 0 ? (1ull << (pins - base)) : 0ull;
-            const int lo = q - base, hi0 = min(qlim - base, LZH_WAVE - 1);
-            const uint64_t P0 = lane_bits(lo, hi0);
-            int ak = prev;
-            bool oke = prev >= 0 ? okp : ok;
-            ce = prev >= 0 ? (uint32_t)(base + prev) : cand;
-            int le = prev >= 0 ? lep : len;
-            uint64_t E = 0;
-            I = I0;
-            int e = 0, eL = 0;
-            bool endp = false;
-            PSide ps;
-            bool have_ps = false;
-            for (int round = 0; round <= LZH_WAVE; round++) {
-                const uint64_t A = ballot(oke);
-                cn = min(le, mlimit - (p + kMinMatch));
-                const bool lng = oke && le == 20 && p + kMinMatch + 20 < mlimit;
-                e = lane + kMinMatch + cn;
-                const int f = ctz64v(e < LZH_WAVE ? (A & (~0ull << e)) : 0ull);
-                Mm = 0;
-                endp = false;
-                const uint64_t r0 = A & P0;
-                if (!r0) {
-                    E = P0;
-                    endp = hi0 >= fv;                            // ran past mflimit (lz4.c:969)
-                } else {
-                    int sl = __builtin_ctzll(r0);
-                    bool endip = false;
-                    const int link = (lng || p + kMinMatch + cn >= mfl1) ? 0x80 : f;
-                    for (;;) {
-                        int fs;
-                        for (;;) {
-                            Mm |= 1ull << sl;
-                            fs = rdlanei(link, sl);
-                            if (fs >= LZH_WAVE) break;
-                            sl = fs;
-                        }
-                        if (fs != 0x80) break;
-                        int es;
-                        if (rdlane((uint32_t)lng, sl)) {         // match runs past the window
-                            const int c = slow_count(in, base + sl, rdlanei((int)ce, sl), mlimit, lane);
-                            es = sl + kMinMatch + c;
-                            cn = lane == sl ? c : cn;
-                            e = lane == sl ? es : e;
-                            fs = ctz64v(es < LZH_WAVE ? (A & (~0ull << es)) : 0ull);
-                        } else {
-                            es = rdlanei(e, sl);
-                        }
-                        if (base + es >= mfl1) { endip = true; break; }   // lz4.c:1142
-                        if (fs >= LZH_WAVE) break;
-                        sl = fs;
-                    }
-                    eL = rdlanei(e, sl);
-                    const uint64_t mle = Mm & (below | (1ull << lane));
-                    const int j = mle ? 63 - __builtin_clzll(mle) : lane;
-                    const int ej = (int)lane_gather((uint32_t)e, j);
-                    const bool inside = mle && lane > j && lane < ej;
-                    const bool probed = lane >= lo && !inside;
-                    E = ballot(probed && (!endip || lane < eL));
-                    I = ballot(mle && lane == ej - 2);           // lz4.c:1146
-                    endp = endip || (eL < LZH_WAVE && LZH_WAVE - 1 >= fv);
-                }
-                I = (Mm ? I : 0ull) | I0 | E;
-                if (!(coll & E)) break;
-                // each collider's candidate: the latest earlier lane of its slot that is inserted (the
-                // slot-group chain by prev)
-                int kt = prev;
-                for (int i = 0; i < LZH_WAVE; i++) {
-                    const bool m = kt >= 0 && !((I >> kt) & 1ull);
-                    if (!ballot(m)) break;
-                    const int kp = (int)lane_gather((uint32_t)prev, m ? kt : lane);
-                    kt = m ? kp : kt;
-                }
-                const bool fix = lane_on(E) && kt != ak;
-                if (!ballot(fix)) break;
-                const bool far = fix && kt >= 0 && kt != prev;
-                if (fix) {
-                    ak = kt;
-                    oke = kt < 0 ? ok : okp;
-                    ce = kt < 0 ? cand : (uint32_t)(base + kt);
-                    le = kt < 0 ? len : lep;
-                }
-                if (ballot(far)) {                               // an older member than prev
-                    if (!have_ps) {
-                        if (R.has(base - 4, base + LZH_WAVE + 28)) ps = p_side_ring_m<false>(R, p);
-                        else ps = p_side_global(in, p);
-                        have_ps = true;
-                    }
-                    const int k = far ? kt : lane;
-                    const uint32_t gw = lane_gather(ps.w, k), g0 = lane_gather(ps.q0, k), g1 = lane_gather(ps.q1, k),
-                                   g2 = lane_gather(ps.q2, k), g3 = lane_gather(ps.q3, k), g4 = lane_gather(ps.q4, k);
-                    if (far) {
-                        le = first_diff20(ps.q0 ^ g0, ps.q1 ^ g1, ps.q2 ^ g2, ps.q3 ^ g3, ps.q4 ^ g4);
-                        oke = valid && gw == ps.w;
-                    }
-                }
-            }
-            // ---- the parse state after the batch
-            if (endp) {
-                nmode = kEnd;
-                if (Mm) anchor = base + eL;
-            } else {
-                if (Mm) {
-                    const int ip = base + eL;
-                    anchor = ip;
-                    so = ip;
-                    qlim = ip + 64;
-                    if (eL < LZH_WAVE) { q = base + LZH_WAVE; pins = -1; }
-                    else { q = ip; pins = eL - 2 >= LZH_WAVE ? ip - 2 : -1; }
-                } else {
-                    q = base + hi0 + 1;
-                    pins = -1;
-                }
-                if (!Mm && hi0 == qlim - base) {                 // 64 probes done: stride batches
-                    nmode = kStride;
-                    s = so + 1;
-                    k0 = LZH_WAVE;
-                    retest = false;
-                } else {
-                    nmode = kRun;
-                    // the loader's speculative base + 64 serves when the next probe and the ip-2 fill lie in it
-                    const int bs = base + LZH_WAVE;
-                    nbase = (q >= bs && q < bs + LZH_WAVE && (pins < 0 || pins >= bs)) ? bs : (pins >= 0 ? pins : q);
-                }
-            }
-#ifndef LZH_P2PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
-            P2CLK(1);
-        } else {
-            // ================= stride batch (long literal run: step > 1): the resolver alone, first sequence only
-            int64_t pp, nxt;
-            if (retest && lane == 0) {
-                pp = s - 1;
-                nxt = s;
-            } else {
-                const int k = retest ? lane - 1 : k0 + lane;
-                const int64_t o = k == 0 ? 0 : 1 + step_prefix(a64 + k - 1) - step_prefix(a64);
-                const int64_t st = k == 0 ? 1 : (a64 + k - 1) >> 6;
-                pp = (int64_t)s + o;
-                nxt = pp + st;
-            }
-            const bool valid = nxt <= mfl1;
-            const int p = valid ? (int)pp : 0;
-            const uint64_t vmask = ballot(valid);
-            const int front = rdlanei(p, 0);
-            const int pmax = vmask ? rdlanei(p, 63 - __builtin_clzll(vmask)) : front;
-            PSide ps = R.has(front - 4, pmax + 28) ? p_side_ring_m<false>(R, p) : p_side_global(in, p);
-            const uint32_t h = hash_of<true>(ps.w, 0);
-            const uint32_t old = T.get(h);
-            uint32_t cand = old;
-            MWin W;
-            W.load(in, cand, valid);
-            if (valid) T.put(h, (uint32_t)p);
-            wave_lds_fence();
-            const uint32_t back = T.get(h);
-            const uint64_t losers = ballot(valid && back != (uint32_t)p);
-            wait_vm();
-            int bkr, len;
-            bool ok = eval_lane(ps, W, valid, bkr, len);
-            uint64_t hits = ballot(ok);
-            const uint64_t tmask = ballot(!valid);
-            const int fi = ffs64(tmask);
-            int fh = ffs64(hits);
-            bool found = hits != 0;
-            int L = found ? fh : fi - 1;
-            uint64_t upto = L < 0 ? 0ull : (L >= 63 ? ~0ull : ((2ull << L) - 1ull));
-            if (!(losers & upto)) {
-                if (valid && lane > L && back == (uint32_t)p) T.put(h, old);
-            } else {   // lanes up to L sharing a slot: each sees the previous lane of its slot
-                if (valid) T.put(h, old);
-                wave_lds_fence();
-                uint64_t grp;
-                int prv;
-                slot_groups(h, valid, losers, grp, prv, lane);
-                const uint32_t ppos = lane_gather((uint32_t)p, prv < 0 ? lane : prv);
-                if (prv >= 0) cand = ppos;
-                W.load(in, cand, valid);
-                wait_vm();
-                ok = eval_lane(ps, W, valid, bkr, len);
-                hits = ballot(ok);
-                fh = ffs64(hits);
-                found = hits != 0;
-                L = found ? fh : fi - 1;
-                upto = L < 0 ? 0ull : (L >= 63 ? ~0ull : ((2ull << L) - 1ull));
-                if (valid && lane <= L) {
-                    const uint64_t later = grp & ~((2ull << lane) - 1ull) & upto;
-                    if (!later) T.put(h, (uint32_t)p);
-                }
-            }
-            wave_lds_fence();
-            if (!found) {
-                if (tmask) nmode = kEnd;                         // ran past mflimit
-                else {
-                    nmode = kStride;
-                    if (retest) { retest = false; k0 = LZH_WAVE - 1; }
-                    else k0 += LZH_WAVE;
-                }
-            } else {
-                const int P = rdlanei(p, fh);
-                const int M = rdlanei((int)cand, fh);
-                int cnt;
-                (void)finish_match<false>(in, P, M, 0, rdlanei(len, fh), anchor, mlimit, cnt, lane, nullptr);
-                sP = P; sM = M; scnt = cnt;
-                const int ip = P + kMinMatch + cnt;
-                anchor = ip;
-                if (ip >= mfl1) {
-                    nmode = kEnd;
-                } else {                                         // back to run batches (the ip-2 fill first)
-                    nmode = kRun;
-                    pins = ip - 2;
-                    nbase = ip - 2;
-                    q = ip;
-                    so = ip;
-                    qlim = ip + 64;
-                }
-            }
-            P2CLK(2);
-        }
-        if (kStats) { if (mode == kRun) P2CNT(0); else P2CNT(1); }
-        if (it > 4 * n + 64) nmode = kEnd;
-        const int cb = 4 * (it & 1);
-        if (lane == 0) {
-            vc[cb] = (uint32_t)I;
-            vc[cb + 1] = (uint32_t)(I >> 32);
-            vc[cb + 2] = (uint32_t)nmode;
-            vc[cb + 3] = (uint32_t)nbase;
-        }
-        wg_barrier();                                            // the verdict on this batch
-        P2CLK(3);
-        // ---- records (under the loader's restore and its next batch)
-        if (mode == kRun) put_records(recs, nrec, Mm, rbase + lane, cn, (uint32_t)(rbase + lane) - ce);
-        else if (sP >= 0) put_records(recs, nrec, 1ull, sP, scnt, (uint32_t)(sP - sM));
-        P2CLK(4);
-        if (nmode == kEnd) break;
-        // (the loader prepared base + 64 when this was a run batch with valid lanes there)
-        const bool spec = mode == kRun && base + 64 < mfl1 && nmode == kRun && nbase == base + 64;
-        if (!spec) {
-            wg_barrier();                                        // the rebuilt batch / the restored table
-            P2CLK(5);
-        }
-        pI = mode == kRun ? I : 0ull;
-        pprev = prev;
-        pbase = rbase;
-        mode = unii(nmode);
-        base = unii(nbase);
-        q = unii(q); qlim = unii(qlim); pins = unii(pins); so = unii(so); anchor = unii(anchor);
-        s = unii(s); k0 = unii(k0); retest = unii(retest) != 0;
-    }
-    if (lane == 0) { rec_hdr[0] = (uint32_t)nrec; rec_hdr[1] = (uint32_t)anchor; }
-    flush_stats(1);
-}
-
-}  // namespace lz4p2
-
-// (5 waves per SIMD: 9 workgroups of 2 waves per CU need 4.5; the VGPR budget is then 96)
-extern "C" __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(5, 8)))
-lzh_lz4_parse2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
-                      uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint64_t frame_size, uint32_t bpf,
-                      unsigned long long* stats) {
-    // table | ring + mirror | mailbox | control words: 18 016 bytes, 9 workgroups (18 waves) per CU
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + 8 + 128 + 16];
-    const uint64_t chunk = blockIdx.x;
-    uint64_t off;
-    int n;
-    if (!block_span(chunk, n_total, chunk_size, frame_size, bpf, off, n)) return;
-    if (n >= 65547) return;   // (the launcher takes byU16 chunks only)
-    const uint64_t readable = min<uint64_t>(in_readable - off, (uint64_t)n + 64);
-    Bytes rin;
-    rin.init(in + off, readable);
-    LDSA uint32_t* tab = (LDSA uint32_t*)lds;
-    LDSA uint32_t* ring = tab + 4096;
-    LDSA uint32_t* mail = ring + lz4v3::kRing / 4 + 8;
-    LDSA uint32_t* ctl = mail + 128;
-    const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
-    if (stats) lz4p2::parse2<true>(rin, n, tab, ring, mail, ctl, rr, rec_hdr + 2 * chunk, stats);
-    else lz4p2::parse2<false>(rin, n, tab, ring, mail, ctl, rr, rec_hdr + 2 * chunk, nullptr);
-}
-
 namespace lz4e {
 
 constexpr int kRingB = 2048;            // LDS output ring (bytes)
@@ -2216,9 +1559,6 @@ lzh_lz4f_linked_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable
 
 #endif
 #include "launch.h"
-#ifndef LZH_LZ4_PARSE2
-#define LZH_LZ4_PARSE2 0      // the two-wave parse (measured slower: profiles/r05_a/notes.txt)
-#endif
 size_t lzh_lz4_rec_stride(uint64_t chunk_size) { return ((chunk_size / 4 + 4) * 8 + 255) / 256 * 256; }
 
 hipError_t lzh_launch_lz4_compress_v2(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
@@ -2239,10 +1579,7 @@ hipError_t lzh_launch_lz4_split(const uint8_t* in, uint64_t n_total, uint64_t in
     if (bpf <= 1) { bpf = 1; frame_size = chunk_size; }
     const uint64_t rs = lzh_lz4_rec_stride(chunk_size);
     uint32_t* hdr = (uint32_t*)(recs + rs * nchunks);
-    if ((stage_mask & 1) && LZH_LZ4_PARSE2 && acc == 1 && chunk_size < 65547)   // (byU16, acceleration 1)
-        hipLaunchKernelGGL(lzh_lz4_parse2_kernel, dim3(nchunks), dim3(128), 0, s, in, n_total, in_readable, chunk_size,
-                           recs, rs, hdr, frame_size, bpf, (unsigned long long*)nullptr);
-    else if (stage_mask & 1)
+    if (stage_mask & 1)
         hipLaunchKernelGGL(lzh_lz4_parse_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable, chunk_size,
                            acc, recs, rs, hdr, frame_size, bpf);
     if (stage_mask & 2)
@@ -2272,17 +1609,5 @@ extern "C" int lzh_debug_lz4_stats(const void* d_in, uint64_t n, uint64_t in_rea
     hipLaunchKernelGGL(lzh_lz4_compress_stats_kernel, dim3((unsigned)k), dim3(64), 0, (hipStream_t)stream,
                        (const uint8_t*)d_in, n, in_readable, chunk_size, acc, (uint8_t*)d_stage, stride, d_csizes, 0u,
                        d_stats);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-// debug: the two-wave parse with phase clocks (stats: 32 x u64; tools/lz4_stats.py --parse2)
-extern "C" int lzh_debug_parse2_stats(const void* d_in, uint64_t n, uint64_t in_readable, uint64_t chunk_size,
-                                      void* d_recs, unsigned long long* d_stats, void* stream) {
-    const uint64_t k = (n + chunk_size - 1) / chunk_size;
-    if (chunk_size >= 65547) return -1;
-    const uint64_t rs = lzh_lz4_rec_stride(chunk_size);
-    hipLaunchKernelGGL(lzh_lz4_parse2_kernel, dim3((unsigned)k), dim3(128), 0, (hipStream_t)stream, (const uint8_t*)d_in, n,
-                       in_readable, chunk_size, (uint8_t*)d_recs, rs, (uint32_t*)((uint8_t*)d_recs + rs * k), chunk_size,
-                       1u, d_stats);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -9,35 +9,6 @@ f.restype = C.c_int
 f.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
 names = ["batches", "collision_batches", "slow_colliders", "sequences", "-", "catchup_slow", "count_slow", "-",
          "-", "hash_ring_miss", "-", "-", "refills", "-", "-", "-"]
-if "--parse2" in sys.argv:   # the two-wave parse kernel's phase clocks (per wave) and events
-    g = lib.lzh_debug_parse2_stats
-    g.restype = C.c_int
-    g.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
-    for corpus in [a for a in sys.argv[1:] if a != "--parse2"] or ["text", "json"]:
-        n = int(os.environ.get("STATS_MIB", "512")) << 20
-        host = L.datagen(corpus, n, seed=12345)
-        d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda"); d_in[:n].copy_(torch.from_numpy(host))
-        k = n // 65536
-        rs = ((65536 // 4 + 4) * 8 + 255) // 256 * 256
-        recs = torch.zeros(rs * k + 8 * k + 256, dtype=torch.uint8, device="cuda")
-        st = torch.zeros(32, dtype=torch.int64, device="cuda")
-        assert g(d_in.data_ptr(), n, d_in.numel(), 65536, recs.data_ptr(), st.data_ptr(),
-                 torch.cuda.current_stream().cuda_stream) == 0
-        torch.cuda.synchronize()
-        v = st.cpu().tolist()
-        lc = ["prepare", "mailbox spin", "(to barrier)", "wait barrier", "restore+advance", "non-spec: undo/restore/prepare",
-              "wait extra barrier", "init"]
-        rc = ["mailbox+hot select", "run resolve", "stride batch", "wait barrier", "records", "wait extra barrier", "-",
-              "init"]
-        for w, names in ((0, lc), (1, rc)):
-            tot = sum(v[8 * w:8 * w + 8]) or 1
-            print(corpus, "loader" if w == 0 else "resolver", "clocks/chunk %.0f:" % (tot / k),
-                  {names[i]: "%.1f%%" % (100 * v[8 * w + i] / tot) for i in range(8) if names[i] != "-"})
-        le = ["spec prepares", "non-spec prepares", "hot batches", "mailbox spins"]
-        re_ = ["run batches", "stride batches", "hot batches", "third-lane evals"]
-        print(corpus, "loader events/chunk", {le[i]: round(v[16 + i] / k, 1) for i in range(4)})
-        print(corpus, "resolver events/chunk", {re_[i]: round(v[24 + i] / k, 1) for i in range(4)})
-    sys.exit(0)
 for corpus in sys.argv[1:] or ["text", "json"]:
     n = int(os.environ.get("STATS_MIB", "512")) << 20
     host = L.datagen(corpus, n, seed=12345)
