@@ -25,6 +25,14 @@
 namespace snv2 {
 
 #define SN_STAT(i, v) do { if (stats && lane == 0) atomicAdd(&stats[i], (unsigned long long)(v)); } while (0)
+// phase clocks of the run batches (experiment builds with -DLZH_SN_CLK; tools/sn_clk.py): the time since the
+// previous mark is charged to phase i, flushed per fragment into lzh_sn_clk_buf
+#ifdef LZH_SN_CLK
+__device__ unsigned long long lzh_sn_clk_buf[16];
+#define SN_CLK(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); snclk[i] += t_ - snclk_last; snclk_last = t_; } while (0)
+#else
+#define SN_CLK(i) ((void)0)
+#endif
 
 constexpr int kRing = 1024;
 constexpr int kAhead = 704;
@@ -368,6 +376,10 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
 
     int next_emit = 0;
     SREC_DECL;
+#ifdef LZH_SN_CLK
+    uint64_t snclk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t snclk_last = __builtin_amdgcn_s_memtime();
+#endif
     if (fn >= 15) {
         const int ip_limit = fn - 15;
         // run-batch state: batch base, search origin, pending re-test (-1: none)
@@ -425,9 +437,11 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 wave_lds_fence();
                 const uint32_t back = T.get(h);
                 const uint64_t losers = ballot(back != (uint32_t)p);
+                SN_CLK(0);
                 SREC_OUT();
                 rc_m = 0;
                 rc_tot = 0;
+                SN_CLK(1);
                 // (the slot groups and the collider pre-evaluation need no candidate bytes: they
                 // run under the candidate loads)
                 // slot groups: every lane of a slot read back the same claim winner
@@ -457,9 +471,11 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                                        lane_gather(ps.q4, k), lane_gather(ps.q5, k));
                     okp = gw == ps.w;
                 }
+                SN_CLK(2);
                 wait_vm();
                 R.ready = R.fill;
                 wave_lds_fence();
+                SN_CLK(3);
                 {
                     const int target = min(base + in.sh + kAhead, endX + 256);
                     for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
@@ -567,6 +583,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                         if (far) { le = lf; oke = gw == ps.w; }
                     }
                 }
+                SN_CLK(4);
                 // ---- records (literal from the previous copy's end, or next_emit)
                 if (Mm) {
                     SN_STAT(3, __builtin_popcountll(Mm));
@@ -597,6 +614,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     }
                     next_emit = base + eL;
                 }
+                SN_CLK(5);
                 if (endp) break;                                         // remainder from next_emit
                 // table: the last inserted lane of each slot, or the slot's old value
                 {   // every lane stores its slot's final value, all lanes of a slot agreeing (a run
@@ -619,9 +637,11 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     rt = -1;
                     base += LZH_WAVE;
                 }
+                SN_CLK(6);
                 continue;
             }
 
+            SN_CLK(6);
             // ================= search batch (sparse probes or near ip_limit): the probe plan
             // along the exact schedule, first hit only (v2)
             // ---- probe plan
@@ -827,8 +847,15 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
             runm = true;
             base = rt - 1;
             org = rt + 1;
+            SN_CLK(7);
         }
     }
+#ifdef LZH_SN_CLK
+    SN_CLK(7);
+    if (lane == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(&lzh_sn_clk_buf[i], (unsigned long long)snclk[i]);
+    if (lane == 0) atomicAdd(&lzh_sn_clk_buf[8], 1ull);
+#endif
     SREC_OUT();
     if (kRec) {   // the fragment's last literal run: a literal-only record
         if (next_emit < fn) {
@@ -1285,3 +1312,14 @@ hipError_t lzh_launch_snappy_compress_v2(const uint8_t* in, uint64_t n_total, ui
                        chunk_size, stage, stride, csizes, 0u, (unsigned long long*)nullptr);
     return hipGetLastError();
 }
+
+#ifdef LZH_SN_CLK
+extern "C" int lzh_debug_snappy_clocks(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(snv2::lzh_sn_clk_buf), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(snv2::lzh_sn_clk_buf), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

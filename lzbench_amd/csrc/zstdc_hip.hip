@@ -891,7 +891,9 @@ __device__ __forceinline__ void fse_encode(BitW<Sink>& b, const LDSA Fse& ct, ui
 }
 
 // ---- Huffman (huf_compress.c), lane 0 only
-__device__ __forceinline__ uint32_t huf_bucket(uint32_t c) { return c < 166 ? c : hb32(c) + 158; }
+// (RANK_POSITION_DISTINCT_COUNT_CUTOFF, huf_compress.c:455, is 158 + BIT_highbit32(158) = 165: bucket 165
+// holds counts 165..255 and is sorted like the other log2 buckets)
+__device__ __forceinline__ uint32_t huf_bucket(uint32_t c) { return c < 165 ? c : hb32(c) + 158; }
 __device__ __forceinline__ HNode hget(const LDSA HNode* a) {
     HNode t;
     t.count = a->count; t.parent = a->parent; t.byte = a->byte; t.nb = a->nb;
@@ -1009,7 +1011,7 @@ __device__ uint32_t huf_build(LDSA Lds& L, uint32_t maxs, uint32_t maxNb) {
             node[p].count = L.cnt[s];
             node[p].byte = (uint8_t)s;
         }
-        for (uint32_t b = 166; b < 191; b++) {
+        for (uint32_t b = 165; b < 191; b++) {
             const uint32_t sz = (uint32_t)cur[b] - base[b];
             if (sz > 1) huf_qsort(node + base[b], 0, (int)sz - 1, L.qs);
         }

@@ -348,9 +348,11 @@ static void fse_encode(bitw* b, const fse_ct* ct, u32* state, u32 sym) {   /* FS
 typedef struct { u32 count; u16 parent; u8 byte; u8 nbBits; } hnode;
 typedef struct { u8 nb[256]; u16 val[256]; u32 tlog; } huf_ct;
 
-/* sort symbols by decreasing count: buckets per distinct small count, log2 buckets above 166,
- * each log2 bucket quick-sorted (HUF_sort / HUF_simpleQuickSort, huf_compress.c:460-595) */
-static u32 huf_bucket(u32 c) { return c < 166 ? c : hb32(c) + 158; }
+/* sort symbols by decreasing count: buckets per distinct small count, log2 buckets from 165 on,
+ * each log2 bucket quick-sorted (HUF_sort / HUF_simpleQuickSort, huf_compress.c:460-595).  The cutoff
+ * RANK_POSITION_DISTINCT_COUNT_CUTOFF (huf_compress.c:455) is 158 + BIT_highbit32(158) = 165, not the 166
+ * its comment states: bucket 165 holds counts 165..255 and is sorted */
+static u32 huf_bucket(u32 c) { return c < 165 ? c : hb32(c) + 158; }
 static void hn_swap(hnode* a, hnode* b) { hnode t = *a; *a = *b; *b = t; }
 static void huf_isort(hnode* a, int lo, int hi) {
     const int size = hi - lo + 1;
@@ -390,7 +392,7 @@ static void huf_sort(hnode* node, const u32* cnt, u32 maxs) {
         node[p].count = cnt[s];
         node[p].byte = (u8)s;
     }
-    for (u32 b = 166; b < 191; b++) {
+    for (u32 b = 165; b < 191; b++) {
         const u32 sz = (u32)cur[b] - base[b];
         if (sz > 1) huf_qsort(node + base[b], 0, (int)sz - 1);
     }

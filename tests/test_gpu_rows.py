@@ -68,6 +68,30 @@ def test_eight_shards_north_star_digest(torch_cuda):
     assert (out == data).all()
 
 
+def _whole_corpora():
+    import json
+    return [e for e in json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize.json")))
+            if e.get("shares") == 8]
+
+
+@pytest.mark.parametrize("big", _whole_corpora(),
+                         ids=lambda b: f"{b['corpus']}{b['size'] >> 30}g-{b['codec']}{b['level']}-b{b['chunk'] >> 10}")
+def test_eight_shards_whole_corpus_digest(torch_cuda, big):
+    """BASELINE.json's 8-GPU workloads as stated -- config 4: 8 GiB of JSON logs, lz4 and snappy -b64; config 5:
+    4 GiB mixed, zstd-1 -b128; and the north star's 8 x 1 GiB text -- as ONE corpus, one lzbench chunk list
+    (lzbench.cpp:366-373), through the -g8 product path on one device (8 logical shards, api.cpp make_plan):
+    the whole packed stream and compr_sizes equal the reference chunk loop's digest of the whole corpus
+    (make_fullsize.py SHARED), and the 8-shard decode round-trips."""
+    import hashlib
+    data = L.datagen(big["corpus"], big["size"], seed=big["seed"])
+    packed, cs = L.compress_chunks(data, big["codec"], big["chunk"], big["level"], ngpus=8)
+    assert len(packed) == big["packed_bytes"]
+    assert hashlib.sha256(cs.astype("<u8").tobytes()).hexdigest() == big["csizes_sha256"]
+    assert hashlib.sha256(packed.tobytes()).hexdigest() == big["packed_sha256"]
+    out = L.decompress_chunks(packed, cs, len(data), big["codec"], big["chunk"], ngpus=8)
+    assert (out == data).all()
+
+
 @pytest.mark.parametrize("codec", ["lz4", "snappy"])
 def test_single_chunk_whole_input_row(torch_cuda, codec):
     """lzbench without -b: one chunk = the whole file (chunk_size clamped to the file size).

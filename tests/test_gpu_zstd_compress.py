@@ -120,3 +120,14 @@ def test_unsupported_level_rejected(torch_cuda):
     d_in = torch.zeros((1 << 20) + 256, dtype=torch.uint8, device="cuda")
     with pytest.raises(RuntimeError):
         dc.compress(d_in)
+
+
+def test_huffman_sort_cutoff_chunk(torch_cuda):
+    """The GPU Huffman build quick-sorts the same HUF_sort regions as the reference (cutoff 165,
+    huf_compress.c:455): chunk 11359 of the 4 GiB config-5 corpus, whose nine symbols of count 164 the
+    reference reorders (tests/test_zstd_oracle.py::test_huffman_sort_cutoff_equals_reference)."""
+    import test_zstd_oracle as T
+    d = T.mixed_chunk_11359()
+    packed, cs = L.compress_chunks(d, "zstd", 131072, 1)
+    ep, ecs = O.compress_chunks(d, "zstd", 131072, 1)
+    assert (cs == ecs).all() and len(packed) == len(ep) and (packed == ep).all()

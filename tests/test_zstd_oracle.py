@@ -61,3 +61,26 @@ def test_restatement_equals_reference_on_random_slices(level):
         a, ca = O.compress_chunks(data, "zstd", chunk, level, use_ref=False)
         b, cb = O.compress_chunks(data, "zstd", chunk, level, use_ref=True)
         assert (ca == cb).all() and a.tobytes() == b.tobytes(), (n, chunk, level)
+
+
+
+def mixed_chunk_11359():
+    """chunk 11359 (128 KiB) of the 4 GiB seed-12345 mixed corpus (config 5): its literal histogram has nine
+    symbols of count 164, which HUF_sort's bucket loop quick-sorts (huf_compress.c:585-592: the loop starts at
+    RANK_POSITION_DISTINCT_COUNT_CUTOFF = 158 + BIT_highbit32(158) = 165, and region 165 holds the symbols of
+    count 164); the quicksort reorders the tie, and two of the nine straddle the depth-9 / depth-10 boundary"""
+    ck, i = 131072, 11359
+    seg = (i * ck) // (16 << 20) * (16 << 20)
+    d = L.datagen("mixed", 32 << 20, seed=12345, offset=seg)
+    return np.ascontiguousarray(d[i * ck - seg:(i + 1) * ck - seg])
+
+
+@pytest.mark.skipif(not O.have_ref(), reason="needs oracle/_ref (the reference build)")
+def test_huffman_sort_cutoff_equals_reference():
+    """The restatement's HUF_sort cutoff is the macro's value (165), not its comment's (166): found by the 4 GiB
+    config-5 digest (tests/test_gpu_rows.py), where this chunk alone came out with the same size and different
+    Huffman code lengths for two symbols of equal count."""
+    d = mixed_chunk_11359()
+    rp, rcs = O.compress_chunks(d, "zstd", 131072, 1, use_ref=True)
+    op, ocs = O.compress_chunks(d, "zstd", 131072, 1, use_ref=False)
+    assert (rcs == ocs).all() and len(rp) == len(op) and (rp == op).all()
