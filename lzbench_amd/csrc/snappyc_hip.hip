@@ -942,716 +942,6 @@ lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readabl
 }
 
 
-// ======================================================================= two-wave parse
-// lzh_snappy_parse2_kernel: lzh_snappy_parse_kernel's fragment parse by a workgroup of TWO waves sharing the
-// fragment's table and input ring (the LZ4 kernel's loader / resolver split, profiles/r05_a: rejected there,
-// where the one-wave parse is issue-bound at 9 waves per CU; the snappy parse runs ONE wave per SIMD -- its
-// 32 KiB table -- and issues in only ~50 % of its cycles, so a second wave has room):
-//   * the LOADER makes every table access and candidate load of the run batches; while the resolver resolves
-//     batch k it prepares batch k+1 at base_k + 64 (snappy's next run-batch base whenever batch k's chain ends
-//     before base_k + 128: the re-test after a copy ending at rt = base_k + eL, eL < 128, is the lane rt - base
-//     of that batch, its ip-1 insert the lane before) and publishes two dwords per lane;
-//   * the RESOLVER resolves (snappy.cc:558-672 as compress_fragment's run batch), keeps the parse state and the
-//     records, and runs the search batches (sparse probes, the fragment's tail) alone -- owning the table and
-//     the ring meanwhile.
-// Hot lanes (a batch-(k+1) lane that read batch k's claim winner) as in the LZ4 version: the loader evaluates
-// both likely outcomes, the resolver picks with I_k, the loader restores batch k and writes the claim winners
-// back after the barrier.
-namespace snp2 {
-using namespace snv2;
-
-enum { kRun = 0, kSearch = 1, kEnd = 2 };
-constexpr int kAhead2 = 640;     // refills never overwrite the bytes at or after front - 128
-
-__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// mailbox lane words (as lz4p2): w0 = ok | len << 1 | okp << 6 | lep << 7 | prev6 << 13 | hot << 19 | g << 20
-// | okB << 26 | lenB << 27 (prev6: prev, or the lane itself: none); w1 = cand | candB << 16
-__device__ __forceinline__ uint32_t pack0(bool ok, int len, bool okp, int lep, int prev6, bool hot, int g, bool okB,
-                                          int lenB) {
-    return (uint32_t)ok | ((uint32_t)len << 1) | ((uint32_t)okp << 6) | ((uint32_t)lep << 7) | ((uint32_t)prev6 << 13) |
-           ((uint32_t)hot << 19) | ((uint32_t)g << 20) | ((uint32_t)okB << 26) | ((uint32_t)lenB << 27);
-}
-
-// candidate window: 7 dwords from (c + sh) & ~3 and the byte shift (compress_fragment's d0..d6, cs)
-struct SW { uint32_t d0, d1, d2, d3, d4, d5, d6, cs; };
-__device__ __forceinline__ void sw_global(const Bytes& in, uint32_t c, SW& W) {
-    const int X = (int)c + in.sh, A = X & ~3;
-    W.d0 = ld_b32(in.r, A); W.d1 = ld_b32(in.r, A + 4); W.d2 = ld_b32(in.r, A + 8); W.d3 = ld_b32(in.r, A + 12);
-    W.d4 = ld_b32(in.r, A + 16); W.d5 = ld_b32(in.r, A + 20); W.d6 = ld_b32(in.r, A + 24);
-    W.cs = (uint32_t)X & 3u;
-}
-__device__ __forceinline__ void sw_ring(const Ring& R, uint32_t c, SW& W) {
-    const int X = (int)c + R.sh, A = X & ~3;
-    const volatile LDSA uint32_t* q = (const volatile LDSA uint32_t*)R.w + ((A & (kRing - 1)) >> 2);
-    W.d0 = q[0]; W.d1 = q[1]; W.d2 = q[2]; W.d3 = q[3]; W.d4 = q[4]; W.d5 = q[5]; W.d6 = q[6];
-    W.cs = (uint32_t)X & 3u;
-}
-__device__ __forceinline__ bool sw_eval(const PS& ps, const SW& W, int& len) {
-    const uint32_t cs = W.cs;
-    len = match_after4(ps, __builtin_amdgcn_alignbyte(W.d2, W.d1, cs), __builtin_amdgcn_alignbyte(W.d3, W.d2, cs),
-                       __builtin_amdgcn_alignbyte(W.d4, W.d3, cs), __builtin_amdgcn_alignbyte(W.d5, W.d4, cs),
-                       __builtin_amdgcn_alignbyte(W.d6, W.d5, cs));
-    return __builtin_amdgcn_alignbyte(W.d1, W.d0, cs) == ps.w;
-}
-__device__ __forceinline__ SW sw_sel(bool c, const SW& a, const SW& b) {
-    SW r;
-    r.d0 = c ? a.d0 : b.d0; r.d1 = c ? a.d1 : b.d1; r.d2 = c ? a.d2 : b.d2; r.d3 = c ? a.d3 : b.d3;
-    r.d4 = c ? a.d4 : b.d4; r.d5 = c ? a.d5 : b.d5; r.d6 = c ? a.d6 : b.d6; r.cs = c ? a.cs : b.cs;
-    return r;
-}
-__device__ __forceinline__ SW sw_gather(const SW& a, int k) {
-    SW r;
-    r.d0 = lane_gather(a.d0, k); r.d1 = lane_gather(a.d1, k); r.d2 = lane_gather(a.d2, k); r.d3 = lane_gather(a.d3, k);
-    r.d4 = lane_gather(a.d4, k); r.d5 = lane_gather(a.d5, k); r.d6 = lane_gather(a.d6, k); r.cs = lane_gather(a.cs, k);
-    return r;
-}
-
-__device__ __forceinline__ void put_records(rsrc_t recs, int& nrec, uint64_t mem, uint32_t P, uint32_t ml, uint32_t off) {
-    const uint64_t m = uni64(mem);
-    if (!m) return;
-    const int ri = nrec + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (lane_on(m)) st_b64(recs, 8 * ri, P | (ml << 24), (ml >> 8) | (off << 16));
-    nrec = unii(nrec + __builtin_popcountll(m));
-}
-
-// One fragment in[0, fn) (chunk positions fbase + p); records appended at nrec (kRec layout).  LDS: table
-// (32 KiB) | ring 1 KiB + 32 B mirror | mailbox 64 x 2 dwords | 16 control dwords:
-//   ctl[4 (i & 1) + 0..3] the resolver's verdict of iteration i: I lo, I hi, mode, next base
-//   ctl[8], ctl[9] ring fill / ready (the loader's, with a published batch or before a search phase)
-//   ctl[10] iterations whose mailbox the resolver has read; ctl[11] the ring fill (= ready) after a search batch
-__device__ void fragment2(const Bytes& in, int fn, LDSA uint16_t* tab, LDSA uint32_t* ringw, LDSA uint32_t* mail,
-                          LDSA uint32_t* ctl, rsrc_t recs, int& nrec, int fbase) {
-    const int lane = threadIdx.x & 63;
-    const int wid = unii((int)(threadIdx.x >> 6));   // 0 resolver, 1 loader
-    volatile LDSA uint32_t* const vc = (volatile LDSA uint32_t*)ctl;
-    volatile LDSA uint32_t* const vm = (volatile LDSA uint32_t*)mail;
-    Table T{tab};
-    const uint32_t tsize = table_size_for((uint32_t)fn);
-    const int shift = 32 - log2floor_u(tsize);
-    {
-        LDSA uint32_t* t4 = (LDSA uint32_t*)tab;
-        const int nvec = (int)(tsize * 2 / 16);
-        for (int i = (int)threadIdx.x; i < nvec; i += 128) lds_zero16(t4 + 4 * i);
-        if (threadIdx.x < 16) vc[threadIdx.x] = 0;
-    }
-    const int endX = fn + in.sh + 8;
-    const int ip_limit = fn - 15;
-    if (fn < 15) {   // the whole fragment is one literal run
-        if (wid == 0) {
-            if (lane == 0) st_b64(recs, 8 * nrec, (uint32_t)(fbase + fn), 0u);
-            nrec++;
-        }
-        return;
-    }
-    wg_barrier();   // (the zeroed table and control words)
-
-    if (wid == 1) {
-        // ================================================================= loader
-        Ring R{ringw, in.sh, 0, 0, true, true};
-        for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
-        wait_vm();
-        R.ready = R.fill;
-        wave_lds_fence();
-        int c_base = 0, c_top = lane;                    // the batch being resolved (k)
-        uint32_t c_h = 0, c_old = 0;
-        uint64_t c_grp = 0;
-        SW Wold = {0, 0, 0, 0, 0, 0, 0, 0};
-        int n_base = 0, n_w = lane;                      // the batch prepared next (k+1)
-        uint32_t n_h = 0, n_v = 0, n_back = 0, n_cold = 0;
-        uint64_t n_grp = 0, n_hot = 0;
-        SW n_W = {0, 0, 0, 0, 0, 0, 0, 0}, n_Wb = {0, 0, 0, 0, 0, 0, 0, 0};
-
-        auto prepare = [&](int nb, bool spec, int it) {
-            n_base = nb;
-            const int p = nb + lane;                     // (run batches: every probe valid, nb + 72 <= ip_limit)
-            const bool ring = R.has(nb, nb + LZH_WAVE + 28);
-            const PS ps = p_side(R, in, ring, p);
-            n_h = (ps.w * 0x1e35a7bdu) >> shift;
-            n_v = T.get(n_h);
-            const bool hot = spec && n_v - (uint32_t)c_base < 64u;
-            n_hot = ballot(hot);
-            sw_global(in, hot ? 0u : n_v, n_W);          // (issued before the claim round trip)
-            T.put(n_h, (uint32_t)p);
-            wave_lds_fence();
-            n_back = T.get(n_h);
-            const uint64_t losers = ballot(n_back != (uint32_t)p);
-            uint64_t grp = 1ull << lane;
-            int prev = -1;
-            bool okp = false;
-            int lep = 0;
-            if (losers) {   // slot groups by the claim winner, bit-sliced (compress_fragment's run batch)
-                const uint32_t W = n_back - (uint32_t)nb;
-                uint32_t ne0 = 0, ne1 = 0;
-#pragma unroll
-                for (int b = 0; b < 6; b++) {
-                    const uint64_t bm = ballot((W >> b) & 1u);
-                    const uint32_t mine = (uint32_t)__builtin_amdgcn_sbfe((int)W, b, 1);
-                    ne0 |= (uint32_t)bm ^ mine;
-                    ne1 |= (uint32_t)(bm >> 32) ^ mine;
-                }
-                grp = ~(((uint64_t)ne1 << 32) | ne0);
-                const uint64_t eb = grp & ((1ull << lane) - 1ull);
-                prev = eb ? 63 - __builtin_clzll(eb) : -1;
-                const int k = prev >= 0 ? prev : lane;
-                const uint32_t gw = lane_gather(ps.w, k);
-                lep = match_after4(ps, lane_gather(ps.q1, k), lane_gather(ps.q2, k), lane_gather(ps.q3, k),
-                                   lane_gather(ps.q4, k), lane_gather(ps.q5, k));
-                okp = gw == ps.w;
-            }
-            n_grp = grp;
-            int g = 0, lenB = 0;
-            bool okB = false;
-            uint32_t cand = n_v;
-            SW WA = n_W;
-            if (n_hot) {   // outcome A: the group's top lane g of batch k inserted; B: none (the slot's old value)
-                n_w = hot ? (int)(n_v - (uint32_t)c_base) : lane;
-                g = (int)lane_gather((uint32_t)c_top, n_w);
-                n_cold = lane_gather(c_old, n_w);
-                n_Wb = sw_gather(Wold, n_w);
-                if (R.has(c_base, c_base + LZH_WAVE + 28)) sw_ring(R, (uint32_t)(c_base + g), WA);
-                else sw_global(in, (uint32_t)(c_base + g), WA);
-                okB = sw_eval(ps, n_Wb, lenB);
-                if (hot) cand = (uint32_t)(c_base + g);
-            }
-            wait_vm();                                    // the candidate windows (and older refills)
-            R.ready = R.fill;
-            wave_lds_fence();
-            {
-                const int target = min(nb + in.sh + kAhead2, endX + 256);
-                for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
-            }
-            int len;
-            const bool ok = sw_eval(ps, lane_on(n_hot) ? WA : n_W, len);
-            const uint32_t w0 = pack0(ok, len, okp, lep, prev >= 0 ? prev : lane, lane_on(n_hot), g, okB, lenB);
-            const uint32_t w1 = (cand & 0xffffu) | (n_cold << 16);
-            if (it >= 0) {   // the resolver has read iteration it's mailbox (it does so right after the barrier)
-                for (int sp = 0; sp < (1 << 20); sp++) {
-                    if (unii((int)vc[10]) > it) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            vm[2 * lane] = w0;
-            vm[2 * lane + 1] = w1;
-            if (lane == 0) { vc[8] = (uint32_t)R.fill; vc[9] = (uint32_t)R.ready; }
-        };
-        auto advance = [&](const uint32_t* fin) {
-            if (fin && n_hot) {
-                const bool hot = lane_on(n_hot);
-                const uint32_t fw = lane_gather(*fin, n_w);
-                const bool inr = hot && fw >= (uint32_t)c_base;
-                SW G = n_Wb;
-                if (ballot(inr)) {
-                    if (R.has(c_base, c_base + LZH_WAVE + 28)) sw_ring(R, inr ? fw : (uint32_t)c_base, G);
-                    else { sw_global(in, inr ? fw : 0u, G); wait_vm(); }
-                }
-                if (hot) {
-                    n_W = inr ? G : n_Wb;
-                    n_v = fw;
-                }
-            }
-            c_base = n_base; c_h = n_h; c_old = n_v; c_grp = n_grp; Wold = n_W;
-            c_top = 63 - __builtin_clzll(c_grp | (1ull << lane));
-        };
-
-        int mode = 1 + LZH_WAVE + 8 > ip_limit ? kSearch : kRun;   // (as the resolver: a short fragment)
-        if (mode == kRun) {
-            prepare(1, false, -1);
-            advance(nullptr);
-        } else if (lane == 0) {
-            vc[8] = (uint32_t)R.fill;
-            vc[9] = (uint32_t)R.ready;
-        }
-        wg_barrier();                                            // the first batch published
-        for (int it = 0;; it++) {
-            const bool have_nxt = mode == kRun && c_base + 64 + LZH_WAVE + 8 <= ip_limit;
-            if (have_nxt) prepare(c_base + 64, true, it);    // batch k+1, speculatively at base_k + 64
-            wg_barrier();                                        // the resolver's verdict on this iteration
-            const int cb = 4 * (it & 1);
-            const uint64_t I = uni64(((uint64_t)vc[cb + 1] << 32) | vc[cb]);
-            const int nmode = unii((int)vc[cb + 2]), nbase = unii((int)vc[cb + 3]);
-            if (nmode == kEnd) break;
-            const bool spec = have_nxt && nmode == kRun && nbase == n_base;
-            uint32_t fin = 0;
-            if (mode == kRun) {   // each slot of batch k ends with its last inserted lane, else its old value
-                const uint64_t gi = c_grp & I;
-                fin = gi ? (uint32_t)(c_base + 63 - __builtin_clzll(gi)) : c_old;
-            }
-            if (have_nxt && !spec) T.put(n_h, n_v);             // undo the speculative claims
-            if (mode == kRun) T.put(c_h, fin);                   // restore(k)
-            if (spec) {
-                if (lane_on(n_hot)) T.put(n_h, n_back);          // the claim winners back
-                wave_lds_fence();
-                advance(&fin);
-            } else {
-                wave_lds_fence();
-                if (mode == kSearch) {                           // the resolver's ring after its search batch
-                    R.fill = unii((int)vc[11]);
-                    R.ready = R.fill;
-                }
-                if (nmode == kRun) {
-                    prepare(nbase, false, -1);                   // (the resolver read iteration it's mailbox)
-                    advance(nullptr);
-                } else {                                         // a search batch next: the resolver takes the ring
-                    wait_vm();
-                    R.ready = R.fill;
-                    if (lane == 0) { vc[8] = (uint32_t)R.fill; vc[9] = (uint32_t)R.ready; }
-                }
-                wg_barrier();                                    // the rebuilt batch / the table for a search batch
-            }
-            mode = nmode;
-            R.fill = unii(R.fill); R.ready = unii(R.ready);
-            c_base = unii(c_base); n_base = unii(n_base);
-        }
-        return;
-    }
-
-    // ===================================================================== resolver
-    int next_emit = 0, base = 1, org = 1, rt = -1, mode = kRun;
-    bool retest = false, U = false;
-    int q0 = 1, t0 = 0, ci0 = 0, cq0 = 1;
-    uint32_t cu0 = 32u;
-    int pbase = 0, pprev = -1;       // the previous run batch: base and slot-group links (hot lanes)
-    uint64_t pI = 0;                 // and its inserted lanes
-    // the parse state after a run batch at (base, org, rt): the next run batch, or the search batches
-    auto next_run_or_search = [&](int nb, int& nmode) {
-        if (nb + LZH_WAVE + 8 > ip_limit || (rt < 0 && nb - org >= LZH_WAVE)) {
-            nmode = kSearch;            // sparse probes or close to ip_limit (exact termination)
-            if (rt >= 0) {
-                retest = true;
-                q0 = rt + 1;
-                t0 = 0;
-            } else {
-                const int d = nb - org;
-                retest = false;
-                q0 = org;
-                t0 = d < LZH_WAVE ? __builtin_popcountll(kPat0 & ((1ull << d) - 1ull))
-                                  : 48 + __builtin_popcountll(kPat1 & ((1ull << (d - LZH_WAVE)) - 1ull));
-            }
-            U = ip_limit - q0 >= 16;
-            ci0 = 0;
-            cq0 = U ? q0 + 16 : q0;
-            cu0 = U ? 48u : 32u;
-        } else {
-            nmode = kRun;
-        }
-    };
-    next_run_or_search(1, mode);     // (a short fragment starts with search batches)
-    wg_barrier();                                                // the first batch published
-    for (int it = 0;; it++) {
-        Ring R{ringw, in.sh, unii((int)vc[8]), unii((int)vc[9]), true, true};
-        int nmode = kEnd, nbase = 0;
-        uint64_t I = 0, Mm = 0;
-        int cn = 0, prev = -1;
-        uint32_t ce = 0;
-        const int rbase = base;
-        int sP = -1, sM = 0, sml = 0;                           // search batch: its copy
-        if (mode == kRun) {
-            const uint32_t w0 = vm[2 * lane], w1 = vm[2 * lane + 1];
-            __builtin_amdgcn_s_waitcnt(0xC07F);              // lgkmcnt(0): the mailbox is in registers
-            if (lane == 0) vc[10] = (uint32_t)(it + 1);        // ... and may be overwritten
-            const bool okp = (w0 >> 6) & 1u;
-            const int lep = (int)((w0 >> 7) & 31u);
-            const int prev6 = (int)((w0 >> 13) & 63u);
-            prev = prev6 == lane ? -1 : prev6;
-            bool ok = w0 & 1u;
-            int len = (int)((w0 >> 1) & 31u);
-            uint32_t cand = w1 & 0xffffu;
-            const uint64_t hotm = ballot((w0 >> 19) & 1u);
-            const int p = base + lane;
-            if (hotm) {   // hot lanes: the last inserted lane of the group in the previous batch
-                const bool hot = lane_on(hotm);
-                const int g = (int)((w0 >> 20) & 63u);
-                int x = hot ? g : -1;
-                for (int i = 0; i < LZH_WAVE; i++) {
-                    const bool m = x >= 0 && !((pI >> x) & 1ull);
-                    if (!ballot(m)) break;
-                    const int xp = (int)lane_gather((uint32_t)pprev, m ? x : lane);
-                    x = m ? xp : x;
-                }
-                const bool useB = hot && x < 0, other = hot && x >= 0 && x != g;
-                if (useB) {
-                    ok = (w0 >> 26) & 1u;
-                    len = (int)(w0 >> 27);
-                    cand = w1 >> 16;
-                }
-                if (ballot(other)) {   // (rare) another lane of the group: evaluated from the ring
-                    const bool ring = R.has(pbase, base + LZH_WAVE + 28);
-                    const PS ps = p_side(R, in, ring, p);
-                    SW W;
-                    if (ring) sw_ring(R, (uint32_t)(pbase + (other ? x : 0)), W);
-                    else { sw_global(in, (uint32_t)(pbase + (other ? x : 0)), W); wait_vm(); }
-                    int l_;
-                    const bool o_ = sw_eval(ps, W, l_);
-                    if (other) { ok = o_; len = l_; cand = (uint32_t)(pbase + x); }
-                }
-            }
-            // ================= run batch (compress_fragment): resolve every copy that starts in the batch
-            const uint64_t below = (1ull << lane) - 1ull;
-            const uint64_t coll = ballot(prev >= 0);
-            const uint64_t P0 = (rt >= 0 ? (1ull << (rt - base)) : 0ull) | pat_from(org - base);
-            const uint64_t I0 = (rt >= 0 && rt - 1 >= base) ? (1ull << (rt - 1 - base)) : 0ull;   // ip-1 (snappy.cc:652)
-            int ak = prev;
-            bool oke = prev >= 0 ? okp : ok;
-            ce = prev >= 0 ? (uint32_t)(base + prev) : cand;
-            int le = prev >= 0 ? lep : len;
-            I = I0;
-            int e = 0, eL = 0;
-            bool endp = false;
-            PS ps;
-            bool have_ps = false;
-            for (int round = 0; round <= LZH_WAVE; round++) {
-                const uint64_t A = ballot(oke);
-                cn = min(le, fn - (p + 4));                      // FindMatchLength limit (ip_end)
-                const bool lng = oke && le == 20 && p + 24 < fn;
-                e = lane + 4 + cn;
-                const int f = ctz64v(A & after_copy(e));
-                const int link = (lng || p + 4 + cn >= ip_limit) ? 0x80 : f;
-                Mm = 0;
-                endp = false;
-                uint64_t E;
-                const uint64_t r0 = A & P0;
-                if (!r0) {
-                    E = P0;
-                } else {
-                    int sl = __builtin_ctzll(r0);
-                    for (;;) {                                   // (links strictly increase)
-                        int fs;
-                        for (;;) {
-                            Mm |= 1ull << sl;
-                            fs = rdlanei(link, sl);
-                            if (fs >= LZH_WAVE) break;
-                            sl = fs;
-                        }
-                        if (fs != 0x80) break;
-                        int es;
-                        if (rdlane((uint32_t)lng, sl)) {         // copy runs past the window
-                            const int a = base + sl + 4, M = rdlanei((int)ce, sl);
-                            int c = 20;
-                            for (int it2 = 0; it2 < (1 << 11) && a + c < fn; it2++) {
-                                const int o = c + 4 * lane;
-                                const uint32_t x = in.w32(a + o) ^ in.w32(M + 4 + o);
-                                const uint64_t ne = ballot(x != 0);
-                                if (ne) {
-                                    const int l = ffs64(ne);
-                                    c += 4 * l + (int)byte_ctz(rdlane(x, l));
-                                    break;
-                                }
-                                c += 4 * LZH_WAVE;
-                            }
-                            c = min(c, fn - a);
-                            es = sl + 4 + c;
-                            cn = lane == sl ? c : cn;
-                            e = lane == sl ? es : e;
-                            fs = ctz64v(A & after_copy(es));
-                        } else {
-                            es = rdlanei(e, sl);
-                        }
-                        if (base + es >= ip_limit) { endp = true; break; }   // snappy.cc:646
-                        if (fs >= LZH_WAVE) break;
-                        sl = fs;
-                    }
-                    eL = rdlanei(e, sl);
-                    const uint64_t mle = Mm & (below | (1ull << lane));
-                    const int j = mle ? 63 - __builtin_clzll(mle) : lane;
-                    const int ej = (int)lane_gather((uint32_t)e, j);
-                    bool pr;
-                    if (!mle) pr = lane_on(P0);
-                    else if (lane == j) pr = true;
-                    else pr = lane >= ej && ((after_copy(ej) >> lane) & 1ull);
-                    E = ballot(pr && (!endp || lane < eL));
-                    I = ballot(mle && lane != j && lane == ej - 1);
-                }
-                I = (Mm ? I : 0ull) | I0 | E;
-                if (!(coll & E)) break;
-                int kt = prev;                                   // the latest earlier inserted lane of the slot
-                for (int i = 0; i < LZH_WAVE; i++) {
-                    const bool m = kt >= 0 && !((I >> kt) & 1ull);
-                    if (!ballot(m)) break;
-                    const int kp = (int)lane_gather((uint32_t)prev, m ? kt : lane);
-                    kt = m ? kp : kt;
-                }
-                const bool fix = lane_on(E) && kt != ak;
-                if (!ballot(fix)) break;
-                const bool far = fix && kt >= 0 && kt != prev;
-                if (fix) {
-                    ak = kt;
-                    oke = kt < 0 ? ok : okp;
-                    ce = kt < 0 ? cand : (uint32_t)(base + kt);
-                    le = kt < 0 ? len : lep;
-                }
-                if (ballot(far)) {                               // an older member than prev
-                    if (!have_ps) { ps = p_side(R, in, R.has(base, base + LZH_WAVE + 28), p); have_ps = true; }
-                    const int k = far ? kt : lane;
-                    const uint32_t gw = lane_gather(ps.w, k);
-                    const int lf = match_after4(ps, lane_gather(ps.q1, k), lane_gather(ps.q2, k),
-                                                lane_gather(ps.q3, k), lane_gather(ps.q4, k), lane_gather(ps.q5, k));
-                    if (far) { le = lf; oke = gw == ps.w; }
-                }
-            }
-            if (Mm) next_emit = base + eL;
-            if (endp) {
-                nmode = kEnd;
-            } else {
-                int nb;
-                if (Mm && eL >= LZH_WAVE) {                      // the re-test in a later batch
-                    rt = base + eL;
-                    org = rt + 1;
-                    // base + 64 holds it when it lies there (the ip-1 insert at the lane before, if any)
-                    nb = rt - base - LZH_WAVE < LZH_WAVE ? base + LZH_WAVE : rt - 1;
-                } else {
-                    if (Mm) org = base + eL + 1;                 // the search continues past the batch
-                    rt = -1;
-                    nb = base + LZH_WAVE;
-                }
-                next_run_or_search(nb, nmode);
-                nbase = nb;
-            }
-        } else {
-            // ================= search batch (sparse probes or near ip_limit): compress_fragment's, the resolver
-            // alone (table and ring)
-            int p = 0;
-            bool valid = false, term = false;
-            int ci = -1;
-            uint32_t u = 0;
-            const bool ins63 = retest;
-            if (retest && lane == 0) {
-                p = rt;
-                valid = true;
-            } else if (ins63 && lane == 63) {
-                p = rt - 1;
-            } else if (!retest || lane < kRT) {
-                const int t = retest ? lane - 1 : t0 + lane;
-                if (U && t < 16) {
-                    p = q0 + t;
-                    valid = true;
-                } else {
-                    ci = U ? t - 16 : t;
-                    u = skip_walk(cu0, ci - ci0);
-                    const int64_t pp = (int64_t)cq0 + (int64_t)(u - cu0);
-                    valid = pp + (int64_t)(u >> 5) <= ip_limit;
-                    term = !valid;
-                    p = valid ? (int)pp : 0;
-                }
-            }
-            const uint64_t vmask = ballot(valid);
-            const uint64_t tmask = ballot(term);
-            const int front = ins63 ? rt - 1 : rdlanei(p, 0);
-            const int pmax = vmask ? rdlanei(p, 63 - __builtin_clzll(vmask)) : front;
-            uint32_t pw;
-            if (R.has(front - 4, pmax + 12)) pw = R.u32(p);
-            else pw = in.w32(p);
-            const uint32_t h = (pw * 0x1e35a7bdu) >> shift;
-            if (ins63 && lane == 63) T.put(h, (uint32_t)(rt - 1));
-            const uint32_t old = T.get(h);
-            if (valid) T.put(h, (uint32_t)p);
-            wave_lds_fence();
-            const uint32_t back = T.get(h);
-            const uint64_t losers = ballot(valid && back != (uint32_t)p);
-            uint32_t cand = old;
-            int cX = (valid ? (int)cand : 0) + in.sh;
-            int cA = cX & ~3;
-            uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0, d5 = 0;
-            if (valid) {
-                d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
-                d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
-            }
-            {
-                const int target = min(front + in.sh + kAhead, endX + 256);
-                for (int r = 0; r < 4 && R.fill < target; r++) R.refill(in.r, lane);
-            }
-            wait_vm();
-            R.ready = R.fill;
-            wave_lds_fence();
-            bool ok = valid && __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)cX & 3u) == pw;
-            uint64_t hits = ballot(ok);
-            const int fi = ffs64(tmask);
-            int fh = ffs64(hits);
-            bool found = hits != 0;
-            int L = found ? fh : fi - 1;
-            uint64_t upto = L < 0 ? 0ull : (L >= 63 ? ~0ull : ((2ull << L) - 1ull));
-            bool exact = false;
-            if (losers & upto) {
-                if (L <= 7) {
-                    bool pr = false;
-#pragma unroll
-                    for (int d = 1; d <= 7; d++) {
-                        const uint32_t hv = lane_gather(h, lane >= d ? lane - d : lane);
-                        pr = pr || (d <= lane && lane <= L && hv == h);
-                    }
-                    exact = ballot(pr) != 0;
-                } else {
-                    exact = true;
-                }
-            }
-            if (!exact) {
-                if (valid && lane > L && back == (uint32_t)p) T.put(h, old);
-                if (losers & upto) {
-                    wave_lds_fence();
-                    if (lane <= L) T.put(h, (uint32_t)p);
-                }
-            } else {
-                if (valid) T.put(h, old);
-                wave_lds_fence();
-                uint64_t pending = losers;
-                uint64_t grp = 1ull << lane;
-                int prv = -1;
-                for (int i2 = 0; i2 < LZH_WAVE && pending; i2++) {
-                    const int l = ffs64(pending);
-                    const uint32_t hv = rdlane(h, l);
-                    const bool mine = valid && h == hv;
-                    const uint64_t m = ballot(mine);
-                    pending &= ~m;
-                    if (mine) {
-                        grp = m;
-                        const uint64_t bl = m & ((1ull << lane) - 1ull);
-                        if (bl) prv = 63 - __builtin_clzll(bl);
-                    }
-                }
-                const uint32_t ppos = lane_gather((uint32_t)p, prv < 0 ? lane : prv);
-                if (prv >= 0) cand = ppos;
-                cX = (valid ? (int)cand : 0) + in.sh;
-                cA = cX & ~3;
-                if (valid) {
-                    d0 = ld_b32(in.r, cA); d1 = ld_b32(in.r, cA + 4); d2 = ld_b32(in.r, cA + 8);
-                    d3 = ld_b32(in.r, cA + 12); d4 = ld_b32(in.r, cA + 16); d5 = ld_b32(in.r, cA + 20);
-                }
-                wait_vm();
-                R.ready = R.fill;
-                ok = valid && __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)cX & 3u) == pw;
-                hits = ballot(ok);
-                fh = ffs64(hits);
-                found = hits != 0;
-                L = found ? fh : fi - 1;
-                upto = L < 0 ? 0ull : (L >= 63 ? ~0ull : ((2ull << L) - 1ull));
-                if (valid && lane <= L) {
-                    const uint64_t later = grp & ~((2ull << lane) - 1ull) & upto;
-                    if (!later) T.put(h, (uint32_t)p);
-                }
-            }
-            wave_lds_fence();
-            if (!found) {
-                if (tmask) {
-                    nmode = kEnd;                                // search exhausted: remainder from next_emit
-                } else {
-                    nmode = kSearch;
-                    const int last = retest ? kRT - 1 : 63;
-                    const int cl = rdlanei(ci, last);
-                    if (cl >= 0) {
-                        const uint32_t ul = rdlane(u, last);
-                        const int ql = rdlanei(p, last);
-                        ci0 = cl + 1;
-                        cq0 = ql + (int)(ul >> 5);
-                        cu0 = ul + (ul >> 5);
-                    }
-                    if (retest) { retest = false; t0 = kRT - 1; }
-                    else t0 += LZH_WAVE;
-                }
-            } else {   // copy at P from candidate M: FindMatchLength(M+4, P+4, fn)
-                const int P = rdlanei(p, fh);
-                const int M = rdlanei((int)cand, fh);
-                const uint32_t e0 = rdlane(d0, fh), e1 = rdlane(d1, fh), e2 = rdlane(d2, fh), e3 = rdlane(d3, fh),
-                               e4 = rdlane(d4, fh), e5 = rdlane(d5, fh);
-                const int sbase = (M + in.sh) & 3;
-                const int kmax = 20 - sbase;
-                const int a = P + 4;
-                const bool rok = R.has(a, a + 20);
-                const bool act = lane < kmax;
-                uint32_t pb = 0;
-                if (rok) pb = R.byte(a + lane);
-                else if (act) pb = in.b(a + lane);
-                const bool eq = act && pb == spec_byte((sbase + 4 + lane) & 31, e0, e1, e2, e3, e4, e5);
-                const uint64_t em = ballot(eq);
-                int len = ffs64((~em & ((1ull << kmax) - 1ull)) | (1ull << kmax));
-                if (len >= kmax && a + len < fn) {
-                    for (int i2 = 0; i2 < (1 << 11) && a + len < fn; i2++) {
-                        const int o = len + 4 * lane;
-                        const uint32_t x = in.w32(a + o) ^ in.w32(M + 4 + o);
-                        const uint64_t ne = ballot(x != 0);
-                        if (ne) {
-                            const int l = ffs64(ne);
-                            len += 4 * l + (__builtin_ctz(rdlane(x, l)) >> 3);
-                            break;
-                        }
-                        len += 4 * LZH_WAVE;
-                    }
-                }
-                len = min(len, fn - a);
-                const int matched = 4 + len;
-                sP = P; sM = M; sml = matched;
-                const int ip = P + matched;
-                next_emit = ip;
-                if (ip >= ip_limit) {
-                    nmode = kEnd;
-                } else {                                         // back to run batches: re-test batch at rt
-                    rt = ip;
-                    org = rt + 1;
-                    const int nb = rt - 1;
-                    next_run_or_search(nb, nmode);
-                    nbase = nb;
-                }
-            }
-            wait_vm();                                           // (its refills landed: the loader may take the ring)
-            if (lane == 0) vc[11] = (uint32_t)R.fill;
-        }
-        if (it > 4 * fn + 64) nmode = kEnd;
-        const int cb = 4 * (it & 1);
-        if (lane == 0) {
-            vc[cb] = (uint32_t)I;
-            vc[cb + 1] = (uint32_t)(I >> 32);
-            vc[cb + 2] = (uint32_t)nmode;
-            vc[cb + 3] = (uint32_t)nbase;
-        }
-        wg_barrier();                                            // the verdict on this iteration
-        if (mode == kRun) put_records(recs, nrec, Mm, (uint32_t)(fbase + rbase + lane), (uint32_t)(4 + cn),
-                                      (uint32_t)(rbase + lane) - ce);
-        else if (sP >= 0) put_records(recs, nrec, 1ull, (uint32_t)(fbase + sP), (uint32_t)sml, (uint32_t)(sP - sM));
-        if (nmode == kEnd) break;
-        const bool spec = mode == kRun && base + 64 + LZH_WAVE + 8 <= ip_limit && nmode == kRun && nbase == base + 64;
-        if (!spec) wg_barrier();                                 // the rebuilt batch / the table for a search batch
-        pI = mode == kRun ? I : 0ull;
-        pprev = prev;
-        pbase = rbase;
-        mode = unii(nmode);
-        base = unii(nbase);
-        rt = unii(rt); org = unii(org); next_emit = unii(next_emit);
-        q0 = unii(q0); t0 = unii(t0); ci0 = unii(ci0); cq0 = unii(cq0); cu0 = uni(cu0);
-        retest = unii(retest) != 0; U = unii(U) != 0;
-    }
-    if (next_emit < fn) {   // the fragment's last literal run: a literal-only record
-        if (lane == 0) st_b64(recs, 8 * nrec, (uint32_t)(fbase + fn), 0u);
-        nrec++;
-    }
-}
-
-}  // namespace snp2
-
-// (4 workgroups of 2 waves per CU: 34 400 bytes of LDS each)
-extern "C" __global__ void __launch_bounds__(128)
-lzh_snappy_parse2_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
-                         uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint32_t frags) {
-    // table | ring + mirror | mailbox | control words
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + 256 + 8 + 128 + 16];
-    const uint64_t chunk = blockIdx.x / frags;
-    const uint32_t f = blockIdx.x - (uint32_t)chunk * frags;
-    const uint64_t off = chunk * chunk_size;
-    if (off >= n_total && !(n_total == 0 && chunk == 0)) return;
-    const uint32_t n = (uint32_t)min(chunk_size, n_total - off);
-    const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
-    uint32_t* hdr = rec_hdr + chunk * frags;
-    int nrec = frags > 1 ? (int)f * kFragRecs : 0;
-    const uint32_t fpos = f << 16;
-    if (fpos < n) {
-        const int fn = (int)min(65536u, n - fpos);
-        const uint64_t readable = min<uint64_t>(in_readable - off - fpos, (uint64_t)fn + 64);
-        Bytes rin;
-        rin.init(in + off + fpos, readable);
-        LDSA uint32_t* ring = (LDSA uint32_t*)lds + (1 << 13);
-        LDSA uint32_t* mail = ring + 256 + 8;
-        snp2::fragment2(rin, fn, (LDSA uint16_t*)lds, ring, mail, mail + 128, rr, nrec, (int)fpos);
-    }
-    if (threadIdx.x == 0) hdr[f] = (uint32_t)nrec;
-}
 
 namespace sne {
 
@@ -1989,9 +1279,6 @@ size_t lzh_snappy_rec_stride(uint64_t chunk_size) {
 
 // parse kernel + emit kernel (records: nchunks x rec_stride bytes, then a u32 count per chunk);
 // stage_mask bit 0 = parse, bit 1 = emit
-#ifndef LZH_SNAPPY_PARSE2
-#define LZH_SNAPPY_PARSE2 0   // the two-wave fragment parse (lzh_snappy_parse2_kernel): 16-21 % slower, profiles/r05_sn2
-#endif
 hipError_t lzh_launch_snappy_split(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                                    uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks, uint8_t* recs,
                                    int stage_mask, hipStream_t s) {
@@ -1999,10 +1286,7 @@ hipError_t lzh_launch_snappy_split(const uint8_t* in, uint64_t n_total, uint64_t
     const uint64_t rs = lzh_snappy_rec_stride(chunk_size);
     uint32_t* hdr = (uint32_t*)(recs + rs * nchunks);
     const uint32_t frags = lzh_snappy_frags(chunk_size);
-    if ((stage_mask & 1) && LZH_SNAPPY_PARSE2)
-        hipLaunchKernelGGL(lzh_snappy_parse2_kernel, dim3(nchunks * frags), dim3(128), 0, s, in, n_total, in_readable,
-                           chunk_size, recs, rs, hdr, frags);
-    else if (stage_mask & 1)
+    if (stage_mask & 1)
         hipLaunchKernelGGL(lzh_snappy_parse_kernel, dim3(nchunks * frags), dim3(64), 0, s, in, n_total, in_readable,
                            chunk_size, recs, rs, hdr, frags);
     if (stage_mask & 2) {
