@@ -34,10 +34,6 @@ __device__ unsigned long long lzh_dec_stats_buf[16];
 #define DMARK(i) ((void)0)
 #endif
 
-#ifndef LZH_DEC_EMIT4
-#define LZH_DEC_EMIT4 0   // four output bytes per lane per pass (groups::emit_group4): 1.3-2.4x slower, profiles/r05_dec4
-#endif
-
 namespace {
 
 #ifndef LZH_DEC_RING
@@ -153,9 +149,6 @@ struct SinkT {
     }
     __device__ __forceinline__ uint32_t dword(int X) const {
         return ((volatile const LDSA uint32_t*)b)[(X & (KW - 1)) >> 2];
-    }
-    __device__ __forceinline__ void put_dword(int X, uint32_t v) const {
-        ((volatile LDSA uint32_t*)b)[(X & (KW - 1)) >> 2] = v;
     }
     // global <- window bytes [flushed, upto)
     __device__ __forceinline__ void flush(int upto, int lane) {
@@ -449,215 +442,6 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
     }
 }
 
-// ---- four output bytes per lane per pass (verdict r4 #3: dword moves)
-// For groups whose members all produce >= 4 bytes (every LZ4 group; snappy groups without 1..3-byte
-// tags): a 256-byte pass gives each lane one window-aligned dword, which then has at most two owners
-// (the member owning its byte 0 and one starting inside it).  Literal bytes come from the input ring
-// as one unaligned 4-byte read per owner; match bytes as one 4-byte read per owner from the window
-// (or the flushed output), two where the copy's period wraps inside the dword -- byte ob of a copy
-// with offset off reads m0 + ((ob - lend) mod off), m0 = the copy's first source byte, which is the
-// byte-by-byte semantics of an overlapping copy with every source before the copy's own output.
-// Copies with offset 1..3 (and a source span that starts before the window's restart point and
-// ends after it) go byte by byte.  In-pass sources: rounds over a 64-bit mask of finished dwords.
-__device__ __forceinline__ uint32_t bytes_mask(int i0, int i1) {   // bytes [i0, i1) of a dword
-    return i1 <= i0 ? 0u : ((0xffffffffu >> (32 - 8 * (i1 - i0))) << (8 * i0));
-}
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
-// L1-bypassing dword of the flushed output at descriptor offset A (bytewise where it would cross
-// the view's end: a straddling dword read returns 0)
-__device__ __forceinline__ uint32_t out_dw(rsrc_t r, int A, int rec) {
-    if (A + 4 <= rec) return __builtin_amdgcn_raw_buffer_load_b32(r, A, 0, 16);
-    uint32_t v = 0;
-    for (int k = 0; k < 3; k++) v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, A + k, 0, 16) << (8 * k);
-    return v;
-}
-
-template <class W, class SinkType>
-__device__ __forceinline__ void emit_group4(const W& w, SinkType& O, LDSA uint8_t* mark, int ip, int op,
-                                            int total, uint64_t keep, int excl, int lit, int lrel, int off,
-                                            int cap, int lane) {
-    constexpr int kP = 4 * LZH_WAVE;
-    constexpr int KW = SinkType::kWin;
-    const int sh = O.out.sh;
-    const bool kmem = lane_on(keep);
-    const int XA = (op + sh) & ~3;                 // window coordinate of pass 0's first dword
-    const int d0 = op + sh - XA;                   // the group's first byte in it
-    // member fields for two gathers: F1 = literal end (group-relative) | (excl - lrel + 512) << 16 (its
-    // literal byte ob is stream byte ip + 512 - (F1 >> 16) + ob); F2 = offset | start (from XA) << 16
-    const int mx = excl + d0;
-    const uint32_t F1 = (uint32_t)(excl + lit) | ((uint32_t)(excl - lrel + 512) << 16);
-    const uint32_t F2 = (uint32_t)off | ((uint32_t)mx << 16);
-    const uint64_t below = (1ull << lane) - 1ull;
-    const int rec = cap + sh;                      // the output view's byte count (Bytes::init of cap bytes)
-    int carry = 0;
-    for (int pb = 0; pb < d0 + total; pb += kP) {
-        // ---- owners: the member marked in the lane's dword (at most one starts in it), else the last
-        // one marked in an earlier dword (or the pass's carry)
-        ((volatile LDSA uint8_t*)mark)[lane] = 0xffu;
-        wave_lds_fence();
-        const bool mine = kmem && mx >= pb && mx < pb + kP;
-        mark[mine ? (mx - pb) >> 2 : LZH_WAVE + lane] = (uint8_t)lane;
-        wave_lds_fence();
-        const uint32_t mk = ((volatile LDSA uint8_t*)mark)[lane];
-        const bool has = mk != 0xffu;
-        const uint64_t lt = ballot(has) & below;
-        const uint32_t mj = lane_gather(mk, lt ? 63 - __builtin_clzll(lt) : lane);
-        const int prevk = lt ? (int)mj : carry;
-        const int km = has ? (int)mk : prevk;
-        const uint32_t g1m = lane_gather(F1, km), g2m = lane_gather(F2, km);
-        const bool two = has && ((g2m >> 16) & 3u) != 0;   // the marked member starts past byte 0
-        uint32_t g1p = g1m, g2p = g2m;
-        if (ballot(two)) {
-            const uint32_t a = lane_gather(F1, prevk), b = lane_gather(F2, prevk);
-            if (two) { g1p = a; g2p = b; }
-        }
-        carry = rdlanei(km, 63);
-        const int j1 = two ? (int)((g2m >> 16) & 3u) : 4;   // owner p: bytes [0, j1), owner m: [j1, 4)
-        const int ob0 = pb + 4 * lane - d0;                  // group-relative index of byte 0
-        const int xown = op + ob0;                           // its output position
-        const int vlo = max(0, -ob0), vhi = clampi(total - ob0, 0, 4);
-        const int lend_p = (int)(g1p & 0xffffu), lend_m = (int)(g1m & 0xffffu);
-        const int off_p = (int)(g2p & 0xffffu), off_m = (int)(g2m & 0xffffu);
-        const int nlp = clampi(lend_p - ob0, 0, j1);         // p: literal [0, nlp), copy [nlp, j1)
-        const int nlm = clampi(lend_m - ob0, j1, 4);         // m: literal [j1, nlm), copy [nlm, 4)
-        const uint32_t LWp = w.lane_word(ip + 512 - (int)(g1p >> 16) + ob0);
-        uint32_t LWm = 0;
-        if (ballot(nlm > j1)) LWm = w.lane_word(ip + 512 - (int)(g1m >> 16) + ob0);
-        const uint32_t lmask = bytes_mask(0, nlp) | bytes_mask(j1, nlm);
-        const uint32_t Vlit = (LWp & bytes_mask(0, nlp)) | (LWm & bytes_mask(j1, nlm));
-        const int pend = XA + pb + kP - sh;                  // output position past the pass
-        const int thr = max(pend - KW, O.ringlo);            // window-resident sources: >= thr
-        const int P0 = pend - kP;
-        // ---- copy spans: s = output position mapped to byte 0, bytes taking it, used range
-        int sA[2], sB[2];
-        uint32_t mA[2], mB[2];
-        bool fA[2], fB[2];
-        bool slow = false;
-        int nlo = LZH_WAVE, nhi = -1;                        // in-pass dwords this lane waits for
-        auto dep = [&](int lo, int hi) {                     // used source positions [lo, hi)
-            if (hi > lo && hi - 1 >= P0) {
-                nlo = min(nlo, max((lo - P0) >> 2, 0));
-                nhi = max(nhi, (hi - 1 - P0) >> 2);
-            }
-        };
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int a = q ? nlm : nlp, b = q ? 4 : j1;
-            const int lend = q ? lend_m : lend_p, of = q ? off_m : off_p;
-            sA[q] = sB[q] = 0; mA[q] = mB[q] = 0u; fA[q] = fB[q] = false;
-            const bool cp = a < b && max(a, vlo) < min(b, vhi);
-            if (ballot(cp)) {
-                const int tA = ob0 + a - lend;               // copy-relative index of byte a (>= 0)
-                const int m0 = op + lend - of;
-                int u = tA;
-                const bool per = cp && of >= 4 && tA + (b - a) > of;
-                if (ballot(per)) u = per ? (int)((uint32_t)tA % (uint32_t)max(of, 1)) : u;
-                const int iw = a + (of - u);                  // first byte past the period's end
-                const int ea = min(b, iw);
-                const bool fast = cp && of >= 4;
-                if (fast) {
-                    sA[q] = m0 + u - a;
-                    mA[q] = bytes_mask(a, ea);
-                    sB[q] = sA[q] - of;
-                    mB[q] = bytes_mask(iw, b);
-                    const int la = m0 + u, ha = m0 + u + (ea - a), lb = m0, hb = m0 + (b - iw);
-                    fA[q] = la < thr;
-                    fB[q] = iw < b && lb < thr;
-                    // (a span that starts before the window restart and ends after it: byte by byte)
-                    const bool straddle = (fA[q] && ha > O.ringlo && la < O.ringlo) ||
-                                          (fB[q] && hb > O.ringlo && lb < O.ringlo);
-                    dep(la, ha);
-                    if (iw < b) dep(lb, hb);
-                    if (straddle) { mA[q] = mB[q] = 0u; slow = true; }
-                } else if (cp) {
-                    slow = true;
-                }
-            }
-        }
-        if (ballot(slow)) {   // per-byte sources: dependencies on earlier dwords (own-dword bytes in registers)
-            if (slow) {
-                nlo = LZH_WAVE; nhi = -1;
-                for (int i = max(nlp, vlo); i < min(4, vhi); i++) {
-                    if ((i >= nlp && i < j1) || i >= nlm) {
-                        const bool qm = i >= j1;
-                        const int lend = qm ? lend_m : lend_p, of = max(qm ? off_m : off_p, 1);
-                        const int s = op + lend - of + (int)((uint32_t)(ob0 + i - lend) % (uint32_t)of);
-                        if (s < xown) dep(s, s + 1);
-                    }
-                }
-            }
-        }
-        const uint64_t need = nhi >= nlo ? ((~0ull >> (63 - (nhi - nlo))) << nlo) : 0ull;
-        const bool anyfar = ballot(fA[0] || fA[1] || fB[0] || fB[1] || slow) != 0;
-        DST(2, 1);
-        DST(3, ballot(slow) != 0);
-        DST(5, anyfar);
-        DST(13, __builtin_popcountll(ballot(slow)));
-        DST(14, __builtin_popcountll(ballot(need != 0ull)));
-        DST(15, __builtin_popcountll(ballot(fA[0] || fA[1] || fB[0] || fB[1])));
-        const int Xw = XA + pb + 4 * lane;
-        auto value = [&]() -> uint32_t {
-            uint32_t V = Vlit;
-            if (vlo > 0) {   // the group's first dword: the previous group's bytes (a copy may read them here)
-                const uint32_t pm = bytes_mask(0, vlo);
-                V = (V & ~pm) | (O.dword(Xw) & pm);
-            }
-#pragma unroll
-            for (int q = 0; q < 2; q++) {
-                if (ballot(mA[q] != 0u)) {
-                    const int X = sA[q] + sh, A = X & ~3;
-                    uint32_t lo, hi;
-                    if (fA[q]) { lo = out_dw(O.out.r, A, rec); hi = out_dw(O.out.r, A + 4, rec); }
-                    else { lo = O.dword(A); hi = O.dword(A + 4); }
-                    V |= __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)X & 3u) & mA[q];
-                }
-                if (ballot(mB[q] != 0u)) {
-                    const int X = sB[q] + sh, A = X & ~3;
-                    uint32_t lo, hi;
-                    if (fB[q]) { lo = out_dw(O.out.r, A, rec); hi = out_dw(O.out.r, A + 4, rec); }
-                    else { lo = O.dword(A); hi = O.dword(A + 4); }
-                    V |= __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)X & 3u) & mB[q];
-                }
-            }
-            if (ballot(slow)) {
-                if (slow) {
-                    for (int i = max(nlp, vlo); i < min(4, vhi); i++) {
-                        if ((i >= nlp && i < j1) || i >= nlm) {
-                            const bool qm = i >= j1;
-                            const int lend = qm ? lend_m : lend_p, of = max(qm ? off_m : off_p, 1);
-                            const int s = op + lend - of + (int)((uint32_t)(ob0 + i - lend) % (uint32_t)of);
-                            uint32_t v;
-                            if (s >= xown) v = (V >> (8 * (s - xown))) & 0xffu;
-                            else if (s >= thr) v = O.get(s);
-                            else v = O.out.b_sc1(s);
-                            V = (V & ~(0xffu << (8 * i))) | (v << (8 * i));
-                        }
-                    }
-                }
-            }
-            return V;
-        };
-        if (anyfar) wait_vm();   // (the flushed bytes' stores are done before they are read back)
-        const uint32_t vm = bytes_mask(vlo, vhi);
-        uint64_t dm = ballot(vm == 0u);
-        for (int r = 0; r <= LZH_WAVE; r++) {
-            const bool go = !lane_on(dm) && (need & ~dm) == 0ull;
-            const uint64_t gm = ballot(go);
-            if (!gm) break;
-            DST(4, 1);
-            if (go) {
-                uint32_t V = value();
-                if (vm != 0xffffffffu) V = (O.dword(Xw) & ~vm) | (V & vm);   // the group's first / last dword
-                O.put_dword(Xw, V);
-            }
-            wave_lds_fence();
-            dm |= gm;
-        }
-        (void)lmask;
-        O.maybe_flush(min(pend, op + total), lane);
-    }
-}
-
 // Lanes on the chain that starts at lane 0 and follows `link` (next lane, strictly increasing;
 // >= 64 = leaves the group, 255 = the lane itself is not taken), by binary lifting: jump tables
 // J_k = link^(2^k) through ds_bpermute, then every lane lifts from lane 0 to the furthest chain
@@ -737,11 +521,8 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
         const int ip_next = ip + rdlanei(pe - ip, lastk);
         DCLK(t1);
         DMARK(3);
-        if (LZH_DEC_EMIT4)   // (every LZ4 sequence produces >= 4 bytes)
-            emit_group4(w, O, mark, ip, op, total, keep, excl, lit, p1 - ip, off, cap, lane);
-        else
-            emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)ml << 16),
-                       (uint32_t)(p1 - ip), off, lane);
+        emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)ml << 16), (uint32_t)(p1 - ip),
+                   off, lane);
 #if LZH_DEC_STATS
         DCLK(t2);
         DST(0, 1);
@@ -867,12 +648,8 @@ __device__ int snappy_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t*
         const int lastk = 63 - __builtin_clzll(keep);
         const int total = rdlanei(incl, lastk);
         const int ip_next = ip + rdlanei(nx - ip, lastk);
-        // (1..3-byte tags, offsets past 16 bits: two bytes per lane)
-        if (LZH_DEC_EMIT4 && !ballot(lane_on(keep) && (len < 4 || off > 0xffff)))
-            emit_group4(w, O, mark, ip, op, total, keep, excl, lit, p1 - ip, off, cap, lane);
-        else
-            emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)(len - lit) << 16),
-                       (uint32_t)(p1 - ip), off, lane);
+        emit_group(w, O, mark, ip, op, total, keep, excl, (uint32_t)lit | ((uint32_t)(len - lit) << 16),
+                   (uint32_t)(p1 - ip), off, lane);
         op += total;
         ip = ip_next;
     }
@@ -941,17 +718,9 @@ __device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, c
 #endif
 }
 
-#ifndef LZH_DEC_W8
-#define LZH_DEC_W8 0
-#endif
-#if LZH_DEC_W8
-#define LZH_DEC_WAVES __attribute__((amdgpu_waves_per_eu(8, 8)))
-#else
-#define LZH_DEC_WAVES
-#endif
 // output window | start marks | input ring
 #define LZH_DEC_KERNEL(NAME, KW)                                                                            \
-    extern "C" __global__ void __launch_bounds__(64) LZH_DEC_WAVES                                         \
+    extern "C" __global__ void __launch_bounds__(64)                                                       \
     NAME(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,              \
          const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out, int32_t* status,     \
          uint32_t chunk0, const uint32_t* desc) {                                                          \

@@ -31,5 +31,3 @@ print("  members/group %.2f  bytes/group %.1f  passes/group %.2f" % (v[1] / max(
 tot = v[12] or 1
 print("  clocks/chunk %.0f: parse %.1f%%  emit %.1f%%  checked %.1f%%  other %.1f%%" % (
     tot / k, 100 * v[8] / tot, 100 * v[9] / tot, 100 * v[10] / tot, 100 * (tot - v[8] - v[9] - v[10]) / tot))
-print("  emit_group4 lanes per pass: slow %.2f  waiting on in-pass sources %.2f  far %.2f" % (
-    v[13] / max(v[2], 1), v[14] / max(v[2], 1), v[15] / max(v[2], 1)))
