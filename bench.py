@@ -404,7 +404,11 @@ def main():
     total_bytes = world * n * args.steps
     value = total_bytes / elapsed / 1e6
     kname = COMPRESS_KERNEL[args.codec]
-    dname = DECOMPRESS_KERNEL.get(args.codec, "lzh_decompress_v2_kernel")
+    dname = DECOMPRESS_KERNEL.get(args.codec)
+    if dname is None:   # LZ4 / snappy: the output-window variant the launcher picks for this many chunks
+        import ctypes
+        kw = L.lib().lzh_debug_decode_window(ctypes.c_uint32(-(-n // chunk)))
+        dname = {8192: "lzh_decompress_w8k_kernel", 16384: "lzh_decompress_w16k_kernel"}.get(kw, "lzh_decompress_v2_kernel")
     res = {
         "metric": metric_for(args.codec, args.chunk_kib, n, args.corpus, args.level),
         "value": round(value, 2),

@@ -2974,11 +2974,11 @@ extern "C" int lzh_debug_force_decode_window(int kw) {
     return 0;
 }
 
-hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
-                                 const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
-                                 int32_t* status, uint32_t nchunks, hipStream_t s, const void* desc) {
-    if (nchunks == 0) return hipSuccess;
-    // waves per CU by LDS (160 KiB; allocation in 512-byte granules; at most 32 waves), per window
+// The LZ4 / snappy decoder's LDS output window for a launch of nchunks on the current device: the
+// widest whose occupancy (waves per CU by LDS: 160 KiB in 512-byte granules, at most 32 waves) still
+// holds every chunk at once; 4096 = lzh_decompress_v2_kernel, 8192 = _w8k, 16384 = _w16k.
+static int decode_window(uint32_t nchunks) {
+    if (g_force_window) return g_force_window;
     static int cus[64];
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -2989,14 +2989,21 @@ hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t pack
         const int lds = (kw + 3 * LZH_WAVE + kRingBytes + 511) / 512 * 512;
         return (uint64_t)nchunks <= (uint64_t)cus[dev] * (uint64_t)min(32, 160 * 1024 / lds);
     };
-    auto k = lzh_decompress_v2_kernel;
-    if (g_force_window) {
-        if (g_force_window == 8192) k = lzh_decompress_w8k_kernel;
-        else if (g_force_window == 16384) k = lzh_decompress_w16k_kernel;
-    } else if (LZH_DEC_WIDE && cus[dev] > 0) {
-        if (LZH_DEC_WIDE >= 2 && fits(16384)) k = lzh_decompress_w16k_kernel;
-        else if (fits(8192)) k = lzh_decompress_w8k_kernel;
+    if (LZH_DEC_WIDE && cus[dev] > 0) {
+        if (LZH_DEC_WIDE >= 2 && fits(16384)) return 16384;
+        if (fits(8192)) return 8192;
     }
+    return 4096;
+}
+// (bench.py names the decode kernel a launch of nchunks runs)
+extern "C" int lzh_debug_decode_window(uint32_t nchunks) { return decode_window(nchunks); }
+
+hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                                 const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
+                                 int32_t* status, uint32_t nchunks, hipStream_t s, const void* desc) {
+    if (nchunks == 0) return hipSuccess;
+    const int kw = decode_window(nchunks);
+    auto k = kw == 16384 ? lzh_decompress_w16k_kernel : kw == 8192 ? lzh_decompress_w8k_kernel : lzh_decompress_v2_kernel;
     hipLaunchKernelGGL(k, dim3(nchunks), dim3(64), 0, s, codec, packed, packed_readable, offsets, csizes, n_total,
                        chunk_size, out, status, 0u, (const uint32_t*)desc);
     if (desc && codec == 0)   // LZ4 frames: the linked ones (descriptors the kernel above skipped)
