@@ -407,8 +407,17 @@ def main():
     dname = DECOMPRESS_KERNEL.get(args.codec)
     if dname is None:   # LZ4 / snappy: the output-window variant the launcher picks for this many chunks
         import ctypes
-        kw = L.lib().lzh_debug_decode_window(ctypes.c_uint32(-(-n // chunk)))
-        dname = {8192: "lzh_decompress_w8k_kernel", 16384: "lzh_decompress_w16k_kernel"}.get(kw, "lzh_decompress_v2_kernel")
+        win = {8192: "lzh_decompress_w8k_kernel", 16384: "lzh_decompress_w16k_kernel"}
+
+        def wkernel(nchunks):
+            return win.get(L.lib().lzh_debug_decode_window(ctypes.c_uint32(nchunks)), "lzh_decompress_v2_kernel")
+        k_all = -(-n // chunk)
+        frags = -(-chunk // 65536)
+        if args.codec == "snappy" and 8 <= frags <= 64:   # split scan, fragments, join, the chunks decoded whole
+            names = ["lzh_snappy_split_kernel", wkernel(k_all * frags), "lzh_snappy_join_kernel", wkernel(k_all)]
+            dname = "+".join(dict.fromkeys(names))
+        else:
+            dname = wkernel(k_all)
     res = {
         "metric": metric_for(args.codec, args.chunk_kib, n, args.corpus, args.level),
         "value": round(value, 2),

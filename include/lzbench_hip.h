@@ -137,10 +137,13 @@ int lzh_debug_gather_order(size_t nsb, const uint64_t* order, const uint64_t* si
 int lzh_compress_async(int codec, int level, const void* d_in, size_t n, size_t in_readable, size_t chunk_size,
                        void* d_packed, size_t packed_cap, uint32_t* d_csizes, uint64_t* d_offsets,
                        void* d_temp, size_t temp_bytes, void* hip_stream);
-/* d_offsets may be NULL (then derived from d_csizes into d_temp).  d_temp / temp_bytes: LZ4 and snappy use
- * temp only for those derived offsets; LZ4 frames / nvcomp need lzh_decompress_temp_bytes; zstd runs its
+/* d_offsets may be NULL (then derived from d_csizes into d_temp).  d_temp / temp_bytes: LZ4 uses temp only
+ * for those derived offsets; LZ4 frames / nvcomp need lzh_decompress_temp_bytes; zstd runs its
  * four-kernel decoder in temp when temp_bytes >= lzh_decompress_temp_bytes (chunks of 16 KiB and more),
- * else every frame in the one-wave decoder (same results, slower).  d_status: nchunks i32,
+ * else every frame in the one-wave decoder (same results, slower); snappy chunks of 512 KiB .. 4 MiB
+ * (8..64 fragments of 64 KiB) decode a fragment per wave (split at the tag that starts each fragment,
+ * whole where that is not possible) when temp_bytes >= lzh_decompress_temp_bytes, else whole (same
+ * results, slower).  d_status: nchunks i32,
  * decoded size per chunk or negative on malformed input (zstd / LZ4 frame / nvcomp container:
  * -1 corrupt, -2 unsupported frame feature).  A chunk whose compressed size equals its size is stored raw (all codecs).
  * Replaces (zstd): lzbench_zstd_decompress, compressors.cpp:1767-1773 (ZSTD_decompressDCtx). */

@@ -172,6 +172,7 @@ size_t lzh_decompress_temp_bytes(int codec, size_t n, size_t chunk_size) {
         t += align_up(nd * 32, 256) + align_up(nd * 4, 256) + align_up(k * 4, 256) + 256;
     }
     if (codec == LZH_CODEC_ZSTD) t += lzh_zstd_decode_temp(n, chunk_size);   // the split decoder (decode_hip.hip)
+    if (codec == LZH_CODEC_SNAPPY) t += lzh_snappy_split_temp(n, chunk_size); // fragment-parallel decode
     return t;
 }
 
@@ -345,9 +346,16 @@ int lzh_decompress_async(int codec, const void* d_packed, size_t packed_readable
                                           bstat, fstat, (const uint8_t*)d_out, d_status, (uint32_t)k, s));
         return LZH_OK;
     }
+    // snappy chunks of several 64 KiB fragments decode a fragment per wave when temp has room for the split
+    // (else, or for chunks of one fragment, whole)
+    const size_t sst = codec == LZH_CODEC_SNAPPY ? lzh_snappy_split_temp(n, chunk_size) : 0;
     if (codec == LZH_CODEC_ZSTD)
         LZH_CHECK(lzh_launch_zstd_decompress((const uint8_t*)d_packed, packed_readable, offs, d_csizes, n, chunk_size,
                                              (uint8_t*)d_out, d_status, (uint32_t)k, zt, s));
+    else if (sst && d_temp && temp_bytes >= scan_bytes + sst)
+        LZH_CHECK(lzh_launch_snappy_split_decompress((const uint8_t*)d_packed, packed_readable, offs, d_csizes, n,
+                                                     chunk_size, (uint8_t*)d_out, d_status, (uint32_t)k,
+                                                     (uint8_t*)d_temp + scan_bytes, s));
     else
         LZH_CHECK(lzh_launch_decompress(codec, (const uint8_t*)d_packed, packed_readable, offs, d_csizes, n,
                                         chunk_size, (uint8_t*)d_out, d_status, (uint32_t)k, s));

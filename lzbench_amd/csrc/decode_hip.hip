@@ -543,15 +543,17 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
 // of snappy_decode below (snappy.cc:848-952) are checked per member against the prefix sum, and
 // the group is cut before the first failure (which, like 2..4-byte literal lengths, runs through
 // the checked per-tag path).
+// (nohdr: a fragment of a stream -- its tags without the varint, decoding exactly cap bytes; see
+// lzh_snappy_split_kernel)
 template <class SinkType>
 __device__ int snappy_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* mark, LDSA uint8_t* ring, int cap,
-                             int lane) {
+                             int lane, bool nohdr = false) {
     Win w;
     w.bind(in, ring);
     w.load(0, lane);
     int ip = 0;
-    uint32_t ulen = 0;
-    for (int shift = 0;; shift += 7) {
+    uint32_t ulen = nohdr ? (uint32_t)cap : 0u;
+    for (int shift = 0; !nohdr; shift += 7) {
         if (ip >= cs || shift >= 32) return -1;
         const uint32_t c = w.byte(ip++);
         const uint32_t val = c & 0x7fu;
@@ -671,7 +673,7 @@ __device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, c
     const uint64_t chunk = (uint64_t)blockIdx.x + chunk0;
     uint64_t ooff, ioff;
     int part, cs;
-    bool raw;
+    bool raw, nohdr = false;
     if (desc) {   // framed layouts: one 32-byte block descriptor each (frame_hip.hip FrameDesc)
         const uint32_t* d = desc + 8 * chunk;
         ioff = (uint64_t)uni(d[1]) << 32 | uni(d[0]);
@@ -680,7 +682,8 @@ __device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, c
         part = (int)uni(d[5]);
         const uint32_t fl = uni(d[6]);
         raw = (fl & 1u) != 0;
-        if (fl & 6u) return;                    // a linked frame's block: lzh_decompress_linked_kernel
+        nohdr = (fl & 8u) != 0;                 // a snappy fragment (lzh_snappy_split_kernel)
+        if (fl & 22u) return;                   // a linked frame's block: lzh_decompress_linked_kernel; 16: skip
         if (part == 0) { if (lane == 0) status[chunk] = 0; return; }   // unused slot
     } else {
         ooff = chunk * chunk_size;
@@ -707,7 +710,7 @@ __device__ __forceinline__ void decompress_chunk(LDSA uint8_t* win, int codec, c
         LDSA uint8_t* mark = win + KW;
         LDSA uint8_t* ring = mark + 3 * LZH_WAVE;
         r = codec == 0 ? groups::lz4_decode(rin, cs, O, mark, ring, part, lane)
-                       : groups::snappy_decode(rin, cs, O, mark, ring, part, lane);
+                       : groups::snappy_decode(rin, cs, O, mark, ring, part, lane, nohdr);
         if (r > 0) O.flush(r, lane);
     }
     if (lane == 0) status[chunk] = r;
@@ -778,6 +781,155 @@ lzh_decompress_linked_kernel(const uint8_t* packed, uint64_t packed_readable, ui
             for (uint32_t bj = bi + 1 + (uint32_t)lane; bj < nlink; bj += LZH_WAVE) status[chunk + bj] = -1;
             break;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Snappy chunks of more than one 64 KiB fragment, decoded a fragment per wave.  The reference
+// compressor compresses every 64 KiB fragment of its input on its own (snappy.cc:1042-1072: a fresh
+// table per fragment, candidates only inside it), so the tags of a stream it wrote start anew at every
+// multiple of 64 KiB of output and no copy reaches into an earlier fragment.  lzh_snappy_split_kernel
+// walks a chunk's tags (one wave per chunk: every lane parses the tag at ip + lane, a scalar walk
+// follows the next-tag links and sums the output lengths) and records the tag that starts each
+// fragment; the fragments then decode in parallel as headerless streams of exactly their size
+// (descriptor flag 8).  A chunk that the walk does not split cleanly (a tag across a fragment start, a
+// varint that is not the chunk's size, a stored chunk, a walk off the stream) or any fragment of which
+// fails (a copy into an earlier fragment is valid snappy, just not what the reference writes) is
+// decoded whole by the serial decoder afterwards, so every verdict and every byte of such a chunk is
+// the serial decoder's.  An accepted split decodes the same tags in the same order as the serial
+// decoder: the fragments partition the chunk's tag sequence, each ends exactly at its share of the
+// stream and of the output, and a copy accepted inside a fragment is accepted in the chunk.
+namespace snsplit {
+constexpr int kFragLog = 16;
+constexpr uint32_t kMaxFrags = 64;   // chunks of up to 4 MiB (larger ones decode whole)
+constexpr uint32_t kMinFrags = 8;    // (by default; see lzh_snappy_split_temp)
+__host__ __device__ inline uint32_t frags(uint64_t chunk_size) { return (uint32_t)((chunk_size + 65535) >> kFragLog); }
+}
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_snappy_split_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                        const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint32_t F, uint32_t* desc,
+                        uint32_t* cflag) {
+    using namespace snsplit;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRingBytes];
+    __shared__ uint32_t bnd[kMaxFrags + 1];
+    const int lane = threadIdx.x;
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t ooff = chunk * chunk_size;
+    if (ooff >= n_total) return;
+    const int part = (int)min(chunk_size, n_total - ooff);
+    const uint64_t ioff = offsets[chunk];
+    const int cs = (int)csizes[chunk];
+    const int nf = (part + (1 << kFragLog) - 1) >> kFragLog;
+    bool ok = cs != part && nf > 1 && nf <= (int)F && F <= kMaxFrags;
+    int ip = 0, op = 0, nb = 0;
+    if (ok) {   // (a uniform walk: ip, op, nb in scalar registers)
+        const uint64_t readable = ioff < packed_readable ? min<uint64_t>(packed_readable - ioff, (uint64_t)cs + 16) : 0;
+        Bytes rin;
+        rin.init(packed + ioff, readable);
+        Win w;
+        w.bind(rin, (LDSA uint8_t*)ring);
+        w.load(0, lane);
+        uint32_t ulen = 0;
+        for (int shift = 0;; shift += 7) {   // varint32 uncompressed length (snappy.cc:1319-1331)
+            if (ip >= cs || shift >= 32) { ok = false; break; }
+            const uint32_t c = w.byte(ip++);
+            ulen |= (c & 0x7fu) << shift;
+            if (c < 128) break;
+        }
+        ok = ok && ulen == (uint32_t)part;
+        if (lane == 0) bnd[0] = (uint32_t)ip;   // fragment 0 starts after the varint
+        nb = 1;
+        for (int guard = 0; ok && ip < cs && guard <= cs; guard++) {
+            ip = unii(ip); op = unii(op); nb = unii(nb);
+            if (!w.covers(ip, ip + 2 * LZH_WAVE)) w.load(ip, lane);
+            // the tag at x = ip + lane: its stream length and output length (snappy.cc:848-952)
+            const int x = ip + lane;
+            const uint32_t tw = w.lane_word(x);
+            const uint32_t c = tw & 0xffu, kind = c & 3u;
+            uint32_t tw2 = 0;                       // (a 4-byte literal length reaches byte x + 4)
+            if (ballot(c == 0xfcu)) tw2 = w.lane_word(x + 1);
+            uint32_t len, sl;                       // output bytes, stream bytes after the tag byte
+            if (kind == 0) {
+                const uint32_t l6 = (c >> 2) + 1u;
+                const uint32_t eb = l6 > 60u ? l6 - 60u : 0u;   // 1..4 length bytes
+                const uint32_t v = eb == 4u ? tw2 : ((tw >> 8) & ((1u << (8u * eb)) - 1u));
+                const uint32_t l = eb ? (v >= 0x00ffffffu ? 0x00ffffffu : v + 1u) : l6;   // (beyond any chunk)
+                len = l;
+                sl = eb + l;
+            } else {
+                len = kind == 1 ? ((c >> 2) & 7u) + 4u : (c >> 2) + 1u;
+                sl = kind == 1 ? 1u : (kind == 2 ? 2u : 4u);
+            }
+            const int adv_l = lane + 1 + (int)sl;              // next tag, from ip (> lane)
+            // the chain from lane 0 (binary lifting, as the decoder's groups); lanes at or past the
+            // stream's end are not tags
+            // (255 is chain_members' "not a tag": a real link that leaves the window is any value >= 64)
+            const int link = x >= cs ? 255 : min(adv_l, 254);
+            const uint64_t M = groups::chain_members(link, lane);
+            const bool mem = lane_on(M);
+            const int L = mem ? (int)len : 0;
+            const int incl = groups::wave_incl_scan(L);
+            const int start = op + incl - L;                   // a member's first output byte
+            // a member starting on a multiple of 64 KiB starts that fragment
+            const bool fb = mem && start > 0 && (start & ((1 << kFragLog) - 1)) == 0 && (start >> kFragLog) < nf;
+            if (fb) bnd[start >> kFragLog] = (uint32_t)x;
+            nb += __builtin_popcountll(ballot(fb));
+            const int lastk = 63 - __builtin_clzll(M | 1ull);
+            op += rdlanei(incl, lastk);
+            ip += rdlanei(adv_l, lastk);
+            if (op > part) ok = false;
+        }
+        ok = ok && ip == cs && op == part && nb == nf;
+    }
+    wave_lds_fence();
+    uint32_t* D = desc + chunk * (uint64_t)F * 8;
+    for (int j = lane; j < (int)F; j += LZH_WAVE) {   // fragment j; unused slots decode nothing (ds = 0)
+        uint32_t a = 0, e = 0, ds = 0;
+        if (ok && j < nf) {
+            a = bnd[j];
+            e = j + 1 < nf ? bnd[j + 1] : (uint32_t)cs;
+            ds = (uint32_t)min(1 << kFragLog, part - (j << kFragLog));
+        }
+        const uint64_t src = ioff + a, dst = ooff + ((uint64_t)j << kFragLog);
+        uint32_t* d = D + 8 * j;
+        d[0] = (uint32_t)src; d[1] = (uint32_t)(src >> 32);
+        d[2] = (uint32_t)dst; d[3] = (uint32_t)(dst >> 32);
+        d[4] = e - a; d[5] = ds; d[6] = 8u; d[7] = 0u;
+    }
+    if (lane == 0) cflag[chunk] = ok ? 0u : 1u;
+}
+
+// chunks finished by fragments since the last reset (tests: lzh_debug_snappy_split_done)
+__device__ unsigned long long lzh_snsplit_done;
+
+// per chunk: split and every fragment decoded exactly its size -> the chunk's status; else a whole-chunk
+// descriptor for the serial pass (flag 16 = skip for the others)
+extern "C" __global__ void __launch_bounds__(256)
+lzh_snappy_join_kernel(const uint64_t* offsets, const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size,
+                       uint32_t F, const uint32_t* desc, const int32_t* fstat, const uint32_t* cflag, uint32_t* sdesc,
+                       int32_t* status, uint32_t nchunks) {
+    const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (c >= nchunks) return;
+    const uint64_t ooff = c * chunk_size;
+    const uint32_t part = (uint32_t)min(chunk_size, n_total - ooff);
+    bool whole = cflag[c] != 0u;
+    for (uint32_t j = 0; !whole && j < F; j++) {
+        const uint32_t ds = desc[(c * F + j) * 8 + 5];
+        if (ds && fstat[c * F + j] != (int32_t)ds) whole = true;
+    }
+    uint32_t* S = sdesc + c * 8;
+    if (whole) {
+        const uint64_t io = offsets[c];
+        const uint32_t cs = csizes[c];
+        S[0] = (uint32_t)io; S[1] = (uint32_t)(io >> 32);
+        S[2] = (uint32_t)ooff; S[3] = (uint32_t)(ooff >> 32);
+        S[4] = cs; S[5] = part; S[6] = cs == part ? 1u : 0u; S[7] = 0u;
+    } else {
+        S[0] = S[1] = S[2] = S[3] = S[4] = S[5] = S[7] = 0u;
+        S[6] = 16u;
+        status[c] = (int32_t)part;
+        atomicAdd(&lzh_snsplit_done, 1ull);
     }
 }
 
@@ -3010,6 +3162,57 @@ hipError_t lzh_launch_decompress(int codec, const uint8_t* packed, uint64_t pack
         hipLaunchKernelGGL(lzh_decompress_linked_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, out,
                            status, (const uint32_t*)desc);
     return hipGetLastError();
+}
+
+// The split pays where a chunk's serial decode is long against the walk: from 8 fragments (512 KiB)
+// (mixed 1 GiB: -b256 walk 3.1 + fragments 3.3 ms against 6.5 ms whole; -b1024 9.2 + 3.4 against 18.5 ms;
+// profiles/r05_snsplit).  Test hooks: the mode (0 off: every chunk whole; 1 from kMinFrags fragments;
+// 2 from 2 fragments), and the number of chunks finished by fragments (reset with reset != 0).
+static int g_snappy_split = 1;
+extern "C" int lzh_debug_snappy_split(int mode) {
+    if (mode < 0 || mode > 2) return -1;
+    g_snappy_split = mode;
+    return 0;
+}
+extern "C" long long lzh_debug_snappy_split_done(int reset) {
+    unsigned long long v = 0;
+    if (reset) return hipMemcpyToSymbol(HIP_SYMBOL(lzh_snsplit_done), &v, sizeof(v)) == hipSuccess ? 0 : -1;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(lzh_snsplit_done), sizeof(v)) != hipSuccess) return -1;
+    return (long long)v;
+}
+
+// temp for the fragment-parallel snappy decode (0: chunks of one fragment, or too large to split):
+// fragment descriptors (32 B) and statuses, per-chunk split flags and whole-chunk descriptors
+size_t lzh_snappy_split_temp(uint64_t n, uint64_t chunk_size) {
+    const uint32_t F = snsplit::frags(chunk_size);
+    if (!g_snappy_split || F < (g_snappy_split == 2 ? 2u : snsplit::kMinFrags) || F > snsplit::kMaxFrags || n == 0)
+        return 0;
+    const uint64_t k = (n + chunk_size - 1) / chunk_size;
+    auto al = [](uint64_t v) { return (v + 255) & ~(uint64_t)255; };
+    return (size_t)(al(k * F * 32) + al(k * F * 4) + al(k * 4) + al(k * 32) + 256);
+}
+
+hipError_t lzh_launch_snappy_split_decompress(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                                              const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
+                                              int32_t* status, uint32_t nchunks, uint8_t* temp, hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    const uint32_t F = snsplit::frags(chunk_size);
+    const uint64_t k = nchunks;
+    auto al = [](uint64_t v) { return (v + 255) & ~(uint64_t)255; };
+    uint32_t* desc = (uint32_t*)temp;
+    int32_t* fstat = (int32_t*)(temp + al(k * F * 32));
+    uint32_t* cflag = (uint32_t*)(temp + al(k * F * 32) + al(k * F * 4));
+    uint32_t* sdesc = (uint32_t*)(temp + al(k * F * 32) + al(k * F * 4) + al(k * 4));
+    if (k * F > 0xffffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(lzh_snappy_split_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
+                       n_total, chunk_size, F, desc, cflag);
+    hipError_t e = lzh_launch_decompress(1, packed, packed_readable, nullptr, nullptr, n_total, chunk_size, out, fstat,
+                                         (uint32_t)(k * F), s, desc);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lzh_snappy_join_kernel, dim3((nchunks + 255) / 256), dim3(256), 0, s, offsets, csizes, n_total,
+                       chunk_size, F, desc, fstat, cflag, sdesc, status, nchunks);
+    return lzh_launch_decompress(1, packed, packed_readable, nullptr, nullptr, n_total, chunk_size, out, status, nchunks,
+                                 s, sdesc);
 }
 
 hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,

@@ -18,6 +18,11 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
                                       const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                       int32_t* status, uint32_t nchunks, uint8_t* zt, hipStream_t s);
 size_t lzh_zstd_decode_temp(uint64_t n, uint64_t chunk_size);
+// snappy chunks of more than one 64 KiB fragment: split scan, fragments in parallel, serial fallback
+size_t lzh_snappy_split_temp(uint64_t n, uint64_t chunk_size);
+hipError_t lzh_launch_snappy_split_decompress(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
+                                              const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
+                                              int32_t* status, uint32_t nchunks, uint8_t* temp, hipStream_t s);
 // smallest chunk the zstd split decoder takes (below it: the one-wave decoder, no temp)
 constexpr uint64_t lzh_zstd_split_min = 16384;
 hipError_t lzh_launch_scan(const uint32_t* csizes, uint64_t nchunks, uint64_t* offsets, uint64_t* total,
