@@ -224,3 +224,19 @@ def test_corrupt_split_streams_verdicts(torch_cuda):
             assert (st_on[i] >= 0) == ok, f"stream {i}: gpu {st_on[i]} reference {ok}"
             if ok:
                 assert st_on[i] == ulen and out_on[i * cap: i * cap + ulen].tobytes() == dst[:ulen].tobytes()
+
+
+def test_split_through_the_batch_rows(torch_cuda):
+    """lzbench's chunk loop (lzbench_hip_decompress_batch, sub-batches with their own temp) at -b1024 takes
+    the split path too, against the reference digest of the same stream"""
+    n = 40 * (1 << 20) + 12345
+    chunk = 1 << 20
+    data = L.datagen("mixed", n, seed=77)
+    packed, cs = L.compress_chunks(data, "snappy", chunk)
+    if O.have_ref():
+        rp, rcs = O.compress_chunks(data, "snappy", chunk, use_ref=True)
+        assert (cs == rcs).all() and len(packed) == len(rp) and (packed == rp).all()
+    _done(reset=True)
+    out = L.decompress_chunks(packed, cs, n, "snappy", chunk)
+    assert _done() > 0
+    assert (out[:n] == data).all()
