@@ -2835,8 +2835,17 @@ lzh_zstd_hdr_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
 // tl-bit lookup, bits below the stream start read as zero); uniform points every kHB steps as in the
 // sequence kernel.  A stream not consumed exactly (huf_streams' verdict 1) sends its frame to the
 // one-wave decoder when the reference would use the double-symbol decoder there, else it is corrupt.
+#ifndef LZH_HUFPAR_GLOBAL
+#define LZH_HUFPAR_GLOBAL 0
+#endif
 namespace zsplit {
 constexpr int kHB = 16;                          // steps between uniform points (= bytes staged per lane)
+// streams lzh_zstd_hufpar_kernel decodes a wave each (the rest: a lane each here)
+constexpr int kParMin = 4096;                   // symbols (>= 64 bits a share)
+constexpr int kParCap = 40 * 1024;              // stream bytes staged in LDS
+__host__ __device__ inline bool huf_par(int on, int nsym, uint32_t sz) {
+    return on && nsym >= kParMin && sz + 8 <= (uint32_t)kParCap;
+}
 }  // namespace zsplit
 
 // HJ sections a wave (4 HJ lanes in use).  The kernel is bound by instruction issue, not by its LDS round
@@ -2847,7 +2856,7 @@ template <int HJ>
 __device__ __forceinline__ void zstd_huf(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,
                                          uint64_t n_total, uint64_t chunk_size, uint8_t* out, int32_t* status,
                                          uint8_t* zt, int32_t* zst, const zsplit::ZHuf* jobs, const uint32_t* njobs,
-                                         unsigned long long* stats) {
+                                         unsigned long long* stats, int par) {
     using namespace zsplit;
     using namespace zstdd;
     constexpr int kHJ = HJ, kHL = 4 * kHJ;          // sections a wave, lanes in use
@@ -2865,7 +2874,8 @@ __device__ __forceinline__ void zstd_huf(const uint8_t* packed, uint64_t packed_
         jf = J->frame; jtblk = J->tblk; jtl = J->tl; jx2 = J->x2; jns = J->ns; jdst = J->dst; jseg = J->seg;
         jlast = J->last; js0 = J->s0[j]; jsz = J->sz[j];
     }
-    bool slive = jlive && zst[jf] == kGo && (uint32_t)j < jns;
+    bool slive = jlive && zst[jf] == kGo && (uint32_t)j < jns &&
+                 !huf_par(par, j == 3 ? (int)jlast : (int)jseg, jsz);   // (long streams: lzh_zstd_hufpar_kernel)
     const ZLayout Z = zlayout(chunk_size);
     // resources from the wave's lowest frame: the packed streams and the table slots (per-lane 32-bit
     // offsets; a section whose offsets would not fit goes to the one-wave decoder)
@@ -3028,17 +3038,155 @@ __device__ __forceinline__ void zstd_huf(const uint8_t* packed, uint64_t packed_
     }
 }
 
+// Long Huffman streams, one per WAVE (self-synchronising parallel decode).  A 4-stream literal section of a
+// frame with few matches holds up to 32 K symbols a stream, and one lane's serial decode of it -- two
+// dependent LDS round trips a symbol -- bounds lzh_zstd_huf_kernel (config 5's 512 MiB share: a third of
+// the frames are whole-block literals).  Here the stream's bits are cut into 64 equal shares, one per lane:
+// every lane decodes its share from its top (lane 0 from the stream's start, the others from a guess),
+// recording where its chain leaves the share and how many symbols it took; a lane whose true start -- the
+// previous lane's exit -- differs from the one it used decodes again from there (Huffman codes
+// resynchronise within a few symbols, so after one such round the exits no longer move); the symbol
+// counts' prefix sum places every share's output, and a last pass writes it.  The chain from the stream's
+// start is the serial decoder's, so the verdict is huf_streams': exact iff it ends exactly at the start of
+// the stream's bits after exactly nsym symbols (else the frame goes to the one-wave decoder (X2) or is
+// corrupt, as in lzh_zstd_huf_kernel).
+
+extern "C" __global__ void __launch_bounds__(64)
+lzh_zstd_hufpar_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t chunk_size,
+                       uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst, const zsplit::ZHuf* jobs,
+                       const uint32_t* njobs, int par) {
+    using namespace zsplit;
+    using namespace zstdd;
+#if !LZH_HUFPAR_GLOBAL
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[kParCap / 4 + 128];   // dword d of the stream at d + 1
+#endif
+    __shared__ __attribute__((aligned(16))) uint16_t tab[2048];
+    const int lane = threadIdx.x;
+    const uint32_t jid = blockIdx.x >> 2, j = blockIdx.x & 3u;
+    if (jid >= *njobs) return;
+    const ZHuf* J = jobs + jid;
+    const uint32_t jf = uni(J->frame), jns = uni(J->ns), jseg = uni(J->seg), jlast = uni(J->last);
+    if (j >= jns) return;
+    const int nsym = (int)(j == 3 ? jlast : jseg);
+    const uint32_t sz = uni(J->sz[j]);
+    if (!huf_par(par, nsym, sz) || uni((uint32_t)zst[jf]) != (uint32_t)kGo) return;
+    const ZLayout Z = zlayout(chunk_size);
+    const int tl = (int)uni(J->tl);
+    {   // the section's table (2^11 16-bit cells: symbol | nbBits << 8)
+        const uint32_t* tb = (const uint32_t*)(zt + (uint64_t)jf * Z.stride + Z.hufs() + (uint64_t)uni(J->tblk) * kHufSlot);
+        for (int i = lane; i < 1024; i += LZH_WAVE) ((LDSA uint32_t*)tab)[i] = tb[i];
+    }
+    // the stream's bytes [A, A + X] (A 4-aligned, the stream starting at byte x0), bits below its start zero
+    const int64_t s0 = (int64_t)offsets[jf] + (int64_t)uni(J->s0[j]);
+    const int64_t A = s0 & ~3ll;
+    const int x0 = (int)(s0 & 3), X = x0 + (int)sz - 1;
+    const int lo = 8 * x0;
+    const int nd = (X + 4) >> 2;
+    const int64_t avail = (int64_t)packed_readable - A;
+    const rsrc_t r = make_rsrc(packed + A, (uint32_t)max<int64_t>(0, min<int64_t>(avail, (int64_t)nd * 4)));
+#if LZH_HUFPAR_GLOBAL
+    // (the stream's bits from memory: per lane the two dwords under the reader and the next lower one in
+    // flight -- a lane reads its share downwards)
+    wait_vm();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    const uint32_t lastb = (ld_b32(r, 4 * (X >> 2)) >> (8 * (X & 3))) & 0xffu;
+    int cd = -1000;
+    uint32_t c0 = 0, c1 = 0, cn = 0;
+    auto ldd = [&](int d) -> uint32_t { return d <= 0 ? 0u : ld_b32(r, 4 * (d - 1)); };   // (d: dword d - 1)
+    auto bits = [&](int bq) -> uint32_t {
+        const int b = bq + 32, d = b >> 5;
+        if (d != cd) {
+            if (d == cd - 1) { c1 = c0; c0 = cn; }
+            else { c0 = ldd(d); c1 = ldd(d + 1); }
+            cd = d;
+            cn = ldd(d - 1);
+        }
+        uint32_t v = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(c1, c0, (uint32_t)b & 31u), 0u, (uint32_t)tl);
+        if (bq < lo) v &= lo - bq >= 32 ? 0u : (~0u << (lo - bq));
+        return v;
+    };
+#else
+    {
+        if (lane == 0) sbuf[0] = 0u;
+        // (LDS-DMA rows of 64 dwords, one wait; past nd the range check reads zeros)
+        for (int d0 = 0; d0 < nd + 2; d0 += LZH_WAVE)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(sbuf + 1 + d0), 4,
+                                                     4 * (d0 + lane), 0, 0, 0);
+    }
+    wait_vm();
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): table and stream in LDS
+    const uint32_t lastb = (sbuf[(X >> 2) + 1] >> (8 * (X & 3))) & 0xffu;
+    // bits [bq, bq + tl) (bq >= -32: the zero dword below the stream), zero below lo
+    auto bits = [&](int bq) -> uint32_t {
+        const int b = bq + 32, d = b >> 5;
+        const volatile LDSA uint32_t* s = (const volatile LDSA uint32_t*)sbuf;
+        uint32_t v = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(s[d + 1], s[d], (uint32_t)b & 31u), 0u, (uint32_t)tl);
+        if (bq < lo) v &= lo - bq >= 32 ? 0u : (~0u << (lo - bq));
+        return v;
+    };
+#endif
+    const int P0 = 8 * X + (lastb ? hb32(lastb) : 0);   // (the end mark: checked non-zero by the header kernel)
+    // this lane's share (P0 - lane * seg, P0 - (lane + 1) * seg], the last one down to lo
+    const int nbits = P0 - lo;
+    const int seg = (nbits + LZH_WAVE - 1) / LZH_WAVE;
+    const int top = P0 - lane * seg;
+    const int bot = lane == LZH_WAVE - 1 ? lo : max(P0 - (lane + 1) * seg, lo);
+    const int guard = seg + 64;
+    // decode the share from start: the chain's exit (the first symbol top at or below bot) and its symbols
+    auto pass = [&](bool act, int start, int& ex, int& cnt, uint8_t* wdst) {
+        int P = start, c = 0;
+#if LZH_HUFPAR_GLOBAL
+        cd = -1000;
+#endif
+        for (int it = 0; it < guard; it++) {
+            const bool go = act && P > bot;
+            if (!ballot(go)) break;
+            if (go) {
+                const uint32_t e = ((const volatile LDSA uint16_t*)tab)[bits(P - tl)];
+                if (wdst) wdst[c] = (uint8_t)e;
+                P -= (int)(e >> 8);
+                c++;
+            }
+        }
+        if (act) { ex = P; cnt = c; }
+    };
+    int start = lane == 0 ? P0 : top, ex = 0, cnt = 0;
+    pass(true, start, ex, cnt, nullptr);
+    for (int round = 0; round < LZH_WAVE; round++) {   // until every share starts where the previous one ends
+        const int prev = (int)lane_gather((uint32_t)ex, lane > 0 ? lane - 1 : 0);
+        const int want = lane == 0 ? P0 : prev;
+        const bool ch = want != start;
+        if (!ballot(ch)) break;
+        if (ch) start = want;
+        pass(ch, start, ex, cnt, nullptr);
+    }
+    const int incl = groups::wave_incl_scan(cnt);
+    const int total = rdlanei(incl, LZH_WAVE - 1);
+    const bool exact = total == nsym && rdlanei(ex, LZH_WAVE - 1) == lo;
+    if (exact) {
+        uint8_t* dst = out + (uint64_t)jf * chunk_size + uni(J->dst) + (uint64_t)j * jseg + (incl - cnt);
+        int ex2 = 0, cnt2 = 0;
+        pass(true, start, ex2, cnt2, dst);
+    } else if (lane == 0) {   // not consumed exactly: X2's verdict (the one-wave decoder) or corrupt
+        if (uni(J->x2)) {
+            atomicMax(&zst[jf], kLegacy);
+        } else if (atomicMax(&zst[jf], kDone) != kDone) {
+            status[jf] = ZC;
+        }
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_huf_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t n_total,
                     uint64_t chunk_size, uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst,
-                    const zsplit::ZHuf* jobs, const uint32_t* njobs, unsigned long long* stats) {
-    zstd_huf<4>(packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst, jobs, njobs, stats);
+                    const zsplit::ZHuf* jobs, const uint32_t* njobs, unsigned long long* stats, int par) {
+    zstd_huf<4>(packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst, jobs, njobs, stats, par);
 }
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_huf8_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t n_total,
                      uint64_t chunk_size, uint8_t* out, int32_t* status, uint8_t* zt, int32_t* zst,
-                     const zsplit::ZHuf* jobs, const uint32_t* njobs, unsigned long long* stats) {
-    zstd_huf<8>(packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst, jobs, njobs, stats);
+                     const zsplit::ZHuf* jobs, const uint32_t* njobs, unsigned long long* stats, int par) {
+    zstd_huf<8>(packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst, jobs, njobs, stats, par);
 }
 
 extern "C" __global__ void __launch_bounds__(64)
@@ -3114,6 +3262,12 @@ extern "C" int lzh_debug_zstd_legacy(int on) {
     return 0;
 }
 // Test hook: force the zstd literal kernel's sections per wave (4 or 8; 0 = by frame count)
+// Test hook: long Huffman streams one per wave (lzh_zstd_hufpar_kernel) on / off
+static int g_zstd_hufpar = 1;
+extern "C" int lzh_debug_zstd_hufpar(int on) {
+    g_zstd_hufpar = on ? 1 : 0;
+    return 0;
+}
 static int g_zstd_huf_sections = 0;
 extern "C" int lzh_debug_zstd_huf_sections(int hj) {
     if (hj != 0 && hj != 4 && hj != 8) return -1;
@@ -3255,7 +3409,10 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
                                             : hcus[hdev] > 0 && (uint64_t)nchunks >= 32ull * (uint64_t)hcus[hdev]) ? 8 : 4;
         hipLaunchKernelGGL(hj == 8 ? lzh_zstd_huf8_kernel : lzh_zstd_huf_kernel, dim3((unsigned)((maxjobs + hj - 1) / hj)),
                            dim3(64), 0, s, packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst,
-                           (const zsplit::ZHuf*)jobs, (const uint32_t*)njobs, hstats);
+                           (const zsplit::ZHuf*)jobs, (const uint32_t*)njobs, hstats, g_zstd_hufpar);
+        hipLaunchKernelGGL(lzh_zstd_hufpar_kernel, dim3((unsigned)(maxjobs * 4)), dim3(64), 0, s, packed, packed_readable,
+                           offsets, chunk_size, out, status, zt, zst, (const zsplit::ZHuf*)jobs, (const uint32_t*)njobs,
+                           g_zstd_hufpar);
 #if LZH_ZSTD_STATS
         {
             unsigned long long h[8];

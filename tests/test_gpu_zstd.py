@@ -28,13 +28,22 @@ def torch_cuda():
     return torch
 
 
-# split: the four kernels (the literal kernel's sections per wave by frame count: 4 for these sizes);
-# split8: the same with 8 sections a wave forced (lzh_debug_zstd_huf_sections); legacy: the one-wave decoder
-PATHS = ["split", "split8", "legacy"]
+# split: the four kernels (the literal kernel's sections per wave by frame count: 4 for these sizes; streams
+# of 4096 symbols and more a wave each, lzh_zstd_hufpar_kernel); split8: the same with 8 sections a wave
+# forced (lzh_debug_zstd_huf_sections); nopar: every stream one lane (lzh_debug_zstd_hufpar off); legacy:
+# the one-wave decoder
+PATHS = ["split", "split8", "nopar", "legacy"]
 
 
 def _legacy(on):
     f = L.lib().lzh_debug_zstd_legacy
+    f.restype = C.c_int
+    f.argtypes = [C.c_int]
+    assert f(1 if on else 0) == 0
+
+
+def _hufpar(on):
+    f = L.lib().lzh_debug_zstd_hufpar
     f.restype = C.c_int
     f.argtypes = [C.c_int]
     assert f(1 if on else 0) == 0
@@ -57,11 +66,13 @@ def gpu_decode(torch, packed, cs, n, chunk, path="split"):
     try:
         _legacy(path == "legacy")
         _huf_sections(8 if path == "split8" else 0)
+        _hufpar(path != "nopar")
         dc.decompress(packed=d_packed, csizes=d_cs)
         torch.cuda.synchronize()
     finally:
         _legacy(False)
         _huf_sections(0)
+        _hufpar(True)
     return dc.status[:dc.k].cpu().numpy(), dc.out[:n].cpu().numpy()
 
 
@@ -369,3 +380,16 @@ def test_many_block_frames_take_the_one_wave_decoder(torch_cuda, path):
                          path)
     assert (st == chunk).all(), st
     assert (out == data).all()
+
+
+def test_long_literal_streams_wave_parallel(torch_cuda):
+    """mixed -b128: a third of its frames are whole-block literals (4 streams of 32 K symbols), decoded a wave
+    a stream; the bytes and statuses equal the per-lane decode's and the input"""
+    torch = torch_cuda
+    n, chunk = 24 << 20, 131072
+    data = L.datagen("mixed", n, seed=12345)
+    packed, cs = L.compress_chunks(data, "zstd", chunk, 1)
+    st, out = gpu_decode(torch, packed, cs, n, chunk, "split")
+    st0, out0 = gpu_decode(torch, packed, cs, n, chunk, "nopar")
+    assert (st == expected_sizes(n, chunk)).all() and (st == st0).all()
+    assert (out == data).all() and (out0 == data).all()

@@ -1,0 +1,19 @@
+# zstd hufpar: LDS-staged stream (in-tree) against bits from memory (build/exp/hpg): tests and timing
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05_hpg; mkdir -p $O
+export TMPDIR=/tmp
+HPG=$GRAFT_REPO_ROOT/build/exp/hpg/liblzbench_hip.so
+LZH_LIB=$HPG timeout -k 10 900 python -u -m pytest tests/test_gpu_zstd.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_hpg.log 2>&1 || { tail -n 30 $O/pytest_hpg.log; exit 1; }
+tail -n 1 $O/pytest_hpg.log
+for v in base hpg; do for m in 512 1024; do
+  ( if [ $v = hpg ]; then export LZH_LIB=$HPG; fi
+    timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/${v}_$m -o run -- python3 tools/prof_kernels.py --codec zstd --level 1 --corpus mixed --chunk-kib 128 --mib $m --reps 3 --decompress > $O/${v}_$m.log 2>&1 ) || exit 1
+done; done
+python3 - $O <<'PY'
+import sqlite3, glob, sys
+for f in sorted(glob.glob(sys.argv[1] + '/*_*/*.db')):
+    c = sqlite3.connect(f)
+    rows = c.execute("select name, count(*), avg(end-start)/1e6 from kernels where name like 'lzh_zstd%' and name not like '%match%' and name not like '%entropy%' group by name order by 3 desc").fetchall()
+    print(f.split('/')[-2], [(r[0][9:], round(r[2], 3)) for r in rows], 'decode sum', round(sum(r[2] for r in rows), 3))
+PY
