@@ -2835,14 +2835,13 @@ lzh_zstd_hdr_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
 // tl-bit lookup, bits below the stream start read as zero); uniform points every kHB steps as in the
 // sequence kernel.  A stream not consumed exactly (huf_streams' verdict 1) sends its frame to the
 // one-wave decoder when the reference would use the double-symbol decoder there, else it is corrupt.
-#ifndef LZH_HUFPAR_GLOBAL
-#define LZH_HUFPAR_GLOBAL 0
-#endif
 namespace zsplit {
 constexpr int kHB = 16;                          // steps between uniform points (= bytes staged per lane)
 // streams lzh_zstd_hufpar_kernel decodes a wave each (the rest: a lane each here)
 constexpr int kParMin = 4096;                   // symbols (>= 64 bits a share)
-constexpr int kParCap = 40 * 1024;              // stream bytes staged in LDS
+// stream bytes staged in LDS (37 KiB a wave with the table: 4 waves per CU; a 4-stream section of 128 KiB of
+// literals has streams of 32 K symbols under 8 bits each, or its literals would not be Huffman-coded)
+constexpr int kParCap = 32 * 1024;
 __host__ __device__ inline bool huf_par(int on, int nsym, uint32_t sz) {
     return on && nsym >= kParMin && sz + 8 <= (uint32_t)kParCap;
 }
@@ -3057,9 +3056,7 @@ lzh_zstd_hufpar_kernel(const uint8_t* packed, uint64_t packed_readable, const ui
                        const uint32_t* njobs, int par) {
     using namespace zsplit;
     using namespace zstdd;
-#if !LZH_HUFPAR_GLOBAL
     __shared__ __attribute__((aligned(16))) uint32_t sbuf[kParCap / 4 + 128];   // dword d of the stream at d + 1
-#endif
     __shared__ __attribute__((aligned(16))) uint16_t tab[2048];
     const int lane = threadIdx.x;
     const uint32_t jid = blockIdx.x >> 2, j = blockIdx.x & 3u;
@@ -3084,28 +3081,6 @@ lzh_zstd_hufpar_kernel(const uint8_t* packed, uint64_t packed_readable, const ui
     const int nd = (X + 4) >> 2;
     const int64_t avail = (int64_t)packed_readable - A;
     const rsrc_t r = make_rsrc(packed + A, (uint32_t)max<int64_t>(0, min<int64_t>(avail, (int64_t)nd * 4)));
-#if LZH_HUFPAR_GLOBAL
-    // (the stream's bits from memory: per lane the two dwords under the reader and the next lower one in
-    // flight -- a lane reads its share downwards)
-    wait_vm();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    const uint32_t lastb = (ld_b32(r, 4 * (X >> 2)) >> (8 * (X & 3))) & 0xffu;
-    int cd = -1000;
-    uint32_t c0 = 0, c1 = 0, cn = 0;
-    auto ldd = [&](int d) -> uint32_t { return d <= 0 ? 0u : ld_b32(r, 4 * (d - 1)); };   // (d: dword d - 1)
-    auto bits = [&](int bq) -> uint32_t {
-        const int b = bq + 32, d = b >> 5;
-        if (d != cd) {
-            if (d == cd - 1) { c1 = c0; c0 = cn; }
-            else { c0 = ldd(d); c1 = ldd(d + 1); }
-            cd = d;
-            cn = ldd(d - 1);
-        }
-        uint32_t v = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(c1, c0, (uint32_t)b & 31u), 0u, (uint32_t)tl);
-        if (bq < lo) v &= lo - bq >= 32 ? 0u : (~0u << (lo - bq));
-        return v;
-    };
-#else
     {
         if (lane == 0) sbuf[0] = 0u;
         // (LDS-DMA rows of 64 dwords, one wait; past nd the range check reads zeros)
@@ -3124,7 +3099,6 @@ lzh_zstd_hufpar_kernel(const uint8_t* packed, uint64_t packed_readable, const ui
         if (bq < lo) v &= lo - bq >= 32 ? 0u : (~0u << (lo - bq));
         return v;
     };
-#endif
     const int P0 = 8 * X + (lastb ? hb32(lastb) : 0);   // (the end mark: checked non-zero by the header kernel)
     // this lane's share (P0 - lane * seg, P0 - (lane + 1) * seg], the last one down to lo
     const int nbits = P0 - lo;
@@ -3135,9 +3109,6 @@ lzh_zstd_hufpar_kernel(const uint8_t* packed, uint64_t packed_readable, const ui
     // decode the share from start: the chain's exit (the first symbol top at or below bot) and its symbols
     auto pass = [&](bool act, int start, int& ex, int& cnt, uint8_t* wdst) {
         int P = start, c = 0;
-#if LZH_HUFPAR_GLOBAL
-        cd = -1000;
-#endif
         for (int it = 0; it < guard; it++) {
             const bool go = act && P > bot;
             if (!ballot(go)) break;
@@ -3157,8 +3128,33 @@ lzh_zstd_hufpar_kernel(const uint8_t* packed, uint64_t packed_readable, const ui
         const int want = lane == 0 ? P0 : prev;
         const bool ch = want != start;
         if (!ballot(ch)) break;
-        if (ch) start = want;
-        pass(ch, start, ex, cnt, nullptr);
+        // decode from the new start (A) alongside the chain already counted from the old one (B), always the
+        // higher of the two, until they meet -- the rest is the counted chain -- or A leaves the share
+        int PA = want, cA = 0, PB = start, cB = 0;
+        bool met = false;
+        for (int it = 0; it < 2 * guard; it++) {
+            met = met || (ch && PA == PB);
+            const bool go = ch && !met && PA > bot;
+            if (!ballot(go)) break;
+            if (go) {
+                const bool a = PA > PB;
+                const uint32_t e = ((const volatile LDSA uint16_t*)tab)[bits((a ? PA : PB) - tl)];
+                const int nb = (int)(e >> 8);
+                PA -= a ? nb : 0;
+                cA += a ? 1 : 0;
+                PB -= a ? 0 : nb;
+                cB += a ? 0 : 1;
+            }
+        }
+        if (ch) {
+            if (met) {
+                cnt = cA + (cnt - cB);   // (ex: the counted chain's exit)
+            } else {
+                ex = PA;
+                cnt = cA;
+            }
+            start = want;
+        }
     }
     const int incl = groups::wave_incl_scan(cnt);
     const int total = rdlanei(incl, LZH_WAVE - 1);
