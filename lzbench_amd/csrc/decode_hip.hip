@@ -2045,6 +2045,12 @@ namespace zsplit {
 using namespace zstdd;
 
 constexpr int kFPW = 8;              // frames per sequence-decoding wave (lanes 0 .. kFPW-1)
+// the dummy stores' area after the frames' temp (512 bytes a sequence wave: a wave's lanes without a record
+// store into their own wave's slice -- one shared slice for every wave was an L2 hot spot)
+inline __host__ __device__ uint64_t zdummy_bytes(uint64_t nchunks) {
+    const uint64_t w = (nchunks + kFPW - 1) / kFPW;
+    return 512 * (w ? w : 1);
+}
 // A block's sequence tables in global memory (kSlot bytes): LL u32[512] | ML u32[512] | OF u16[256].
 // LL / ML cell: next-state base (9) | nbBits << 9 (4) | extra bits << 13 (5) | pow << 18 | lo << 19
 // (7): the baseline is lo, or 2^extra + lo for the codes whose baseline is >= 128 (LL 2^n, ML
@@ -2447,7 +2453,7 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     // (fills are global_load_lds rows from per-lane addresses: with a buffer resource the kernel's
     // scalar-register pressure moved it to vector registers and every fill became a waterfall loop)
     const int64_t readable = (int64_t)packed_readable;
-    uint64_t* const dummy = (uint64_t*)(zt + (uint64_t)nchunks * Z.stride);   // (512 bytes: see the flush)
+    uint64_t* const dummy = (uint64_t*)(zt + (uint64_t)nchunks * Z.stride) + 64ull * blockIdx.x;   // (the wave's slice)
     const int lo4 = lane * 4;
     int phase = live ? 0 : 3, res = kGo;   // 0 block start, 1 waiting for fills, 2 sequences, 3 finished
     int b = 0, op = 0, sfl = 0, rep0 = 1, rep1 = 4, rep2 = 8;   // (sfl: sequences stored)
@@ -2472,6 +2478,7 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     };
 
     uint64_t sst[6] = {0, 0, 0, 0, 0, 0}, tmark = 0;   // (LZH_ZSTD_STATS: uniform points, steps, ...)
+    const uint64_t tm0 = LZH_ZSTD_STATS ? __builtin_amdgcn_s_memtime() : 0, tr0 = LZH_ZSTD_STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the compiler's own wait tracking sees it
     for (int ival = 0;; ival++) {
         if (LZH_ZSTD_STATS) {
@@ -2697,8 +2704,11 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
             sfl += keep;
         }
     }
-    if (LZH_ZSTD_STATS && stats && lane == 0)
+    if (LZH_ZSTD_STATS && stats && lane == 0) {
         for (int k = 0; k < 6; k++) atomicAdd(&stats[k], (unsigned long long)sst[k]);
+        atomicAdd(&stats[8], (unsigned long long)(__builtin_amdgcn_s_memtime() - tm0));   // (the in-kernel clock)
+        atomicAdd(&stats[9], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tr0));
+    }
     if (LZH_ZSTD_STATS && stats && live && res == kLegacy) atomicAdd(&stats[6], 1ull);
     if (live) {
         if (res == kLegacy) {
@@ -2886,7 +2896,8 @@ __device__ __forceinline__ void zstd_huf(const uint8_t* packed, uint64_t packed_
     const rsrc_t rz = rsrc_over(zb0, (uint64_t)0xffffffffull);
     const uint64_t toff = (uint64_t)(jf - fmin) * Z.stride + Z.hufs() + (uint64_t)jtblk * kHufSlot;
     bool far_ = jlive && toff + kHufSlot > 0xffffffffull;
-    uint8_t* const dummy = zt + (uint64_t)(chunk_size ? (n_total + chunk_size - 1) / chunk_size : 0) * Z.stride;
+    const uint64_t nfr = chunk_size ? (n_total + chunk_size - 1) / chunk_size : 0;
+    uint8_t* const dummy = zt + nfr * Z.stride + (64ull * blockIdx.x) % zdummy_bytes(nfr);   // (spread like the seq kernel's)
     const int l4 = lane * 4;
     const int tl = (int)jtl;
     // this lane's stream
@@ -3379,7 +3390,7 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
     const int32_t* zsel = nullptr;
     if (zt && !g_zstd_legacy) {   // the split kernels; frames they leave go to the one-wave decoder below
         const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
-        int32_t* zst = (int32_t*)(zt + (uint64_t)nchunks * Z.stride + 512);   // (512 bytes: the dummy words)
+        int32_t* zst = (int32_t*)(zt + (uint64_t)nchunks * Z.stride + zsplit::zdummy_bytes(nchunks));   // (after the dummy words)
         zsplit::ZFrame* zfr = (zsplit::ZFrame*)((uint8_t*)zst + (((uint64_t)nchunks * 4 + 255) & ~255ull));
         uint32_t* njobs = (uint32_t*)((uint8_t*)zfr + (((uint64_t)nchunks * sizeof(zsplit::ZFrame) + 255) & ~255ull));
         zsplit::ZHuf* jobs = (zsplit::ZHuf*)((uint8_t*)njobs + 256);
@@ -3427,21 +3438,22 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         unsigned long long* sstats = nullptr;
 #if LZH_ZSTD_STATS
         static unsigned long long* d_sst = nullptr;
-        if (!d_sst) (void)hipMalloc(&d_sst, 8 * sizeof(unsigned long long));
-        (void)hipMemsetAsync(d_sst, 0, 8 * sizeof(unsigned long long), s);
+        if (!d_sst) (void)hipMalloc(&d_sst, 16 * sizeof(unsigned long long));
+        (void)hipMemsetAsync(d_sst, 0, 16 * sizeof(unsigned long long), s);
         sstats = d_sst;
 #endif
         hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3((nchunks + zsplit::kFPW - 1) / zsplit::kFPW), dim3(64), 0, s, packed,
                            packed_readable, offsets, chunk_size, nchunks, status, zt, zst, zfr, sstats);
 #if LZH_ZSTD_STATS
         {
-            unsigned long long h[8];
+            unsigned long long h[16];
             (void)hipMemcpyAsync(h, d_sst, sizeof(h), hipMemcpyDeviceToHost, s);
             (void)hipStreamSynchronize(s);
             const double w = (double)((nchunks + zsplit::kFPW - 1) / zsplit::kFPW);
             fprintf(stderr, "zstd seq kernel per wave: intervals %.0f (with block starts %.0f), steps %.0f; clocks per "
-                            "interval: uniform point %.0f (its wait %.0f), steps %.0f; frames to the one-wave decoder %llu\n",
-                    h[2] / w, h[3] / w, h[4] / w, (double)h[0] / h[2], (double)h[5] / h[2], (double)h[1] / h[2], h[6]);
+                            "interval: uniform point %.0f (its wait %.0f), steps %.0f; frames to the one-wave decoder %llu; clock %.0f MHz\n",
+                    h[2] / w, h[3] / w, h[4] / w, (double)h[0] / h[2], (double)h[5] / h[2], (double)h[1] / h[2], h[6],
+                    100.0 * (double)h[8] / (double)(h[9] ? h[9] : 1));
         }
 #endif
         hipLaunchKernelGGL(lzh_zstd_exec_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
@@ -3473,6 +3485,6 @@ size_t lzh_zstd_decode_temp(uint64_t n, uint64_t chunk_size) {
     if (chunk_size < lzh_zstd_split_min) return 0;
     const uint64_t k = (n + chunk_size - 1) / chunk_size;
     const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
-    return k * Z.stride + 512 + ((k * 4 + 255) & ~255ull) + ((k * sizeof(zsplit::ZFrame) + 255) & ~255ull) + 256 +
+    return k * Z.stride + zsplit::zdummy_bytes(k) + ((k * 4 + 255) & ~255ull) + ((k * sizeof(zsplit::ZFrame) + 255) & ~255ull) + 256 +
            k * Z.bmax * sizeof(zsplit::ZHuf) + 256;
 }

@@ -252,6 +252,35 @@ __device__ void tab_put_pos(const Tab& T, const Bytes& in, int pos, const ZParam
     T.put(h, (uint32_t)pos + 1);
 }
 
+#ifndef LZH_ZSTDC_STATS
+#define LZH_ZSTDC_STATS 0   // match / entropy kernel phase clocks (tools/zstdc_stats.py)
+#endif
+#if LZH_ZSTDC_STATS
+__device__ unsigned long long lzh_zstdc_stats_buf[24];
+#endif
+// match-kernel phase clocks (indices 0..5: search batches, match, fills + repcodes, batches, sequences,
+// frames), accumulated in registers and added once per frame
+struct MStat {
+    uint64_t v[5] = {0, 0, 0, 0, 0}, last = 0;
+    __device__ __forceinline__ void mark(int i) {
+        if (LZH_ZSTDC_STATS) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            v[i] += t - last;
+            last = t;
+        }
+    }
+    __device__ __forceinline__ void start() { if (LZH_ZSTDC_STATS) last = __builtin_amdgcn_s_memtime(); }
+    __device__ __forceinline__ void count(int i) { if (LZH_ZSTDC_STATS) v[i]++; }
+    __device__ __forceinline__ void flush(int lane) {
+#if LZH_ZSTDC_STATS
+        if (lane == 0) {
+            for (int i = 0; i < 5; i++) atomicAdd(&lzh_zstdc_stats_buf[i], (unsigned long long)v[i]);
+            atomicAdd(&lzh_zstdc_stats_buf[5], 1ull);
+        }
+#endif
+    }
+};
+
 // The parse of one block [bs, be) of a frame (positions relative to the frame start; table
 // entries hold position + 1, 0 = empty).  Mirrors zstd_fast.c:92-315.
 // dst[d0, d0+len) = src[s0, s0+len) for one wave: runs of up to 256 bytes load everything first
@@ -280,6 +309,9 @@ __device__ __forceinline__ void lit_copy(const Bytes& src, int s0, const Bytes& 
     if (tl) dst.st8(d0 + t0 + lane, tb);
 }
 
+#ifndef LZH_ZSTD_PREF
+#define LZH_ZSTD_PREF 1   // the first batch's loads issued with the previous sequence's table fills
+#endif
 #ifndef LZH_ZSTD_FWD
 #define LZH_ZSTD_FWD 16   // lanes of the forward compare in the match's round trip (4 bytes each; longer: count_fwd)
 #endif
@@ -304,39 +336,71 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
     }
     const int j = lane >> 1, half = lane & 1;
     const uint64_t below = (1ull << lane) - 1ull;
+    MStat ms;
+    ms.start();
+    // probe schedule of a batch from (A, D, s, nx): pair j of lane (A_j, D_j), and the state after 32 pairs
+    struct Sched { int Aj, Dj, A32, D32, s32, n32; };
+    auto sched = [&](int A, int D, int s, int nx) -> Sched {
+        Sched S;
+        if (D == 2 && s == 2 && A + 62 < nx) {
+            S.Aj = A + 2 * j;
+            S.Dj = 2;
+            S.A32 = A + 60; S.D32 = 2; S.s32 = 2; S.n32 = nx;
+            pair_step(S.A32, S.D32, S.s32, S.n32);
+            pair_step(S.A32, S.D32, S.s32, S.n32);
+        } else {
+            int a = A, d = D, ss = s, nn = nx;
+            for (int i = 0; i < j; i++) pair_step(a, d, ss, nn);
+            S.Aj = a;
+            S.Dj = d;
+            pair_step(a, d, ss, nn);
+            S.A32 = rdlanei(a, 63); S.D32 = rdlanei(d, 63); S.s32 = rdlanei(ss, 63); S.n32 = rdlanei(nn, 63);
+        }
+        return S;
+    };
+    // a batch's P-side and rep-side loads (branch-free: clamped positions)
+    struct PLoad { uint64_t w8; uint32_t rv, rm; };
+    auto pload = [&](const Sched& S, int A) -> PLoad {
+        const bool valid = j == 0 || S.Aj + 1 + S.Dj < ilimit;
+        const bool rok = valid && !half && r1 > 0;
+        PLoad L;
+        L.w8 = ld64(in, valid ? S.Aj + half : A);
+        L.rv = in.w32(rok ? S.Aj + S.Dj : A);
+        L.rm = in.w32(rok ? S.Aj + S.Dj - (int)r1 : A);
+        return L;
+    };
+    // the first batch after a sequence is scheduled and loaded with that sequence's table fills (one
+    // round trip for both); a repcode sequence there moves the start and drops it
+    bool pre = false;
+    Sched S0{};
+    PLoad L0{};
     for (;;) {
         if (ip + (int)P.step + 1 >= ilimit) break;
         int A = ip, D = (int)P.step, s = (int)P.step, nx = ip + 128;
         int kind = 0, ev = 0, ecand = 0;
         int eA = 0, eD = 0;
         bool ended = false;
+        Sched S;
+        PLoad Ld;
+        if (LZH_ZSTD_PREF && pre) {
+            S = S0;
+            Ld = L0;
+        } else {
+            S = sched(A, D, s, nx);
+            Ld = pload(S, A);
+        }
         for (;;) {
             ZMK(0);
-            // ---- probe schedule of the batch: pair j of lane (A_j, D_j), and the state after 32 pairs
-            int Aj, Dj;
-            int A32, D32, s32, n32;
-            if (D == 2 && s == 2 && A + 62 < nx) {
-                Aj = A + 2 * j;
-                Dj = 2;
-                A32 = A + 60; D32 = 2; s32 = 2; n32 = nx;
-                pair_step(A32, D32, s32, n32);
-                pair_step(A32, D32, s32, n32);
-            } else {
-                int a = A, d = D, ss = s, nn = nx;
-                for (int i = 0; i < j; i++) pair_step(a, d, ss, nn);
-                Aj = a;
-                Dj = d;
-                pair_step(a, d, ss, nn);
-                A32 = rdlanei(a, 63); D32 = rdlanei(d, 63); s32 = rdlanei(ss, 63); n32 = rdlanei(nn, 63);
-            }
+            ms.count(3);
+            const int Aj = S.Aj, Dj = S.Dj, A32 = S.A32, D32 = S.D32, s32 = S.s32, n32 = S.n32;
             const bool valid = j == 0 || Aj + 1 + Dj < ilimit;
             const uint64_t vmask = ballot(valid);
             const int q = Aj + half;
             ZMK(1);
             // ---- P side, rep side
             const bool rok = valid && !half && r1 > 0;
-            const uint64_t w8 = ld64(in, valid ? q : A);                  // (branch-free: clamped positions)
-            const uint32_t rv = in.w32(rok ? Aj + Dj : A), rm = in.w32(rok ? Aj + Dj - (int)r1 : A);
+            const uint64_t w8 = Ld.w8;
+            const uint32_t rv = Ld.rv, rm = Ld.rm;
             const uint32_t h = zh<kMls>(w8, P.hlog, P.mls);
             ZMK(2);
             // ---- table read, claim, read back
@@ -405,9 +469,13 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             }
             if (vmask != ~0ull || A32 + 1 + D32 >= ilimit) { ended = true; break; }
             A = A32; D = D32; s = s32; nx = n32;
+            S = sched(A, D, s, nx);
+            Ld = pload(S, A);
         }
+        ms.mark(0);
         if (ended) break;
         ZMK(5);
+        ms.count(4);
         // ---- the match.  m0 / p0: its start and source before the backward extension; the bytes
         // of the backward and forward compares and the literal run [anchor, m0) are loaded in one
         // round trip (the forward count from m0 + 4 does not depend on the backward extension; the
@@ -460,6 +528,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             else fw = fmax <= kF ? max(fmax, 0) : kF + count_fwd(in, m0 + 4 + kF, p0 + 4 + kF, fmax - kF, lane);
         }
         ZMK(6);
+        ms.mark(1);
         const int mstart = m0 - bk;
         const int len = 4 + bk + fw;
         O.nl += mstart - anchor;
@@ -469,6 +538,11 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
         {   // table fills (zstd_fast.c:216-231) and the immediate repcode check: loads in one round trip
             const uint64_t h1 = ld64(in, ip1), h2 = ld64(in, cur0 + 2), h3 = ld64(in, ip - 2);
             const uint32_t c0 = in.w32(ip), c1 = in.w32(ip - (int)r2);
+            if (LZH_ZSTD_PREF) {   // (unconditional: past ilimit the loop ends and they go unused)
+                S0 = sched(ip, (int)P.step, (int)P.step, ip + 128);
+                L0 = pload(S0, ip);
+                pre = true;
+            }
             if (lane == 0) {
                 if (ip1 < ip) T.put(zh<kMls>(h1, P.hlog, P.mls), (uint32_t)ip1 + 1);
                 if (ip <= ilimit) {
@@ -479,6 +553,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             T.fence();
             bool more = ip <= ilimit && r2 > 0 && c0 == c1;
             while (more) {
+                pre = false;
                 const int rl = 4 + count_fwd(in, ip + 4, ip + 4 - (int)r2, be - (ip + 4), lane);
                 const uint32_t t = r2; r2 = r1; r1 = t;
                 if (lane == 0) tab_put_pos<kMls>(T, in, ip, P);
@@ -489,7 +564,9 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 more = ip <= ilimit && r2 > 0 && in.w32(ip) == in.w32(ip - (int)r2);
             }
         }
+        ms.mark(2);
     }
+    ms.flush(lane);
     rep[0] = r1 ? r1 : saved;
     rep[1] = r2 ? r2 : saved;
     copy_span(in, anchor, O.lits, O.nl, be - anchor, lane, LZH_WAVE);   // last literals
@@ -500,11 +577,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
 #define LZH_ZSTD_TAB17 1   // 17-bit hash-table entries (LdsTab17) for chunks <= 128 KiB
 #endif
 
-#ifndef LZH_ZSTDC_STATS
-#define LZH_ZSTDC_STATS 0   // entropy-kernel phase clocks (tools/zstdc_stats.py)
-#endif
 #if LZH_ZSTDC_STATS
-__device__ unsigned long long lzh_zstdc_stats_buf[24];
 // entropy-kernel phase clocks (indices 16..23): lane 0 adds the clocks since its previous mark
 #define ZEM(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); if (threadIdx.x == 0) atomicAdd(&lzh_zstdc_stats_buf[16 + (i)], (unsigned long long)(t_ - ze_last)); ze_last = t_; } while (0)
 #define ZEM_DECL uint64_t ze_last = __builtin_amdgcn_s_memtime()

@@ -1,7 +1,7 @@
 # zstd decode: long Huffman streams a wave each (lzh_zstd_hufpar_kernel): zstd GPU tests, then decode timing
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r05_hufpar; mkdir -p $O
+O=${O:-gpurun_out/r05_hufpar}; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests/test_gpu_zstd.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -n 40 $O/pytest.log; exit 1; }
 tail -n 2 $O/pytest.log

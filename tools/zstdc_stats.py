@@ -26,4 +26,8 @@ v = list(buf)
 blocks = max(n // chunk, 1)
 ze = {16: "lit_histo", 17: "huf_tree", 18: "huf_streams", 19: "seq_histo", 20: "fse_tables", 21: "seq_chains", 22: "seq_packing"}
 zt = sum(v[i] for i in ze) or 1
+fr = max(v[5], 1)
+print(corpus, chunk >> 10, "KiB: match kernel per frame: clocks search %.0f match %.0f fills %.0f; batches %.0f, "
+      "sequences %.0f; clocks per batch %.0f, per sequence (match + fills) %.0f" % (
+          v[0] / fr, v[1] / fr, v[2] / fr, v[3] / fr, v[4] / fr, v[0] / max(v[3], 1), (v[1] + v[2]) / max(v[4], 1)))
 print(corpus, chunk >> 10, "KiB:", "entropy clocks/block %.0f:" % (zt / blocks), {k: "%.1f%%" % (100 * v[i] / zt) for i, k in ze.items()})
