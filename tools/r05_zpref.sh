@@ -6,7 +6,7 @@ O=${O:-gpurun_out/r05_zpref}; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_zstd_compress.py tests/test_zstd_golden.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -n 40 $O/pytest.log; exit 1; }
 tail -n 2 $O/pytest.log
-timeout -k 10 600 bash tools/zstdc_ab.sh base nopref > $O/ab.log 2>&1 || { cat $O/ab.log; exit 1; }
+timeout -k 10 600 bash tools/zstdc_ab.sh base ${AB:-nopref} > $O/ab.log 2>&1 || { cat $O/ab.log; exit 1; }
 cat $O/ab.log
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 tools/prof_kernels.py --codec zstd --level 1 --corpus mixed --chunk-kib 128 --mib 512 --reps 3 > $O/prof.log 2>&1 || exit 1
 python3 - $O <<'PY'
