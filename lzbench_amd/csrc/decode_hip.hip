@@ -2072,7 +2072,10 @@ struct ZBlk {                        // a block of the frame (header kernel)
     uint32_t tll, tof, tml;          // the blocks (of this frame) whose table slots hold LL / OF / ML
     uint32_t pad;
 };
-struct ZFrame { int32_t nblk, n, ccrc, pad; };   // blocks, content size, checksum position (-1: none)
+// blocks, content size, checksum position (-1: none); sv: the sequence kernel's verdict (kGo, kLegacy or
+// an error), applied by the execution kernel -- the sequence kernel runs beside the literal kernels, which
+// write zst / status themselves, and their verdict comes first
+struct ZFrame { int32_t nblk, n, ccrc, sv; };
 struct ZExe { uint32_t op0, seq0; };             // a block's output position and first sequence
 // a Huffman-coded literal section (header kernel -> literal kernel): its frame, the block whose
 // table slot holds its table, the table log, whether the reference would decode it with the
@@ -2428,7 +2431,7 @@ __device__ __forceinline__ int vsel(bool c, int a, int b) {
 // branches but the skip and the block's end.
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t chunk_size,
-                    uint32_t nchunks, int32_t* status, uint8_t* zt, int32_t* zst, const zsplit::ZFrame* zfr,
+                    uint32_t nchunks, int32_t* status, uint8_t* zt, const int32_t* zst, zsplit::ZFrame* zfr,
                     unsigned long long* stats) {
     using namespace zsplit;
     using namespace zstdd;
@@ -2710,14 +2713,7 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
         atomicAdd(&stats[9], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tr0));
     }
     if (LZH_ZSTD_STATS && stats && live && res == kLegacy) atomicAdd(&stats[6], 1ull);
-    if (live) {
-        if (res == kLegacy) {
-            zst[f] = kLegacy;
-        } else if (res != kGo) {
-            status[f] = res;
-            zst[f] = kDone;
-        }
-    }
+    if (live) zfr[f].sv = res;   // (kGo, kLegacy or an error: lzh_zstd_exec_kernel applies it)
 }
 
 namespace zsplit {
@@ -3199,12 +3195,24 @@ lzh_zstd_huf8_kernel(const uint8_t* packed, uint64_t packed_readable, const uint
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_exec_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, const uint32_t* csizes,
                      uint64_t n_total, uint64_t chunk_size, uint8_t* out, int32_t* status, const uint8_t* zt,
-                     const int32_t* zst, const zsplit::ZFrame* zfr) {
+                     int32_t* zst, const zsplit::ZFrame* zfr) {
     __shared__ __attribute__((aligned(16))) uint8_t win[zstdd::kZW + 3 * LZH_WAVE];
     const int lane = threadIdx.x;
     const uint64_t chunk = blockIdx.x;
     const uint64_t ooff = chunk * chunk_size;
-    if (ooff >= n_total || zst[chunk] != zsplit::kGo) return;
+    if (ooff >= n_total || zst[chunk] != zsplit::kGo) return;   // (the header / literal kernels' verdict first)
+    const int sv = zfr[chunk].sv;                                // then the sequence kernel's
+    if (sv != zsplit::kGo) {
+        if (lane == 0) {
+            if (sv == zsplit::kLegacy) {
+                zst[chunk] = zsplit::kLegacy;
+            } else {
+                status[chunk] = sv;
+                zst[chunk] = zsplit::kDone;
+            }
+        }
+        return;
+    }
     const int part = (int)min(chunk_size, n_total - ooff);
     const uint64_t ioff = offsets[chunk];
     const int cs = (int)csizes[chunk];
@@ -3259,6 +3267,8 @@ lzh_zstd_decompress_kernel(const uint8_t* packed, uint64_t packed_readable, cons
 }
 
 #include "launch.h"
+
+#include <mutex>
 // Test hook: force the LZ4 / snappy decoder's output window (4096, 8192 or 16384; 0 = by chunk count)
 // so that the parity tests run every window kernel on the same streams.
 static int g_force_window = 0;
@@ -3270,6 +3280,35 @@ extern "C" int lzh_debug_zstd_legacy(int on) {
 }
 // Test hook: force the zstd literal kernel's sections per wave (4 or 8; 0 = by frame count)
 // Test hook: long Huffman streams one per wave (lzh_zstd_hufpar_kernel) on / off
+// the sequence kernel on a per-device side stream beside the literal kernels (0: all on the caller's stream)
+static int g_zstd_side = 1;
+extern "C" int lzh_debug_zstd_side(int on) {
+    g_zstd_side = on ? 1 : 0;
+    return 0;
+}
+static hipStream_t g_side_stream[64];
+static std::mutex g_side_mu;
+// (events per thread: a call's fork / join records and waits are enqueued by the calling thread in order)
+static thread_local hipEvent_t t_side_ev[64][2];
+static bool side_for(int dev, hipStream_t& ss, hipEvent_t& fork, hipEvent_t& join) {
+    if (dev < 0 || dev >= 64) return false;
+    {
+        std::lock_guard<std::mutex> g(g_side_mu);
+        if (!g_side_stream[dev]) {
+            int lo = 0, hi = 0;
+            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+            hipStream_t st = nullptr;   // (the highest priority: its waves go out before the literal kernels')
+            if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi) != hipSuccess) return false;
+            g_side_stream[dev] = st;
+        }
+    }
+    for (int i = 0; i < 2; i++)
+        if (!t_side_ev[dev][i] && hipEventCreateWithFlags(&t_side_ev[dev][i], hipEventDisableTiming) != hipSuccess) return false;
+    ss = g_side_stream[dev];
+    fork = t_side_ev[dev][0];
+    join = t_side_ev[dev][1];
+    return true;
+}
 static int g_zstd_hufpar = 1;
 extern "C" int lzh_debug_zstd_hufpar(int on) {
     g_zstd_hufpar = on ? 1 : 0;
@@ -3397,6 +3436,27 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         (void)hipMemsetAsync(njobs, 0, 4, s);
         hipLaunchKernelGGL(lzh_zstd_hdr_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
                            n_total, chunk_size, out, status, zt, zst, zfr, stats, jobs, njobs);
+        static int hcus[64];
+        int hdev = 0;
+        (void)hipGetDevice(&hdev);
+        if (hdev < 0 || hdev >= 64) hdev = 0;
+        // the sequence kernel needs the header kernel's output only (its verdict goes to zfr[].sv): it runs
+        // on a side stream beside the literal kernels, launched first -- its waves, one per SIMD at config 5's
+        // share, take their SIMDs and the literal waves fill the rest -- and the execution kernel joins both
+        hipStream_t sq = s;
+        hipEvent_t fork = nullptr, join = nullptr;
+        if (!LZH_ZSTD_STATS && g_zstd_side && side_for(hdev, sq, fork, join)) {
+            (void)hipEventRecord(fork, s);
+            (void)hipStreamWaitEvent(sq, fork, 0);
+        } else {
+            sq = s;
+            join = nullptr;
+        }
+        if (!LZH_ZSTD_STATS) {
+            hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3((nchunks + zsplit::kFPW - 1) / zsplit::kFPW), dim3(64), 0, sq,
+                               packed, packed_readable, offsets, chunk_size, nchunks, status, zt, zst, zfr, nullptr);
+            if (join) (void)hipEventRecord(join, sq);
+        }
         const uint64_t maxjobs = (uint64_t)nchunks * Z.bmax;
         unsigned long long* hstats = nullptr;
 #if LZH_ZSTD_STATS
@@ -3406,10 +3466,6 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         hstats = d_hst;
 #endif
         // (8 sections a wave once the frames -- about one Huffman job each -- fill 8 x 4 waves per CU)
-        static int hcus[64];
-        int hdev = 0;
-        (void)hipGetDevice(&hdev);
-        if (hdev < 0 || hdev >= 64) hdev = 0;
         if (!hcus[hdev] && hipDeviceGetAttribute(&hcus[hdev], hipDeviceAttributeMultiprocessorCount, hdev) != hipSuccess)
             hcus[hdev] = 0;
         const int hj = (g_zstd_huf_sections ? g_zstd_huf_sections == 8
@@ -3442,8 +3498,9 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         (void)hipMemsetAsync(d_sst, 0, 16 * sizeof(unsigned long long), s);
         sstats = d_sst;
 #endif
-        hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3((nchunks + zsplit::kFPW - 1) / zsplit::kFPW), dim3(64), 0, s, packed,
-                           packed_readable, offsets, chunk_size, nchunks, status, zt, zst, zfr, sstats);
+        if (LZH_ZSTD_STATS)
+            hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3((nchunks + zsplit::kFPW - 1) / zsplit::kFPW), dim3(64), 0, s,
+                               packed, packed_readable, offsets, chunk_size, nchunks, status, zt, zst, zfr, sstats);
 #if LZH_ZSTD_STATS
         {
             unsigned long long h[16];
@@ -3456,6 +3513,7 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
                     100.0 * (double)h[8] / (double)(h[9] ? h[9] : 1));
         }
 #endif
+        if (join) (void)hipStreamWaitEvent(s, join, 0);
         hipLaunchKernelGGL(lzh_zstd_exec_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
                            n_total, chunk_size, out, status, zt, zst, zfr);
         zsel = zst;

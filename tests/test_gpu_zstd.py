@@ -30,8 +30,9 @@ def torch_cuda():
 
 # split: the four kernels (the literal kernel's sections per wave by frame count: 4 for these sizes; streams
 # of 4096 symbols and more a wave each, lzh_zstd_hufpar_kernel); split8: the same with 8 sections a wave
-# forced (lzh_debug_zstd_huf_sections); nopar: every stream one lane (lzh_debug_zstd_hufpar off); legacy:
-# the one-wave decoder
+# forced (lzh_debug_zstd_huf_sections); nopar: every stream one lane (lzh_debug_zstd_hufpar off) and every
+# kernel on the caller's stream in order (lzh_debug_zstd_side off: by default the sequence kernel runs on a
+# side stream beside the literal kernels); legacy: the one-wave decoder
 PATHS = ["split", "split8", "nopar", "legacy"]
 
 
@@ -44,6 +45,13 @@ def _legacy(on):
 
 def _hufpar(on):
     f = L.lib().lzh_debug_zstd_hufpar
+    f.restype = C.c_int
+    f.argtypes = [C.c_int]
+    assert f(1 if on else 0) == 0
+
+
+def _side(on):
+    f = L.lib().lzh_debug_zstd_side
     f.restype = C.c_int
     f.argtypes = [C.c_int]
     assert f(1 if on else 0) == 0
@@ -67,12 +75,14 @@ def gpu_decode(torch, packed, cs, n, chunk, path="split"):
         _legacy(path == "legacy")
         _huf_sections(8 if path == "split8" else 0)
         _hufpar(path != "nopar")
+        _side(path != "nopar")
         dc.decompress(packed=d_packed, csizes=d_cs)
         torch.cuda.synchronize()
     finally:
         _legacy(False)
         _huf_sections(0)
         _hufpar(True)
+        _side(True)
     return dc.status[:dc.k].cpu().numpy(), dc.out[:n].cpu().numpy()
 
 
