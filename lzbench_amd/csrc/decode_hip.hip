@@ -2532,6 +2532,7 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 op += rs;
                 continue;
             }
+            if (sfl + nseq > smax) { res = kLegacy; phase = 3; break; }   // (the layout's record slots)
             lA = (int)(B.logs & 255u);
             oA = (int)((B.logs >> 8) & 255u);
             mA = (int)(B.logs >> 16);
@@ -2676,13 +2677,15 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 cL = *(const LDSA uint32_t*)(S + sLL * kRow + lo4);
                 cM = *(const LDSA uint32_t*)(S + kLdsML + sML * kRow + lo4);
                 cO = *(const LDSA uint16_t*)(S + kLdsOF + (sOF >> 1) * kRow + lo4 + (sOF & 1) * 2);
-                // the reference updates the states after the last sequence too and accepts an exhausted
-                // or overrun stream there (ZSTD_decompressSequences_body: reload >= completed); then the
-                // checks of ZSTD_execSequence, and the layout's limits (else the one-wave decoder decodes)
-                const int lrem = rs - lp;
-                const bool bad = (P < lo) | (lastq & (P - lo > ns)) | (ll > lrem) | ((uint32_t)off > (uint32_t)(op + ll)) |
-                                 (op + ll + ml > n - (lrem - ll));
-                const bool lim17 = ((ll | ml) >= (1 << kLenBits)) | (sfl >= smax);
+                // the checks of ZSTD_execSequence and the layout's limit (else the one-wave decoder decodes).
+                // Per step only the offset and the record width: the stream position only falls and the
+                // literals used / the output plus the literals left only grow, so the checks on those hold
+                // at every sequence of a block exactly when they hold at its last -- that is where they are
+                // made (with the reference's end of stream: it updates the states after the last sequence too
+                // and accepts an exhausted or overrun stream there, ZSTD_decompressSequences_body: reload >=
+                // completed).  A frame that fails is not executed, so nothing reads the records before it.
+                const bool bad = (uint32_t)off > (uint32_t)(op + ll);
+                const bool lim17 = (ll | ml) >= (1 << kLenBits);
                 r0 = (uint32_t)ll | ((uint32_t)ml << kLenBits);
                 r1 = ((uint32_t)ml >> (32 - kLenBits)) | ((uint32_t)off << (2 * kLenBits - 32));
                 keep = !(bad | lim17);
@@ -2691,9 +2694,11 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 i++;
                 if (bad | lim17 | lastq) {   // an error, a limit, or the block's end (its last literals)
                     const int rem = rs - lp;
-                    if (!(bad | lim17) && rem > n - op) res = ZC;
                     if (bad | lim17) {
                         res = bad ? ZC : kLegacy;
+                        phase = 3;
+                    } else if ((P < lo) | (P - lo > ns) | (rem < 0) | (rem > n - op)) {
+                        res = ZC;
                         phase = 3;
                     } else {
                         op += rem;

@@ -1,7 +1,7 @@
 # zstd decode: the sequence kernel on a side stream -- zstd GPU tests (every path), then the A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r05_zside; mkdir -p $O
+O=${O:-gpurun_out/r05_zside}; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests/test_gpu_zstd.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -n 40 $O/pytest.log; exit 1; }
 tail -n 2 $O/pytest.log
