@@ -2459,7 +2459,8 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     uint64_t* const dummy = (uint64_t*)(zt + (uint64_t)nchunks * Z.stride) + 64ull * blockIdx.x;   // (the wave's slice)
     const int lo4 = lane * 4;
     int phase = live ? 0 : 3, res = kGo;   // 0 block start, 1 waiting for fills, 2 sequences, 3 finished
-    int b = 0, op = 0, sfl = 0, rep0 = 1, rep1 = 4, rep2 = 8;   // (sfl: sequences stored)
+    int b = 0, op = 0, rep0 = 1, rep1 = 4, rep2 = 8;
+    uint32_t sfl = 0;                                           // sequences stored
     int rs = 0, lp = 0, nseq = 0, i = 0, lA = 0, oA = 0, mA = 0;
     uint32_t sLL = 0, sOF = 0, sML = 0;
     const uint8_t *tLL = zb, *tOF = zb, *tML = zb;   // the block's table slots
@@ -2480,6 +2481,14 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
         return __builtin_amdgcn_ubfe(v, 0u, (uint32_t)w);
     };
 
+    // every step stores one record per lane at seqp[sfl] and advances sfl when the record is kept: a lane
+    // without one writes the slot its next record overwrites (or the spare slot past its last), a lane
+    // without a frame its own word of the wave's dummy slice (its sfl stays 0)
+    uint64_t* const seqp = live ? seqs : dummy + lane;
+    // (the lane's column of the bit ring, opaque to the compiler: it would split the ring's offset back out
+    // and add it per address, the ds_read2 offset field being too small for it)
+    const LDSA uint8_t* rb = S + kLdsRing + lo4;
+    asm volatile("" : "+v"(rb));
     uint64_t sst[6] = {0, 0, 0, 0, 0, 0}, tmark = 0;   // (LZH_ZSTD_STATS: uniform points, steps, ...)
     const uint64_t tm0 = LZH_ZSTD_STATS ? __builtin_amdgcn_s_memtime() : 0, tr0 = LZH_ZSTD_STATS ? __builtin_amdgcn_s_memrealtime() : 0;
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the compiler's own wait tracking sees it
@@ -2532,7 +2541,7 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 op += rs;
                 continue;
             }
-            if (sfl + nseq > smax) { res = kLegacy; phase = 3; break; }   // (the layout's record slots)
+            if ((int)sfl + nseq > smax - 1) { res = kLegacy; phase = 3; break; }   // (the layout's record slots, one spare)
             lA = (int)(B.logs & 255u);
             oA = (int)((B.logs >> 8) & 255u);
             mA = (int)(B.logs >> 16);
@@ -2643,10 +2652,10 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 // the fields: offset extra bits, ML extra bits, LL extra bits, LL / ML / OF state bits
                 const int P1 = P - ofc, P2 = P1 - am, P3 = P2 - al, P4 = P3 - (lastq ? 0 : ns);
                 // (the eight ring loads issued together, then used: the scheduler would wait after each pair)
-                const LDSA uint8_t* a1 = S + kLdsRing + ((P1 >> 5) & 63) * kRow + lo4;
-                const LDSA uint8_t* a2 = S + kLdsRing + ((P2 >> 5) & 63) * kRow + lo4;
-                const LDSA uint8_t* a3 = S + kLdsRing + ((P3 >> 5) & 63) * kRow + lo4;
-                const LDSA uint8_t* a4 = S + kLdsRing + ((P4 >> 5) & 63) * kRow + lo4;
+                const LDSA uint8_t* a1 = rb + ((P1 >> 5) & 63) * kRow;
+                const LDSA uint8_t* a2 = rb + ((P2 >> 5) & 63) * kRow;
+                const LDSA uint8_t* a3 = rb + ((P3 >> 5) & 63) * kRow;
+                const LDSA uint8_t* a4 = rb + ((P4 >> 5) & 63) * kRow;
                 const uint32_t w1l = *(const LDSA uint32_t*)a1, w1h = *(const LDSA uint32_t*)(a1 + kRow);
                 const uint32_t w2l = *(const LDSA uint32_t*)a2, w2h = *(const LDSA uint32_t*)(a2 + kRow);
                 const uint32_t w3l = *(const LDSA uint32_t*)a3, w3h = *(const LDSA uint32_t*)(a3 + kRow);
@@ -2657,8 +2666,8 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 const uint32_t lb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w3h, w3l, (uint32_t)P3 & 31u), 0u, (uint32_t)al);
                 const uint32_t sb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w4h, w4l, (uint32_t)P4 & 31u), 0u,
                                                           (uint32_t)(lastq ? 0 : ns));
-                const int ml = (int)(eM >> 19) + (((eM >> 18) & 1u) ? (1 << am) : 0) + (int)mb;
-                const int ll = (int)(eL >> 19) + (((eL >> 18) & 1u) ? (1 << al) : 0) + (int)lb;
+                const int ml = (int)((__builtin_amdgcn_ubfe(eM, 18u, 1u) << am) + (eM >> 19) + mb);
+                const int ll = (int)((__builtin_amdgcn_ubfe(eL, 18u, 1u) << al) + (eL >> 19) + lb);
                 // repcodes (ZSTD_decodeSequence): ofc > 1 a new offset; else repcode j = ofc + ll0 + bit
                 // (selects on lane masks: the compiler would branch on them)
                 const bool big = ofc > 1;
@@ -2708,7 +2717,7 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 }
                 if (LZH_ZSTD_STATS) sst[4]++;
             }
-            *(keep ? seqs + sfl : dummy + lane) = (uint64_t)r0 | ((uint64_t)r1 << 32);
+            seqp[sfl] = (uint64_t)r0 | ((uint64_t)r1 << 32);
             sfl += keep;
         }
     }
