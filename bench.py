@@ -52,10 +52,11 @@ BASELINE_METRIC = "comp+decomp MB/s, lz4 -b64 on 1 GiB; ratio + bit-exact vs CPU
 COMPRESS_KERNEL = {"lz4": "lzh_lz4_parse_kernel", "lz4fast": "lzh_lz4_parse_kernel",
                    "snappy": "lzh_snappy_parse_kernel",
                    "zstd": "lzh_zstd_match_kernel+lzh_zstd_entropy_kernel"}
-# (zstd decodes in four kernels, and frames the split layout does not fit in a fifth: the stage)
-# (the literal kernel comes in two widths, lzh_zstd_huf_kernel / lzh_zstd_huf8_kernel, picked by frame count)
-DECOMPRESS_KERNEL = {"zstd": "lzh_zstd_hdr_kernel+lzh_zstd_huf_kernel+lzh_zstd_huf8_kernel+lzh_zstd_seq_kernel"
-                             "+lzh_zstd_exec_kernel+lzh_zstd_decompress_kernel"}
+# (zstd decodes in five kernels, and frames the split layout does not fit in a sixth: the stage)
+# (the per-lane literal kernel comes in two widths, lzh_zstd_huf_kernel / lzh_zstd_huf8_kernel, picked by frame
+# count; streams of 4096+ symbols go to lzh_zstd_hufpar_kernel; the sequence kernel runs beside them)
+DECOMPRESS_KERNEL = {"zstd": "lzh_zstd_hdr_kernel+lzh_zstd_huf_kernel+lzh_zstd_huf8_kernel+lzh_zstd_hufpar_kernel"
+                             "+lzh_zstd_seq_kernel+lzh_zstd_exec_kernel+lzh_zstd_decompress_kernel"}
 
 
 def log(*a):
