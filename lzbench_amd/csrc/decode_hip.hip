@@ -3304,7 +3304,7 @@ static hipStream_t g_side_stream[64];
 static std::mutex g_side_mu;
 // (events per thread: a call's fork / join records and waits are enqueued by the calling thread in order)
 static thread_local hipEvent_t t_side_ev[64][2];
-static bool side_for(int dev, hipStream_t& ss, hipEvent_t& fork, hipEvent_t& join) {
+bool lzh_side_stream(int dev, hipStream_t& ss, hipEvent_t& fork, hipEvent_t& join) {
     if (dev < 0 || dev >= 64) return false;
     {
         std::lock_guard<std::mutex> g(g_side_mu);
@@ -3459,7 +3459,7 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         // share, take their SIMDs and the literal waves fill the rest -- and the execution kernel joins both
         hipStream_t sq = s;
         hipEvent_t fork = nullptr, join = nullptr;
-        if (!LZH_ZSTD_STATS && g_zstd_side && side_for(hdev, sq, fork, join)) {
+        if (!LZH_ZSTD_STATS && g_zstd_side && lzh_side_stream(hdev, sq, fork, join)) {
             (void)hipEventRecord(fork, s);
             (void)hipStreamWaitEvent(sq, fork, 0);
         } else {

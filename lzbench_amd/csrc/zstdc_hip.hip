@@ -594,10 +594,10 @@ using namespace zc;
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_match_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int level,
                       int k, uint8_t* scratch, uint64_t fstride, uint64_t seq_off, uint64_t lit_off, uint64_t tab_off,
-                      uint32_t lds_arg) {
+                      uint32_t lds_arg, uint32_t f0) {
     extern __shared__ __attribute__((aligned(16))) uint32_t zlds[];
     const int lane = threadIdx.x;
-    const uint64_t f = blockIdx.x;
+    const uint64_t f = (uint64_t)blockIdx.x + f0;   // (f0: the launch's first frame)
     const uint64_t ioff = f * chunk_size;
     if (ioff >= n_total && !(n_total == 0 && f == 0)) return;
     const uint64_t nf = n_total ? min(chunk_size, n_total - ioff) : 0;
@@ -1671,11 +1671,11 @@ __device__ int encode_sequences(LDSA Lds& L, const Bytes& att, const Bytes& tmp,
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_entropy_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int level, int k,
                         uint8_t* scratch, uint64_t fstride, uint64_t seq_off, uint64_t lit_off, uint64_t att_off,
-                        uint64_t tmp_off, uint8_t* stage, uint64_t stride, uint32_t* csizes) {
+                        uint64_t tmp_off, uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t f0) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_raw[(sizeof(ze::Lds) + 3) / 4];
     LDSA ze::Lds& L = *(LDSA ze::Lds*)lds_raw;
     const int lane = threadIdx.x;
-    const uint64_t f = blockIdx.x;
+    const uint64_t f = (uint64_t)blockIdx.x + f0;
     const uint64_t ioff = f * chunk_size;
     if (ioff >= n_total && !(n_total == 0 && f == 0)) return;
     const uint64_t nf = n_total ? min(chunk_size, n_total - ioff) : 0;
@@ -1831,6 +1831,13 @@ int lzh_zstd_level_ok(int level, size_t chunk_size) {
     return 1;
 }
 
+// the split of single-block frames over the side stream (0: every launch on the caller's stream)
+static int g_zstdc_split = 1;
+extern "C" int lzh_debug_zstdc_split(int on) {
+    g_zstdc_split = on ? 1 : 0;
+    return 0;
+}
+
 hipError_t lzh_launch_zstd_compress(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                                     int level, uint8_t* stage, uint64_t stride, uint32_t* csizes, uint32_t nchunks,
                                     uint8_t* scratch, hipStream_t s) {
@@ -1850,13 +1857,39 @@ hipError_t lzh_launch_zstd_compress(const uint8_t* in, uint64_t n_total, uint64_
     const uint32_t t17 = (2u << PF.hlog) + std::max((1u << PF.hlog) / 8u, 4u);
     const uint32_t lds_tab = (4u << PF.hlog) > (uint32_t)LZH_ZSTD_LDS_MAX ? 0u
                              : (LZH_ZSTD_TAB17 && chunk_size <= 131072u) ? ((t17 + 15u) & ~15u) : (ebytes << PF.hlog);
-    for (uint32_t k = 0; k < std::max(nblocks, 1u); k++) {
-        hipLaunchKernelGGL(lzh_zstd_match_kernel, dim3(nchunks), dim3(64), lds_tab, s, in, n_total, in_readable,
+    auto match = [&](hipStream_t st, uint32_t k, uint32_t f0, uint32_t nf) {
+        hipLaunchKernelGGL(lzh_zstd_match_kernel, dim3(nf), dim3(64), lds_tab, st, in, n_total, in_readable,
                            chunk_size, level, (int)k, scratch, (uint64_t)fstride, Lo.seq_off, Lo.lit_off, Lo.tab_off,
-                           lds_tab);
-        hipLaunchKernelGGL(lzh_zstd_entropy_kernel, dim3(nchunks), dim3(64), 0, s, in, n_total, in_readable,
+                           lds_tab, f0);
+    };
+    auto entropy = [&](hipStream_t st, uint32_t k, uint32_t f0, uint32_t nf) {
+        hipLaunchKernelGGL(lzh_zstd_entropy_kernel, dim3(nf), dim3(64), 0, st, in, n_total, in_readable,
                            chunk_size, level, (int)k, scratch, (uint64_t)fstride, Lo.seq_off, Lo.lit_off, Lo.att_off,
-                           Lo.tmp_off, stage, stride, csizes);
+                           Lo.tmp_off, stage, stride, csizes, f0);
+    };
+    // Single-block frames: a frame's entropy stage needs only its own match stage, so the frames split in
+    // two.  The first half runs match + entropy on the library's high-priority side stream (its waves go
+    // out first), the second half's match on the caller's stream beside it; the first half's entropy then
+    // runs beside the second half's matching and only the second half's entropy is left at the end.
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipStream_t sq = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    if (g_zstdc_split && std::max(nblocks, 1u) == 1 && nchunks >= 2 && lzh_side_stream(dev, sq, fork, join)) {
+        const uint32_t h = nchunks / 2;
+        (void)hipEventRecord(fork, s);
+        (void)hipStreamWaitEvent(sq, fork, 0);
+        match(sq, 0, 0, h);
+        match(s, 0, h, nchunks - h);
+        entropy(sq, 0, 0, h);
+        (void)hipEventRecord(join, sq);
+        entropy(s, 0, h, nchunks - h);
+        (void)hipStreamWaitEvent(s, join, 0);
+        return hipGetLastError();
+    }
+    for (uint32_t k = 0; k < std::max(nblocks, 1u); k++) {
+        match(s, k, 0, nchunks);
+        entropy(s, k, 0, nchunks);
     }
     return hipGetLastError();
 }

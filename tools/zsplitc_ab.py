@@ -1,0 +1,34 @@
+"""tools/zsplitc_ab.py -- zstd-1 -b128 compress at config 5's shares: single-block frames split over the
+side stream (lzh_debug_zstdc_split 1, default) against every launch on the caller's stream (0); HIP-event
+time of DeviceCodec.compress (kernels + scan/pack), best of 6 alternating reps; packed bytes equal."""
+import ctypes as C, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch, lzbench_amd as L
+split = L.lib().lzh_debug_zstdc_split
+split.restype = C.c_int
+split.argtypes = [C.c_int]
+for corpus, mib in (("mixed", 512), ("mixed", 1024), ("text", 512)):
+    n = mib << 20
+    host = L.datagen(corpus, n, seed=12345)
+    d_in = torch.zeros(n + 256, dtype=torch.uint8, device="cuda")
+    d_in[:n].copy_(torch.from_numpy(host))
+    dc = L.DeviceCodec("zstd", n, 128 << 10, level=1)
+    best = {0: 1e9, 1: 1e9}
+    ref = None
+    for r in range(6):
+        for on in (1, 0):
+            split(on)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            dc.compress(d_in)
+            b.record()
+            torch.cuda.synchronize()
+            best[on] = min(best[on], a.elapsed_time(b))
+            tot = dc.packed_total()
+            got = dc.packed[:tot].cpu()
+            if ref is None:
+                ref = got
+            assert torch.equal(got, ref), (corpus, mib, on)
+    split(1)
+    print(f"{corpus} {mib} MiB compress: split {best[1]:.3f} ms, serial {best[0]:.3f} ms", flush=True)
