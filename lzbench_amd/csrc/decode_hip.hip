@@ -2047,9 +2047,9 @@ using namespace zstdd;
 constexpr int kFPW = 8;              // frames per sequence-decoding wave (lanes 0 .. kFPW-1)
 // the dummy stores' area after the frames' temp (512 bytes a sequence wave: a wave's lanes without a record
 // store into their own wave's slice -- one shared slice for every wave was an L2 hot spot)
-inline __host__ __device__ uint64_t zdummy_bytes(uint64_t nchunks) {
+inline __host__ __device__ uint64_t zdummy_bytes(uint64_t nchunks) {   // (two launches' worth: see the launcher)
     const uint64_t w = (nchunks + kFPW - 1) / kFPW;
-    return 512 * (w ? w : 1);
+    return 2 * 512 * (w ? w : 1);
 }
 // A block's sequence tables in global memory (kSlot bytes): LL u32[512] | ML u32[512] | OF u16[256].
 // LL / ML cell: next-state base (9) | nbBits << 9 (4) | extra bits << 13 (5) | pow << 18 | lo << 19
@@ -2075,7 +2075,7 @@ struct ZBlk {                        // a block of the frame (header kernel)
 // blocks, content size, checksum position (-1: none); sv: the sequence kernel's verdict (kGo, kLegacy or
 // an error), applied by the execution kernel -- the sequence kernel runs beside the literal kernels, which
 // write zst / status themselves, and their verdict comes first
-struct ZFrame { int32_t nblk, n, ccrc, sv; };
+struct ZFrame { int32_t nblk, n, ccrc, sv, nsq, pad0, pad1, pad2; };   // (nsq: the frame's sequences)
 struct ZExe { uint32_t op0, seq0; };             // a block's output position and first sequence
 // a Huffman-coded literal section (header kernel -> literal kernel): its frame, the block whose
 // table slot holds its table, the table log, whether the reference would decode it with the
@@ -2337,7 +2337,7 @@ __device__ __forceinline__ int hdr_frame_body(const Bytes& rin, const Bytes& rou
     if (ltot > n) return ZC;   // an accepted frame's output holds every literal
     ZBlk* blk = (ZBlk*)zb;
     uint8_t* cells = zb + Z.cells();
-    int lacc = n - ltot, tll = 0, tof = 0, tml = 0, thuf = 0;
+    int lacc = n - ltot, tll = 0, tof = 0, tml = 0, thuf = 0, nsq = 0;
     for (int b = 0; b < nb; b++) {
         const uint32_t bh = fbyte(fw, p, lane) | (fbyte(fw, p + 1, lane) << 8) | (fbyte(fw, p + 2, lane) << 16);
         p += 3;
@@ -2357,10 +2357,12 @@ __device__ __forceinline__ int hdr_frame_body(const Bytes& rin, const Bytes& rou
                                     jobs, njobs, frame, lane);
             if (r != 0) return r;   // (an error, or kLegacy)
             p += bsz;
+            nsq += (int)B.nseq;
         }
         if (lane == 0) blk[b] = B;
     }
     if (p + ccrc != cs) return ZC;
+    fr.nsq = nsq;
     fr.nblk = nb;
     fr.n = n;
     fr.ccrc = ccrc ? p : -1;
@@ -2432,14 +2434,21 @@ __device__ __forceinline__ int vsel(bool c, int a, int b) {
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, uint64_t chunk_size,
                     uint32_t nchunks, int32_t* status, uint8_t* zt, const int32_t* zst, zsplit::ZFrame* zfr,
-                    unsigned long long* stats) {
+                    unsigned long long* stats, const uint32_t* flist, const uint32_t* fcnt, int which) {
     using namespace zsplit;
     using namespace zstdd;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsSeq];
     LDSA uint8_t* const S = (LDSA uint8_t*)lds;
     const int lane = threadIdx.x;
-    const uint32_t f = blockIdx.x * kFPW + (uint32_t)lane;
-    const bool live = lane < kFPW && f < nchunks && zst[f] == kGo;
+    // (the chain of one wave per SIMD is the kernel's time: its instructions go first when other kernels' waves
+    // -- the literal and execution kernels beside it -- share its SIMD)
+    __builtin_amdgcn_s_setprio(3);
+    // frames: lane of wave blockIdx.x, or (which 0 / 1) entry of the planned short list (from the front) /
+    // long list (from the back) -- lzh_zstd_plan_kernel
+    const uint32_t x = blockIdx.x * kFPW + (uint32_t)lane;
+    const bool inl = lane < kFPW && (which < 0 ? x < nchunks : x < fcnt[which]);
+    const uint32_t f = !inl ? 0u : which < 0 ? x : (which == 0 ? flist[x] : flist[nchunks - 1 - x]);
+    const bool live = inl && zst[f] == kGo;
     const ZLayout Z = zlayout(chunk_size);
     uint8_t* const zb = zt + (uint64_t)(live ? f : 0) * Z.stride;
     const ZBlk* blk = (const ZBlk*)zb;
@@ -2456,7 +2465,8 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
     // (fills are global_load_lds rows from per-lane addresses: with a buffer resource the kernel's
     // scalar-register pressure moved it to vector registers and every fill became a waterfall loop)
     const int64_t readable = (int64_t)packed_readable;
-    uint64_t* const dummy = (uint64_t*)(zt + (uint64_t)nchunks * Z.stride) + 64ull * blockIdx.x;   // (the wave's slice)
+    uint64_t* const dummy = (uint64_t*)(zt + (uint64_t)nchunks * Z.stride) +
+                            64ull * (blockIdx.x + (which == 1 ? gridDim.x : 0u));   // (the wave's slice)
     const int lo4 = lane * 4;
     int phase = live ? 0 : 3, res = kGo;   // 0 block start, 1 waiting for fills, 2 sequences, 3 finished
     int b = 0, op = 0, rep0 = 1, rep1 = 4, rep2 = 8;
@@ -2837,7 +2847,7 @@ lzh_zstd_hdr_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
         return;
     }
     const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
-    zsplit::ZFrame fr{0, 0, -1, 0};
+    zsplit::ZFrame fr{0, 0, -1, 0, 0, 0, 0, 0};
     const int r = zsplit::hdr_frame(rin, rout, cs, L, part, zt + chunk * Z.stride, Z, fr, lane, stats, jobs, njobs,
                                     (uint32_t)chunk);
     if (lane == 0) {
@@ -3206,13 +3216,60 @@ lzh_zstd_huf8_kernel(const uint8_t* packed, uint64_t packed_readable, const uint
     zstd_huf<8>(packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst, jobs, njobs, stats, par);
 }
 
+// The sequence / execution plan: frames the header and literal kernels left at kGo, split by their sequence
+// count -- long (nsq > max / 2) at the back of `flist`, short at the front, each in frame order -- so that the
+// execution of the short frames runs while the long ones still decode (the sequence kernel's time is its
+// longest chains').  One workgroup of 1024 threads; fcnt = {short, long}.
+extern "C" __global__ void __launch_bounds__(1024)
+lzh_zstd_plan_kernel(const int32_t* zst, const zsplit::ZFrame* zfr, uint32_t nchunks, uint32_t* flist, uint32_t* fcnt) {
+    __shared__ uint32_t smax, wsum[2][16], base[2];
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    if (t == 0) { smax = 0; base[0] = 0; base[1] = 0; }
+    __syncthreads();
+    uint32_t m = 0;
+    for (uint32_t i = t; i < nchunks; i += 1024)
+        if (zst[i] == zsplit::kGo) m = max(m, (uint32_t)max(zfr[i].nsq, 0));
+    atomicMax(&smax, m);
+    __syncthreads();
+    const uint32_t thr = smax / 2;
+    for (uint32_t i0 = 0; i0 < nchunks; i0 += 1024) {
+        const uint32_t i = i0 + t;
+        const bool go = i < nchunks && zst[i] == zsplit::kGo;
+        const bool lng = go && (uint32_t)max(zfr[i].nsq, 0) > thr;
+        const uint64_t bs = __builtin_amdgcn_ballot_w64(go && !lng), bl = __builtin_amdgcn_ballot_w64(lng);
+        const uint64_t below = (1ull << lane) - 1ull;
+        if (lane == 0) { wsum[0][w] = (uint32_t)__builtin_popcountll(bs); wsum[1][w] = (uint32_t)__builtin_popcountll(bl); }
+        __syncthreads();
+        uint32_t ps = base[0], pl = base[1];
+        for (uint32_t k = 0; k < w; k++) { ps += wsum[0][k]; pl += wsum[1][k]; }
+        if (go && !lng) flist[ps + (uint32_t)__builtin_popcountll(bs & below)] = i;
+        if (lng) flist[nchunks - 1 - (pl + (uint32_t)__builtin_popcountll(bl & below))] = i;
+        __syncthreads();
+        if (t == 0)
+            for (uint32_t k = 0; k < 16; k++) { base[0] += wsum[0][k]; base[1] += wsum[1][k]; }
+        __syncthreads();
+    }
+    if (t == 0) {
+        // the long list rounded up to whole sequence waves with the short list's last frames, so that the two
+        // launches' frames need no more waves than one launch's (a wave more than there are SIMDs would wait
+        // for a whole chain); the ranges are disjoint or the entries already in place (see the indices)
+        uint32_t ns = base[0], nl = base[1];
+        const uint32_t m = min((uint32_t)(zsplit::kFPW - nl % zsplit::kFPW) % zsplit::kFPW, ns);
+        for (uint32_t j = 0; j < m; j++) flist[nchunks - 1 - (nl + j)] = flist[ns - 1 - j];
+        fcnt[0] = ns - m;
+        fcnt[1] = nl + m;
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(64)
 lzh_zstd_exec_kernel(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets, const uint32_t* csizes,
                      uint64_t n_total, uint64_t chunk_size, uint8_t* out, int32_t* status, const uint8_t* zt,
-                     int32_t* zst, const zsplit::ZFrame* zfr) {
+                     int32_t* zst, const zsplit::ZFrame* zfr, const uint32_t* flist, const uint32_t* fcnt, int which,
+                     uint32_t nchunks) {
     __shared__ __attribute__((aligned(16))) uint8_t win[zstdd::kZW + 3 * LZH_WAVE];
     const int lane = threadIdx.x;
-    const uint64_t chunk = blockIdx.x;
+    if (which >= 0 && blockIdx.x >= fcnt[which]) return;
+    const uint64_t chunk = which < 0 ? blockIdx.x : (which == 0 ? flist[blockIdx.x] : flist[nchunks - 1 - blockIdx.x]);
     const uint64_t ooff = chunk * chunk_size;
     if (ooff >= n_total || zst[chunk] != zsplit::kGo) return;   // (the header / literal kernels' verdict first)
     const int sv = zfr[chunk].sv;                                // then the sequence kernel's
@@ -3300,28 +3357,35 @@ extern "C" int lzh_debug_zstd_side(int on) {
     g_zstd_side = on ? 1 : 0;
     return 0;
 }
-static hipStream_t g_side_stream[64];
+static hipStream_t g_side_stream[64][2];
 static std::mutex g_side_mu;
 // (events per thread: a call's fork / join records and waits are enqueued by the calling thread in order)
-static thread_local hipEvent_t t_side_ev[64][2];
-bool lzh_side_stream(int dev, hipStream_t& ss, hipEvent_t& fork, hipEvent_t& join) {
-    if (dev < 0 || dev >= 64) return false;
+static thread_local hipEvent_t t_side_ev[64][2][2];
+bool lzh_side_stream(int dev, hipStream_t& ss, hipEvent_t& fork, hipEvent_t& join, int k) {
+    if (dev < 0 || dev >= 64 || k < 0 || k > 1) return false;
     {
         std::lock_guard<std::mutex> g(g_side_mu);
-        if (!g_side_stream[dev]) {
+        if (!g_side_stream[dev][k]) {
             int lo = 0, hi = 0;
             if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
-            hipStream_t st = nullptr;   // (the highest priority: its waves go out before the literal kernels')
+            hipStream_t st = nullptr;   // (the highest priority: their waves go out before the caller's stream's)
             if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi) != hipSuccess) return false;
-            g_side_stream[dev] = st;
+            g_side_stream[dev][k] = st;
         }
     }
     for (int i = 0; i < 2; i++)
-        if (!t_side_ev[dev][i] && hipEventCreateWithFlags(&t_side_ev[dev][i], hipEventDisableTiming) != hipSuccess) return false;
-    ss = g_side_stream[dev];
-    fork = t_side_ev[dev][0];
-    join = t_side_ev[dev][1];
+        if (!t_side_ev[dev][k][i] && hipEventCreateWithFlags(&t_side_ev[dev][k][i], hipEventDisableTiming) != hipSuccess)
+            return false;
+    ss = g_side_stream[dev][k];
+    fork = t_side_ev[dev][k][0];
+    join = t_side_ev[dev][k][1];
     return true;
+}
+// the sequence / execution plan by sequence count (lzh_zstd_plan_kernel; 0: one sequence launch)
+static int g_zstd_plan = 1;
+extern "C" int lzh_debug_zstd_plan(int on) {
+    g_zstd_plan = on ? 1 : 0;
+    return 0;
 }
 static int g_zstd_hufpar = 1;
 extern "C" int lzh_debug_zstd_hufpar(int on) {
@@ -3457,19 +3521,39 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         // the sequence kernel needs the header kernel's output only (its verdict goes to zfr[].sv): it runs
         // on a side stream beside the literal kernels, launched first -- its waves, one per SIMD at config 5's
         // share, take their SIMDs and the literal waves fill the rest -- and the execution kernel joins both
-        hipStream_t sq = s;
-        hipEvent_t fork = nullptr, join = nullptr;
-        if (!LZH_ZSTD_STATS && g_zstd_side && lzh_side_stream(hdev, sq, fork, join)) {
-            (void)hipEventRecord(fork, s);
-            (void)hipStreamWaitEvent(sq, fork, 0);
-        } else {
-            sq = s;
-            join = nullptr;
-        }
-        if (!LZH_ZSTD_STATS) {
-            hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3((nchunks + zsplit::kFPW - 1) / zsplit::kFPW), dim3(64), 0, sq,
-                               packed, packed_readable, offsets, chunk_size, nchunks, status, zt, zst, zfr, nullptr);
-            if (join) (void)hipEventRecord(join, sq);
+        // and after the plan (lzh_zstd_plan_kernel) the frames with the longest sequence chains decode on one
+        // side stream, the rest on another, so that the execution kernel runs the short ones while the long
+        // ones still decode
+        uint32_t* flist = (uint32_t*)((uint8_t*)jobs + (uint64_t)nchunks * Z.bmax * sizeof(zsplit::ZHuf) + 256);
+        uint32_t* fcnt = flist + nchunks;
+        hipStream_t sq[2] = {s, s};
+        hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
+        const bool side = !LZH_ZSTD_STATS && g_zstd_side && lzh_side_stream(hdev, sq[0], fork[0], join[0], 0) &&
+                          lzh_side_stream(hdev, sq[1], fork[1], join[1], 1);
+        const unsigned sgrid = (nchunks + zsplit::kFPW - 1) / zsplit::kFPW;
+        if (!hcus[hdev] && hipDeviceGetAttribute(&hcus[hdev], hipDeviceAttributeMultiprocessorCount, hdev) != hipSuccess)
+            hcus[hdev] = 0;
+        // (the plan only while the sequence waves leave LDS room beside them -- at most 2 of a CU's 4 -- for the
+        // literal kernels, whose end the execution of the short frames waits for; else one sequence launch)
+        const bool plan = side && g_zstd_plan && hcus[hdev] > 0 && sgrid <= 2u * (unsigned)hcus[hdev];
+        if (plan) {
+            hipLaunchKernelGGL(lzh_zstd_plan_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)zst,
+                               (const zsplit::ZFrame*)zfr, nchunks, flist, fcnt);
+            for (int k = 0; k < 2; k++) {   // long list (which 1) on side stream 0, launched first
+                (void)hipEventRecord(fork[k], s);
+                (void)hipStreamWaitEvent(sq[k], fork[k], 0);
+                hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3(sgrid), dim3(64), 0, sq[k], packed, packed_readable,
+                                   offsets, chunk_size, nchunks, status, zt, zst, zfr, nullptr, (const uint32_t*)flist,
+                                   (const uint32_t*)fcnt, 1 - k);
+                (void)hipEventRecord(join[k], sq[k]);
+            }
+        } else if (side) {
+            (void)hipEventRecord(fork[0], s);
+            (void)hipStreamWaitEvent(sq[0], fork[0], 0);
+            hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3(sgrid), dim3(64), 0, sq[0], packed, packed_readable, offsets,
+                               chunk_size, nchunks, status, zt, zst, zfr, nullptr, (const uint32_t*)nullptr,
+                               (const uint32_t*)nullptr, -1);
+            (void)hipEventRecord(join[0], sq[0]);
         }
         const uint64_t maxjobs = (uint64_t)nchunks * Z.bmax;
         unsigned long long* hstats = nullptr;
@@ -3480,8 +3564,6 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         hstats = d_hst;
 #endif
         // (8 sections a wave once the frames -- about one Huffman job each -- fill 8 x 4 waves per CU)
-        if (!hcus[hdev] && hipDeviceGetAttribute(&hcus[hdev], hipDeviceAttributeMultiprocessorCount, hdev) != hipSuccess)
-            hcus[hdev] = 0;
         const int hj = (g_zstd_huf_sections ? g_zstd_huf_sections == 8
                                             : hcus[hdev] > 0 && (uint64_t)nchunks >= 32ull * (uint64_t)hcus[hdev]) ? 8 : 4;
         hipLaunchKernelGGL(hj == 8 ? lzh_zstd_huf8_kernel : lzh_zstd_huf_kernel, dim3((unsigned)((maxjobs + hj - 1) / hj)),
@@ -3512,9 +3594,10 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         (void)hipMemsetAsync(d_sst, 0, 16 * sizeof(unsigned long long), s);
         sstats = d_sst;
 #endif
-        if (LZH_ZSTD_STATS)
-            hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3((nchunks + zsplit::kFPW - 1) / zsplit::kFPW), dim3(64), 0, s,
-                               packed, packed_readable, offsets, chunk_size, nchunks, status, zt, zst, zfr, sstats);
+        if (!side)
+            hipLaunchKernelGGL(lzh_zstd_seq_kernel, dim3(sgrid), dim3(64), 0, s, packed, packed_readable, offsets,
+                               chunk_size, nchunks, status, zt, zst, zfr, sstats, (const uint32_t*)nullptr,
+                               (const uint32_t*)nullptr, -1);
 #if LZH_ZSTD_STATS
         {
             unsigned long long h[16];
@@ -3527,9 +3610,19 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
                     100.0 * (double)h[8] / (double)(h[9] ? h[9] : 1));
         }
 #endif
-        if (join) (void)hipStreamWaitEvent(s, join, 0);
-        hipLaunchKernelGGL(lzh_zstd_exec_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets, csizes,
-                           n_total, chunk_size, out, status, zt, zst, zfr);
+        if (plan) {
+            for (int k = 1; k >= 0; k--) {   // the short list once its sequences are done, then the long one
+                (void)hipStreamWaitEvent(s, join[k], 0);
+                hipLaunchKernelGGL(lzh_zstd_exec_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets,
+                                   csizes, n_total, chunk_size, out, status, zt, zst, zfr, (const uint32_t*)flist,
+                                   (const uint32_t*)fcnt, 1 - k, nchunks);
+            }
+        } else {
+            if (side) (void)hipStreamWaitEvent(s, join[0], 0);
+            hipLaunchKernelGGL(lzh_zstd_exec_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets,
+                               csizes, n_total, chunk_size, out, status, zt, zst, zfr, (const uint32_t*)nullptr,
+                               (const uint32_t*)nullptr, -1, nchunks);
+        }
         zsel = zst;
     }
     hipLaunchKernelGGL(lzh_zstd_decompress_kernel, dim3(nchunks), dim3(64), 0, s, packed, packed_readable, offsets,
@@ -3558,5 +3651,5 @@ size_t lzh_zstd_decode_temp(uint64_t n, uint64_t chunk_size) {
     const uint64_t k = (n + chunk_size - 1) / chunk_size;
     const zsplit::ZLayout Z = zsplit::zlayout(chunk_size);
     return k * Z.stride + zsplit::zdummy_bytes(k) + ((k * 4 + 255) & ~255ull) + ((k * sizeof(zsplit::ZFrame) + 255) & ~255ull) + 256 +
-           k * Z.bmax * sizeof(zsplit::ZHuf) + 256;
+           k * Z.bmax * sizeof(zsplit::ZHuf) + 256 + ((k * 4 + 8 + 255) & ~255ull);   // (+ the plan's frame list, counts)
 }

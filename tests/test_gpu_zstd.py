@@ -32,7 +32,9 @@ def torch_cuda():
 # of 4096 symbols and more a wave each, lzh_zstd_hufpar_kernel); split8: the same with 8 sections a wave
 # forced (lzh_debug_zstd_huf_sections); nopar: every stream one lane (lzh_debug_zstd_hufpar off) and every
 # kernel on the caller's stream in order (lzh_debug_zstd_side off: by default the sequence kernel runs on a
-# side stream beside the literal kernels); legacy: the one-wave decoder
+# side stream beside the literal kernels; split and split8 differ there too: split plans the sequence kernel in
+# two launches by sequence count, lzh_zstd_plan_kernel, split8 runs one -- lzh_debug_zstd_plan); legacy: the
+# one-wave decoder
 PATHS = ["split", "split8", "nopar", "legacy"]
 
 
@@ -57,6 +59,13 @@ def _side(on):
     assert f(1 if on else 0) == 0
 
 
+def _plan(on):
+    f = L.lib().lzh_debug_zstd_plan
+    f.restype = C.c_int
+    f.argtypes = [C.c_int]
+    assert f(1 if on else 0) == 0
+
+
 def _huf_sections(hj):
     f = L.lib().lzh_debug_zstd_huf_sections
     f.restype = C.c_int
@@ -76,6 +85,7 @@ def gpu_decode(torch, packed, cs, n, chunk, path="split"):
         _huf_sections(8 if path == "split8" else 0)
         _hufpar(path != "nopar")
         _side(path != "nopar")
+        _plan(path != "split8")
         dc.decompress(packed=d_packed, csizes=d_cs)
         torch.cuda.synchronize()
     finally:
@@ -83,6 +93,7 @@ def gpu_decode(torch, packed, cs, n, chunk, path="split"):
         _huf_sections(0)
         _hufpar(True)
         _side(True)
+        _plan(True)
     return dc.status[:dc.k].cpu().numpy(), dc.out[:n].cpu().numpy()
 
 
