@@ -73,6 +73,9 @@ def test_extra_operation_is_safe(dis):
     lst = V.kernel_listing(dis, kernel)
     idx = _step_stores(lst)
     bad = list(lst)
-    a, ins = bad[idx[0] - 1]
-    bad[idx[0] - 1] = (a, "global_load_dword v0, v[0:1], off")   # one more load in the step
+    # a vector ALU instruction of the step turned into one more load (a scalar one may be the loop
+    # counter's compare, which the checker's constant tracking needs)
+    j = max(i for i in range(idx[0]) if bad[i][1].startswith("v_"))
+    a, ins = bad[j]
+    bad[j] = (a, "global_load_dword v0, v[0:1], off")
     assert V.check_listing(bad, kernel, base=lst[0][0]) == []
