@@ -658,7 +658,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         // re-test at a match end, then 64 step-1 search probes, lz4.c:955-969 / :1148-1200);
         // pins = a pending ip-2 table fill (lz4.c:1145-1146) sitting at base.  Stride batches
         // (any other schedule): one sequence per batch, the search from s with k0 probes done.
-        bool runb = kFast || acc == 1, retest = false, go = true;
+        int runb = kFast || acc == 1, retest = 0, go = 1;   // (ints: uniform SGPR phis, not lane masks)
         const int dlim = kFast ? 2 + 62 * acc : 64;      // last run-batch probe: segment origin + dlim
         int base = b0 + 1, q = b0 + 1, qlim = b0 + dlim, pins = -1;
         int so = b0;                             // segment origin (kFast pattern phase)
@@ -671,9 +671,13 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             PAT = 3ull | (PER << 2);
         }
 
-        for (int guard = 0; go && !(kLinked && aborted) && guard < 4 * n + 64; guard++) {
-            // (the loop-carried parse state is wave-uniform: readfirstlane keeps it in SGPRs)
-            runb = unii(runb) != 0; retest = unii(retest) != 0;
+        for (int guard = 0;; guard++) {
+            // (the loop-carried parse state is wave-uniform: readfirstlane keeps it in SGPRs, and the
+            // exit test on uniform values is a scalar branch, not an exec-mask loop exit)
+            go = unii(go);
+            if (kLinked) aborted = unii(aborted) != 0;
+            if (!go || (kLinked && aborted) || guard >= 4 * n + 64) break;
+            runb = unii(runb); retest = unii(retest);
             base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
             op = unii(op); anchor = unii(anchor); rc_tot = unii(rc_tot); nrec = unii(nrec);
             R.fill = unii(R.fill); R.ready = unii(R.ready); O.flushed = unii(O.flushed);
@@ -692,9 +696,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 }
                 const int d = q - so;
                 s = so + 1;
-                retest = d <= 0;
+                retest = d <= 0 ? 1 : 0;
                 k0 = d <= 1 ? 0 : 1 + (d - 2 + acc - 1) / acc;
-                runb = false;
+                runb = 0;
             }
             LZ_CLK(9);                                                 // (loop overhead / uncharged)
 
@@ -964,7 +968,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     wave_lds_fence();
                 };
                 if (endp) {
-                    go = false;
+                    go = 0;
                     if (Mm) anchor = base + eL;
                     if (kLinked) {   // the next block starts from this table: no ip-2 fill after a match
                         // ending past mflimit (lz4.c:1142-1146)
@@ -1005,10 +1009,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     }
                     wave_lds_fence();
                     if (!Mm && hi0 == qlim - base) {                   // 64 probes done: stride batches
-                        runb = false;
+                        runb = 0;
                         s = so + 1;
                         k0 = LZH_WAVE;
-                        retest = false;
+                        retest = 0;
                     } else {
                         base = pins >= 0 ? pins : q;
                     }
@@ -1054,9 +1058,12 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 }
             }
             wave_lds_fence();
+            // (uniform: a phi of `found` the compiler takes as divergent turns the whole batch loop's
+            // state into VGPR copies read back by readfirstlane at every iteration)
+            found = unii(found) != 0; fh = unii(fh);
             if (!found) {
-                if (tmask) go = false;                                 // ran past mflimit
-                else if (retest) { retest = false; k0 = LZH_WAVE - 1; }
+                if (tmask) go = 0;                                 // ran past mflimit
+                else if (retest) { retest = 0; k0 = LZH_WAVE - 1; }
                 else k0 += LZH_WAVE;
             } else {
                 LZ_STAT(3, 1);
@@ -1080,9 +1087,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 const int ip = P + kMinMatch + cnt;
                 anchor = ip;
                 if (ip >= mfe) {
-                    go = false;
+                    go = 0;
                 } else if (acc == 1 || kFast) {                        // back to run batches
-                    runb = true;
+                    runb = 1;
                     pins = ip - 2;
                     base = ip - 2;
                     q = ip;
@@ -1095,7 +1102,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     const uint32_t hm2 = hash_of<kSmall>(w, bb);
                     if (lane == 0) T.put(hm2, (uint32_t)(ip - 2));
                     wave_lds_fence();
-                    retest = true;
+                    retest = 1;
                     s = ip + 1;
                     k0 = 0;
                 }

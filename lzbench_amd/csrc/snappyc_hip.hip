@@ -725,6 +725,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     exact = true;
                 }
             }
+            exact = unii(exact) != 0;
             if (!exact) {
                 if (valid && lane > L && back == (uint32_t)p) T.put(h, old);
                 if (losers & upto) {
@@ -771,6 +772,9 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     if (!later) T.put(h, (uint32_t)p);
                 }
             }
+            // (uniform: a phi of `found` / `exact` the compiler takes as divergent turns the batch loop's
+            // state into VGPR copies read back by readfirstlane at every iteration)
+            found = unii(found) != 0; fh = unii(fh);
             if (!found) {
                 wave_lds_fence();
                 if (tmask) break;                         // search exhausted: remainder from next_emit
