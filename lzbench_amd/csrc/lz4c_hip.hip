@@ -18,9 +18,6 @@
 // Long catch-ups / matches / literal runs beyond the windows take lane-parallel slow paths.
 #include "common.h"
 
-#ifndef LZH_LZ4_NORING
-#define LZH_LZ4_NORING 0
-#endif
 namespace lz4v3 {
 
 // optional per-kernel event counters (debug builds of the launch only; nullptr in production)
@@ -624,7 +621,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
 #pragma unroll
         for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
     }
-    constexpr bool kRingOn = !(kRec && LZH_LZ4_NORING);   // (experiment flag: the parse kernel without its ring)
+    constexpr bool kRingOn = true;   // (without the ring -- more waves, P sides from memory -- 6 % slower, profiles/r05_lnr)
     Ring R{ringw, in.sh, 0, 0, kRingOn, kRec};   // (the parse kernel's ring carries a 32-byte mirror)
     if (kLinked) R.fill = max(((b0 + in.sh) & ~255) - 256, 0);   // (a block's ring starts just before it)
     OutRing O{outb, out.sh, 0};
@@ -1210,11 +1207,7 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                      uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint64_t frame_size, uint32_t bpf) {
-#if LZH_LZ4_NORING   // (experiment: the table alone, 16 KiB -> 10 waves per CU; every P-side read from memory)
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096];
-#else
     __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + 8];   // table | ring + mirror
-#endif
     const uint64_t chunk = blockIdx.x;
     uint64_t off;
     int n;

@@ -22,9 +22,6 @@
 //   * deferred, branch-free emission of literal + copy (EmitLiteral / EmitCopy, :342-443).
 #include "common.h"
 
-#ifndef LZH_SN_NORING
-#define LZH_SN_NORING 0
-#endif
 namespace snv2 {
 
 #define SN_STAT(i, v) do { if (stats && lane == 0) atomicAdd(&stats[i], (unsigned long long)(v)); } while (0)
@@ -370,7 +367,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
         const int nvec = (int)(tsize * 2 / 16);
         for (int i = lane; i < nvec; i += LZH_WAVE) lds_zero16(t4 + 4 * i);
     }
-    Ring R{ringw, in.sh, 0, 0, !(kRec && LZH_SN_NORING), kRec};   // (parse kernel: mirrored ring)
+    Ring R{ringw, in.sh, 0, 0, true, kRec};   // (parse kernel: mirrored ring; without it 4-6 % slower, profiles/r05_snr)
     const int endX = fn + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
     wait_vm();
@@ -926,11 +923,7 @@ constexpr int kFragRecs = 16384 + 32;
 extern "C" __global__ void __launch_bounds__(64)
 lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                         uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint32_t frags) {
-#if LZH_SN_NORING   // (experiment: the table alone, 32 KiB -> 5 waves per CU; every P-side read from memory)
-    __shared__ __attribute__((aligned(16))) uint32_t lds[1 << 13];
-#else
     __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + 256 + 8];   // table | ring + mirror
-#endif
     const uint64_t chunk = blockIdx.x / frags;
     const uint32_t f = blockIdx.x - (uint32_t)chunk * frags;
     const uint64_t off = chunk * chunk_size;
