@@ -422,8 +422,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 // the winner's offset from the batch's first position)
                 const int A0 = rdlanei(Aj, 0);
                 const int span = rdlanei(Aj, 62) + 2 - A0;
-                int nbits = 1;
-                while ((1 << nbits) < span) nbits++;
+                const int nbits = span > 2 ? 32 - __builtin_clz((uint32_t)span - 1u) : 1;   // ceil(log2 span), >= 1
                 const uint32_t wr = (back - 1u - (uint32_t)A0) & Tab::kBackMask;
                 uint64_t eq = vmask;
                 for (int b = 0; b < nbits; b++) {
