@@ -425,7 +425,15 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 const int nbits = span > 2 ? 32 - __builtin_clz((uint32_t)span - 1u) : 1;   // ceil(log2 span), >= 1
                 const uint32_t wr = (back - 1u - (uint32_t)A0) & Tab::kBackMask;
                 uint64_t eq = vmask;
-                for (int b = 0; b < nbits; b++) {
+                // (the first 6 bits unrolled, without the loop's scalar chain: bits at or past nbits are 0
+                // in every valid lane's offset, so those rounds leave eq as it is)
+#pragma unroll
+                for (int b = 0; b < 6; b++) {
+                    const bool wb = (wr >> b) & 1u;
+                    const uint64_t bm = ballot(valid && wb);
+                    eq &= wb ? bm : ~bm;
+                }
+                for (int b = 6; b < nbits; b++) {
                     const bool wb = (wr >> b) & 1u;
                     const uint64_t bm = ballot(valid && wb);
                     eq &= wb ? bm : ~bm;
