@@ -442,13 +442,19 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 const uint64_t eb = grp & below;
                 prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
             }
-            const int src = prev < 0 ? lane : prev;
-            const int qprev = lane_gather((uint32_t)q, src);
-            const uint32_t wprev = lane_gather((uint32_t)w8, src);
-            const uint32_t cand = prev >= 0 ? (uint32_t)qprev + 1 : old;
+            uint32_t cand = old;
+            bool hit = ook && cwo == (uint32_t)w8;
+            if (losers) {   // (a batch without a collision needs no gathers: most batches)
+                const int src = prev < 0 ? lane : prev;
+                const int qprev = lane_gather((uint32_t)q, src);
+                const uint32_t wprev = lane_gather((uint32_t)w8, src);
+                if (prev >= 0) {
+                    cand = (uint32_t)qprev + 1;
+                    hit = valid && wprev == (uint32_t)w8;
+                }
+            }
             ZMK(3);
             // ---- candidate compare (an in-batch candidate is past the prefix start)
-            const bool hit = prev >= 0 ? (valid && wprev == (uint32_t)w8) : (ook && cwo == (uint32_t)w8);
             const bool rhit = rok && rv == rm;
             const uint64_t R = ballot(rhit), H = ballot(hit), E = R | H;
             ZMK(4);
