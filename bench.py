@@ -135,11 +135,30 @@ def cpu_baseline(sample: np.ndarray, codec: str, chunk: int, level: int, iters: 
     }
 
 
+_HASHES = None
+
+
+def _loaded_hashes():
+    """kernel code hashes of the library this process loads (lzbench_amd.kernel_hash)"""
+    global _HASHES
+    if _HASHES is None:
+        from lzbench_amd import kernel_hash
+        try:
+            _HASHES = kernel_hash.kernel_hashes(L.LIB_PATH)
+        except (OSError, ValueError):
+            _HASHES = {}
+    return _HASHES
+
+
 def traffic_for(kernel, workload):
-    """HBM-side bytes per dispatch of `kernel` from the committed PMC profiles (profiles/traffic*.json,
+    """(HBM-side bytes per dispatch of `kernel`, None) from the committed PMC profiles (profiles/traffic*.json,
     written by tools/pmc_traffic.sh: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes on the
-    same workload; one file per workload), or None when no profile covers this kernel/workload."""
+    same workload; one file per workload), or (None, reason) when no profile covers this kernel/workload or the
+    profile was taken of other machine code than the loaded library's (each profile records the code hash of
+    every kernel it measured, lzbench_amd/kernel_hash.py)."""
     import glob
+    have = _loaded_hashes()
+    reason = f"no profiles/traffic*.json for {kernel} on {workload}"
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic*.json"))):
         try:
             with open(path) as f:
@@ -148,13 +167,19 @@ def traffic_for(kernel, workload):
                 continue
             # a stage of several kernels ("a+b"): the sum over the kernels the profile holds (a kernel
             # no dispatch of which ran in the profiled pass has no entry and contributes nothing)
-            parts = [t["kernels"].get(k) for k in kernel.split("+")]
-            if all(p is None for p in parts):
-                return None
-            return int(sum(p["traffic_bytes_per_dispatch"] for p in parts if p is not None))
+            parts = {k: t["kernels"].get(k) for k in kernel.split("+")}
+            if all(p is None for p in parts.values()):
+                continue
+            stale = [k for k, p in parts.items()
+                     if p is not None and (p.get("kernel_hash") is None or p["kernel_hash"] != have.get(k))]
+            if stale:
+                reason = (f"{os.path.relpath(path, ROOT)} measured other code of {', '.join(stale)} "
+                          f"(profile hash {parts[stale[0]].get('kernel_hash')}, loaded {have.get(stale[0])})")
+                continue
+            return int(sum(p["traffic_bytes_per_dispatch"] for p in parts.values() if p is not None)), None
         except (OSError, KeyError, ValueError):
             continue
-    return None
+    return None, reason
 
 
 def fullsize_digest(corpus, codec, chunk, level, n, seed, offset=0):
@@ -419,6 +444,8 @@ def main():
             dname = "+".join(dict.fromkeys(names))
         else:
             dname = wkernel(k_all)
+    tr_c, why_c = traffic_for(kname, wkey)
+    tr_d, why_d = traffic_for(dname, wkey)
     res = {
         "metric": metric_for(args.codec, args.chunk_kib, n, args.corpus, args.level),
         "value": round(value, 2),
@@ -448,8 +475,10 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic_for(kname, wkey),
-            "traffic_source": "profiles/traffic*.json (rocprofv3 FETCH_SIZE + WRITE_SIZE, separate passes, per launch)",
+            "traffic": tr_c,
+            "traffic_source": "profiles/traffic*.json (rocprofv3 FETCH_SIZE + WRITE_SIZE, separate passes, per launch; "
+                              "only for the machine code the profile measured)",
+            **({"traffic_null_reason": why_c} if tr_c is None else {}),
             "kernel": kname,
             "kernel_ms": round(k_ms, 3),
             "algorithmic_bytes_per_launch": int(algo_bytes),
@@ -469,7 +498,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(dec_achieved / HBM_PEAK_GBS, 5),
-            "traffic": traffic_for(dname, wkey),
+            "traffic": tr_d,
+            **({"traffic_null_reason": why_d} if tr_d is None else {}),
             "kernel": dname,
             "kernel_ms": round(d_ms, 3),
         },

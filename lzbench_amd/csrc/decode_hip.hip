@@ -2704,7 +2704,11 @@ lzh_zstd_seq_kernel(const uint8_t* packed, uint64_t packed_readable, const uint6
                 // and accepts an exhausted or overrun stream there, ZSTD_decompressSequences_body: reload >=
                 // completed).  A frame that fails is not executed, so nothing reads the records before it.
                 const bool bad = (uint32_t)off > (uint32_t)(op + ll);
-                const bool lim17 = (ll | ml) >= (1 << kLenBits);
+                // (the output bound per step too: op and lp are 32-bit, and up to 2^15 sequences of < 2^18 bytes
+                // each could wrap op back into range before the block-end check; such a frame goes to the one-wave
+                // decoder, whose verdict is ZSTD_execSequence's.  With it op <= n at every step, so lp <= op never
+                // wraps either.)
+                const bool lim17 = ((ll | ml) >= (1 << kLenBits)) | (op + ll + ml > n);
                 r0 = (uint32_t)ll | ((uint32_t)ml << kLenBits);
                 r1 = ((uint32_t)ml >> (32 - kLenBits)) | ((uint32_t)off << (2 * kLenBits - 32));
                 keep = !(bad | lim17);
@@ -3357,29 +3361,59 @@ extern "C" int lzh_debug_zstd_side(int on) {
     g_zstd_side = on ? 1 : 0;
     return 0;
 }
-static hipStream_t g_side_stream[64][2];
+// Side streams per caller stream (and per slot k): independent callers -- the batched rows' two alternating
+// kernel streams, other threads' streams -- never queue behind each other's forked kernels.  Each entry owns its
+// fork / join events (a call records and waits them on its own caller stream, in order).  A caller stream on a
+// device other than the current one, or past kMaxSide entries, gets no side stream: the caller then launches
+// everything on its own stream, in order.
+struct SideEntry {
+    hipStream_t caller;
+    int dev, k;
+    hipStream_t ss;
+    hipEvent_t fork, join;
+};
+static constexpr int kMaxSide = 256;
+static SideEntry g_side[kMaxSide];
+static int g_nside = 0;
 static std::mutex g_side_mu;
-// (events per thread: a call's fork / join records and waits are enqueued by the calling thread in order)
-static thread_local hipEvent_t t_side_ev[64][2][2];
-bool lzh_side_stream(int dev, hipStream_t& ss, hipEvent_t& fork, hipEvent_t& join, int k) {
-    if (dev < 0 || dev >= 64 || k < 0 || k > 1) return false;
-    {
-        std::lock_guard<std::mutex> g(g_side_mu);
-        if (!g_side_stream[dev][k]) {
-            int lo = 0, hi = 0;
-            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
-            hipStream_t st = nullptr;   // (the highest priority: their waves go out before the caller's stream's)
-            if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi) != hipSuccess) return false;
-            g_side_stream[dev][k] = st;
+bool lzh_side_stream(hipStream_t s, hipStream_t& ss, hipEvent_t& fork, hipEvent_t& join, int k) {
+    if (k < 0 || k > 1) return false;
+    int dev = -1, sdev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    hipDevice_t d = 0;
+    if (hipStreamGetDevice(s, &d) != hipSuccess) return false;
+    sdev = (int)d;
+    if (sdev != dev) return false;
+    std::lock_guard<std::mutex> g(g_side_mu);
+    for (int i = 0; i < g_nside; i++)
+        if (g_side[i].caller == s && g_side[i].dev == dev && g_side[i].k == k) {
+            ss = g_side[i].ss;
+            fork = g_side[i].fork;
+            join = g_side[i].join;
+            return true;
         }
+    if (g_nside >= kMaxSide) return false;
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+    SideEntry e{s, dev, k, nullptr, nullptr, nullptr};
+    // (the highest priority: their waves go out before the caller's stream's)
+    if (hipStreamCreateWithPriority(&e.ss, hipStreamNonBlocking, hi) != hipSuccess) return false;
+    if (hipEventCreateWithFlags(&e.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e.join, hipEventDisableTiming) != hipSuccess) {
+        if (e.fork) (void)hipEventDestroy(e.fork);
+        (void)hipStreamDestroy(e.ss);
+        return false;
     }
-    for (int i = 0; i < 2; i++)
-        if (!t_side_ev[dev][k][i] && hipEventCreateWithFlags(&t_side_ev[dev][k][i], hipEventDisableTiming) != hipSuccess)
-            return false;
-    ss = g_side_stream[dev][k];
-    fork = t_side_ev[dev][k][0];
-    join = t_side_ev[dev][k][1];
+    g_side[g_nside++] = e;
+    ss = e.ss;
+    fork = e.fork;
+    join = e.join;
     return true;
+}
+// (tests: how many side streams the library holds)
+extern "C" int lzh_debug_side_streams() {
+    std::lock_guard<std::mutex> g(g_side_mu);
+    return g_nside;
 }
 // the sequence / execution plan by sequence count (lzh_zstd_plan_kernel; 0: one sequence launch)
 static int g_zstd_plan = 1;
@@ -3528,8 +3562,8 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         uint32_t* fcnt = flist + nchunks;
         hipStream_t sq[2] = {s, s};
         hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
-        const bool side = !LZH_ZSTD_STATS && g_zstd_side && lzh_side_stream(hdev, sq[0], fork[0], join[0], 0) &&
-                          lzh_side_stream(hdev, sq[1], fork[1], join[1], 1);
+        const bool side = !LZH_ZSTD_STATS && g_zstd_side && lzh_side_stream(s, sq[0], fork[0], join[0], 0) &&
+                          lzh_side_stream(s, sq[1], fork[1], join[1], 1);
         const unsigned sgrid = (nchunks + zsplit::kFPW - 1) / zsplit::kFPW;
         if (!hcus[hdev] && hipDeviceGetAttribute(&hcus[hdev], hipDeviceAttributeMultiprocessorCount, hdev) != hipSuccess)
             hcus[hdev] = 0;
@@ -3569,9 +3603,10 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
         hipLaunchKernelGGL(hj == 8 ? lzh_zstd_huf8_kernel : lzh_zstd_huf_kernel, dim3((unsigned)((maxjobs + hj - 1) / hj)),
                            dim3(64), 0, s, packed, packed_readable, offsets, n_total, chunk_size, out, status, zt, zst,
                            (const zsplit::ZHuf*)jobs, (const uint32_t*)njobs, hstats, g_zstd_hufpar);
-        hipLaunchKernelGGL(lzh_zstd_hufpar_kernel, dim3((unsigned)(maxjobs * 4)), dim3(64), 0, s, packed, packed_readable,
-                           offsets, chunk_size, out, status, zt, zst, (const zsplit::ZHuf*)jobs, (const uint32_t*)njobs,
-                           g_zstd_hufpar);
+        if (g_zstd_hufpar)   // (off: the per-lane kernel above decoded every stream)
+            hipLaunchKernelGGL(lzh_zstd_hufpar_kernel, dim3((unsigned)(maxjobs * 4)), dim3(64), 0, s, packed,
+                               packed_readable, offsets, chunk_size, out, status, zt, zst, (const zsplit::ZHuf*)jobs,
+                               (const uint32_t*)njobs, g_zstd_hufpar);
 #if LZH_ZSTD_STATS
         {
             unsigned long long h[8];

@@ -18,10 +18,10 @@ hipError_t lzh_launch_zstd_decompress(const uint8_t* packed, uint64_t packed_rea
                                       const uint32_t* csizes, uint64_t n_total, uint64_t chunk_size, uint8_t* out,
                                       int32_t* status, uint32_t nchunks, uint8_t* zt, hipStream_t s);
 size_t lzh_zstd_decode_temp(uint64_t n, uint64_t chunk_size);
-// per-device library stream k (0 or 1; highest priority, created once) and this thread's fork / join events
-// for it (decode_hip.hip): work forked to it after a record of `fork` on the caller's stream joins back through
-// `join`
-bool lzh_side_stream(int dev, hipStream_t& ss, hipEvent_t& fork, hipEvent_t& join, int k = 0);
+// side stream k (0 or 1; highest priority, created once) of the caller's stream s and its fork / join events
+// (decode_hip.hip): work forked to it after a record of `fork` on s joins back through `join`.  False (launch
+// on s) when s belongs to another device than the current one.
+bool lzh_side_stream(hipStream_t s, hipStream_t& ss, hipEvent_t& fork, hipEvent_t& join, int k = 0);
 // snappy chunks of more than one 64 KiB fragment: split scan, fragments in parallel, serial fallback
 size_t lzh_snappy_split_temp(uint64_t n, uint64_t chunk_size);
 hipError_t lzh_launch_snappy_split_decompress(const uint8_t* packed, uint64_t packed_readable, const uint64_t* offsets,

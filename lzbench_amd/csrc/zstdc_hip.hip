@@ -977,8 +977,10 @@ __device__ __forceinline__ void fse_encode(BitW<Sink>& b, const LDSA Fse& ct, ui
 }
 
 // ---- Huffman (huf_compress.c), lane 0 only
-// (RANK_POSITION_DISTINCT_COUNT_CUTOFF, huf_compress.c:455, is 158 + BIT_highbit32(158) = 165: bucket 165
-// holds counts 165..255 and is sorted like the other log2 buckets)
+// (RANK_POSITION_DISTINCT_COUNT_CUTOFF, huf_compress.c:455, is 158 + BIT_highbit32(158) = 165.  HUF_sort stores
+// a symbol at region HUF_getIndex(count) + 1 (:577): its sort loop starts at region 165, the count-164 ties, and
+// counts 165..255 are its region 166.  Buckets here are its regions minus one: bucket 165 holds counts 165..255
+// and is sorted like the other log2 buckets)
 __device__ __forceinline__ uint32_t huf_bucket(uint32_t c) { return c < 165 ? c : hb32(c) + 158; }
 __device__ __forceinline__ HNode hget(const LDSA HNode* a) {
     HNode t;
@@ -1881,14 +1883,12 @@ hipError_t lzh_launch_zstd_compress(const uint8_t* in, uint64_t n_total, uint64_
                            Lo.tmp_off, stage, stride, csizes, f0);
     };
     // Single-block frames: a frame's entropy stage needs only its own match stage, so the frames split in
-    // two.  The first half runs match + entropy on the library's high-priority side stream (its waves go
+    // two.  The first half runs match + entropy on the caller stream's high-priority side stream (its waves go
     // out first), the second half's match on the caller's stream beside it; the first half's entropy then
     // runs beside the second half's matching and only the second half's entropy is left at the end.
-    int dev = 0;
-    (void)hipGetDevice(&dev);
     hipStream_t sq = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    if (g_zstdc_split && std::max(nblocks, 1u) == 1 && nchunks >= 2 && lzh_side_stream(dev, sq, fork, join)) {
+    if (g_zstdc_split && std::max(nblocks, 1u) == 1 && nchunks >= 2 && lzh_side_stream(s, sq, fork, join)) {
         const uint32_t h = nchunks / 2;
         (void)hipEventRecord(fork, s);
         (void)hipStreamWaitEvent(sq, fork, 0);

@@ -351,7 +351,10 @@ typedef struct { u8 nb[256]; u16 val[256]; u32 tlog; } huf_ct;
 /* sort symbols by decreasing count: buckets per distinct small count, log2 buckets from 165 on,
  * each log2 bucket quick-sorted (HUF_sort / HUF_simpleQuickSort, huf_compress.c:460-595).  The cutoff
  * RANK_POSITION_DISTINCT_COUNT_CUTOFF (huf_compress.c:455) is 158 + BIT_highbit32(158) = 165, not the 166
- * its comment states: bucket 165 holds counts 165..255 and is sorted */
+ * its comment states.  HUF_sort stores a symbol at region HUF_getIndex(count) + 1 (huf_compress.c:577), so the
+ * reference's sort loop starts at region 165, which holds the count-164 ties (sorting them changes nothing),
+ * and counts 165..255 are its region 166.  Buckets here are the reference's regions minus one: bucket 165
+ * holds counts 165..255, and the sorted buckets start there */
 static u32 huf_bucket(u32 c) { return c < 165 ? c : hb32(c) + 158; }
 static void hn_swap(hnode* a, hnode* b) { hnode t = *a; *a = *b; *b = t; }
 static void huf_isort(hnode* a, int lo, int hi) {

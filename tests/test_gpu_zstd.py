@@ -414,3 +414,50 @@ def test_long_literal_streams_wave_parallel(torch_cuda):
     st0, out0 = gpu_decode(torch, packed, cs, n, chunk, "nopar")
     assert (st == expected_sizes(n, chunk)).all() and (st == st0).all()
     assert (out == data).all() and (out0 == data).all()
+
+
+def _rle_seq_frame(nseq: int, n: int = 131072) -> bytes:
+    """A single-segment frame of one compressed block (RFC 8878 3.1.1.3): nseq raw literals and nseq sequences
+    with RLE-coded LL / OF / ML codes 1 / 0 / 52 -- literal length 1, repcode 1 (offset 1), match length
+    65539 + 16 extra bits, all 0xFFFC: 131071 -- so every sequence adds 2^17 output bytes.  nseq = 1 is a valid
+    frame of exactly n = 2^17 bytes; nseq = 32769 sums the sequences to 2^32 + 2^17, which a 32-bit output
+    position wraps to exactly n (the reference rejects it at its second sequence, ZSTD_execSequence)."""
+    lit = bytes([0x41]) * nseq
+    if nseq < 32:
+        lh = bytes([nseq << 3])                                   # raw, 5-bit size
+    else:
+        lh = bytes([0x0C | ((nseq & 15) << 4), (nseq >> 4) & 0xFF, nseq >> 12])   # raw, 20-bit size
+    if nseq < 128:
+        sh = bytes([nseq])
+    elif nseq < 0x7F00:
+        sh = bytes([128 + (nseq >> 8), nseq & 0xFF])
+    else:
+        sh = bytes([255]) + (nseq - 0x7F00).to_bytes(2, "little")
+    sh += bytes([(1 << 6) | (1 << 4) | (1 << 2), 1, 0, 52])     # LL / OF / ML RLE; their codes
+    # the bitstream, read backwards: per sequence 0 offset bits, 16 ML bits, 0 LL bits (RLE states: 0 bits)
+    bits = (0xFFFC).to_bytes(2, "little") * nseq + b"\x01"     # (the end marker)
+    body = lh + lit + sh + bits
+    fh = b"\x28\xb5\x2f\xfd" + bytes([0x20 | (2 << 6)]) + n.to_bytes(4, "little")
+    return fh + (1 | (2 << 1) | (len(body) << 3)).to_bytes(3, "little") + body
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_sequences_past_2_31_output_bytes(torch_cuda, path):
+    """(round-5 advisor) sequences whose lengths sum past 2^31 -- a 32-bit output position wraps back into
+    range -- get the reference's verdict on every path; the one-sequence frame of the same layout decodes exact"""
+    chunk = 131072
+    R = O.ref() if O.have_ref() else None
+    frames = [_rle_seq_frame(1), _rle_seq_frame(32769)]
+    expect = np.frombuffer(b"\x41" * chunk, np.uint8)
+    if R is not None:
+        for f, want in zip(frames, (chunk, None)):
+            src = np.frombuffer(f, np.uint8).copy()
+            dst = np.zeros(chunk + 64, np.uint8)
+            r = R.ref_zstd_decompress(src.ctypes.data, len(f), dst.ctypes.data, chunk)
+            assert (r == chunk) == (want == chunk), r
+            if want == chunk:
+                assert (dst[:chunk] == expect).all()
+    st, out = gpu_decode(torch_cuda, np.frombuffer(b"".join(frames), np.uint8), [len(f) for f in frames], 2 * chunk,
+                         chunk, path)
+    assert st[0] == chunk and (out[:chunk] == expect).all(), st
+    assert st[1] < 0, st

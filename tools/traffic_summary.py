@@ -15,7 +15,14 @@ for f in glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"), recu
     for (kern, name), v in s.items():
         if kern.startswith("lzh_"):
             res[kern][name + "_bytes_per_dispatch"] = v / max(1, len(d[(kern, name)])) * 1024.0
+# the machine code measured: the code hash of each kernel in the library the passes loaded (bench.py reports a
+# profile's traffic only while the loaded library's kernel has the same hash)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from lzbench_amd import kernel_hash
+lib = os.environ.get("LZH_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lzbench_amd", "liblzbench_hip.so")
+hashes = kernel_hash.kernel_hashes(lib)
 for k, v in res.items():
+    v["kernel_hash"] = hashes.get(k)
     v["traffic_bytes_per_dispatch"] = v.get("FETCH_SIZE_bytes_per_dispatch", 0.0) + v.get("WRITE_SIZE_bytes_per_dispatch", 0.0)
 wkey = sys.argv[2] if len(sys.argv) > 2 else "lz4/1/64/text/1073741824"   # bench.py's workload key
 json.dump({"workload": "tools/prof_kernels.py " + wkey, "workload_key": wkey, "kernels": res}, open(os.path.join(out, "traffic.json"), "w"), indent=1)
