@@ -1,9 +1,9 @@
-# tools/r05_ab.sh VARIANT CODEC "CORPUS:CHUNK_KIB ..." -- parity (rows vs the reference at 1 GiB) and a
+# tools/rows_ab.sh VARIANT CODEC "CORPUS:CHUNK_KIB ..." -- parity (rows vs the reference at 1 GiB) and a
 # compress-kernel A/B (in-tree vs build/exp/VARIANT, alternating, two rounds), rocprofv3 kernel traces
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 V=$1; C=$2; W=$3
-O=gpurun_out/r05_ab_$V; mkdir -p $O
+O=gpurun_out/ab_$V; mkdir -p $O
 export TMPDIR=/tmp
 LIB=$GRAFT_REPO_ROOT/build/exp/$V/liblzbench_hip.so
 for w in $W; do c=${w%%:*}; k=${w##*:}
