@@ -81,6 +81,24 @@ __device__ __forceinline__ uint32_t lane_gather(uint32_t v, int src) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
 
+// Wave-wide inclusive max of x >= 0 by DPP row shifts and row broadcasts (no LDS round trip); with
+// x = (member ? end : 0) over lanes whose members' ends increase with the lane, it gives every lane the end
+// of the last member at or before it (0: none)
+__device__ __forceinline__ int wave_incl_max(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false));   // row_shr:1
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false));   // row_shr:2
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false));   // row_shr:4
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false));   // row_shr:8
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));   // row_bcast:15 -> rows 1, 3
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+// the value of lane - 1 (0 in lane 0): DPP wave_shr:1
+__device__ __forceinline__ int wave_shr1(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x138, 0xf, 0xf, false); }
+// the same by byte address (4 x the source lane; a constant offset can fold into ds_bpermute's offset field)
+__device__ __forceinline__ uint32_t lane_gather_b(uint32_t v, int addr) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v);
+}
 // compiler-level ordering for LDS traffic between lanes of the one wave of a workgroup
 // (DS instructions of a wave execute in order in hardware)
 __device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }

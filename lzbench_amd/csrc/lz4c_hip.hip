@@ -226,6 +226,19 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
+#ifndef LZH_LZ4_DPPEND
+#define LZH_LZ4_DPPEND 1
+#endif
+#ifndef LZH_LZ4_RESTORE2
+#define LZH_LZ4_RESTORE2 1
+#endif
+#ifndef LZH_LZ4_RW   // the parse kernel without its LDS input ring: register-window P sides, 10 waves per CU
+#define LZH_LZ4_RW 1
+#endif
+#ifndef LZH_LZ4_PADLDS
+#define LZH_LZ4_PADLDS 0
+#endif
+
 // Sequences found by one batch, one per member lane (the lane of the sequence's match start):
 // anchor, literal count, offset, match length - 4, first output byte within the batch's
 // output.  Emitted lane-parallel under the NEXT batch's candidate loads.  Plain locals (a
@@ -380,6 +393,25 @@ __device__ __forceinline__ PSide p_side_global(const Bytes& in, int p) {
                    a6 = ld_b32(in.r, A + 24), a7 = ld_b32(in.r, A + 28);
     PSide v;
     v.m4 = __builtin_amdgcn_alignbyte(a1, a0, s);
+    v.w = __builtin_amdgcn_alignbyte(a2, a1, s);
+    v.q0 = __builtin_amdgcn_alignbyte(a3, a2, s);
+    v.q1 = __builtin_amdgcn_alignbyte(a4, a3, s);
+    v.q2 = __builtin_amdgcn_alignbyte(a5, a4, s);
+    v.q3 = __builtin_amdgcn_alignbyte(a6, a5, s);
+    v.q4 = __builtin_amdgcn_alignbyte(a7, a6, s);
+    return v;
+}
+
+// the same from a register window: lane l of Wc holds the dword at window byte 4l; ol = the lane's position's
+// byte offset in the window (0 <= ol, (ol & ~3) + 24 < 256): its seven dwords by ds_bpermute (no LDS allocation)
+__device__ __forceinline__ PSide p_side_win(uint32_t Wc, int ol) {
+    const int a = ol & ~3;
+    const uint32_t s = (uint32_t)ol & 3u;
+    const uint32_t a1 = lane_gather_b(Wc, a), a2 = lane_gather_b(Wc, a + 4), a3 = lane_gather_b(Wc, a + 8),
+                   a4 = lane_gather_b(Wc, a + 12), a5 = lane_gather_b(Wc, a + 16), a6 = lane_gather_b(Wc, a + 20),
+                   a7 = lane_gather_b(Wc, a + 24);
+    PSide v;
+    v.m4 = 0;   // (no in-kernel catch-up on this path)
     v.w = __builtin_amdgcn_alignbyte(a2, a1, s);
     v.q0 = __builtin_amdgcn_alignbyte(a3, a2, s);
     v.q1 = __builtin_amdgcn_alignbyte(a4, a3, s);
@@ -594,7 +626,9 @@ struct LinkCtl {
 // e+1, e+2, then steps of acc for 64 probes: offsets {0, 1, 2, 2+acc, 2+2acc, ..} from e.  Run
 // batches cover the first 64 search probes of each segment (as with acc 1); later probes and the
 // chunk tail (where a probe's forwardIp could pass mflimit) go through stride batches.
-template <bool kSmall, bool kStats, bool kRec = false, bool kFast = false, bool kLinked = false>
+// kRW (records only): no LDS input ring -- the table alone (16 KiB) leaves room for 10 waves per CU instead of 9 --
+// and the run batches' P sides come from a register window of the input (see the loop top)
+template <bool kSmall, bool kStats, bool kRec = false, bool kFast = false, bool kLinked = false, bool kRW = false>
 __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc, LDSA uint32_t* tab,
                                LDSA uint32_t* ringw, LDSA uint8_t* outb, uint32_t* out_size,
                                unsigned long long* stats, rsrc_t recs, uint32_t* rec_hdr, LinkCtl* lk = nullptr) {
@@ -621,7 +655,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
 #pragma unroll
         for (int i = 0; i < 16; i++) lds_zero16(t4 + 4 * (i * LZH_WAVE + lane));
     }
-    constexpr bool kRingOn = true;   // (without the ring -- more waves, P sides from memory -- 6 % slower, profiles/r05_lnr)
+    static_assert(!kRW || kRec, "the register window serves the records-only parse");
+    // (without the ring and with every P side from memory -- 10 waves -- 6 % slower, profiles/r05_lnr; kRW keeps
+    // the P sides off memory's latency with a register window)
+    constexpr bool kRingOn = !kRW;
     Ring R{ringw, in.sh, 0, 0, kRingOn, kRec};   // (the parse kernel's ring carries a 32-byte mirror)
     if (kLinked) R.fill = max(((b0 + in.sh) & ~255) - 256, 0);   // (a block's ring starts just before it)
     OutRing O{outb, out.sh, 0};
@@ -671,6 +708,15 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             PAT = 3ull | (PER << 2);
         }
 
+        // (kRW) register window over the input: Wc = the 256 bytes at descriptor offset WX (a multiple of 4), one
+        // dword a lane; Wn = the 256 bytes at WX + 128, loaded at the top of every batch (unconditionally, so no
+        // register merges with a load in flight) and ready after that batch's load wait.  A run batch at base
+        // uses Wc when its 64 positions' P sides lie in it (0 <= base + sh - WX <= kWinMax), else moves the
+        // window up by 128 (Wc = Wn) when that covers it, else takes its P sides from memory and restarts the
+        // window at its base.
+        constexpr int kWinMax = 168;           // lane 63's last dword ((o + 63) & ~3) + 24 stays below byte 256
+        uint32_t Wc = 0, Wn = 0;
+        int WX = 0, wc_ok = 0, wn_ok = 0;
         for (int guard = 0;; guard++) {
             // (the loop-carried parse state is wave-uniform: readfirstlane keeps it in SGPRs, and the
             // exit test on uniform values is a scalar branch, not an exec-mask loop exit)
@@ -730,7 +776,26 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             // ---- P-side bytes (ring when it covers the batch), hash, table read / claim / read back
             PSide ps;
             uint32_t b4 = 0;
-            if (R.has(front - 4, pmax + 28)) {
+            if (kRW) {
+                WX = unii(WX); wc_ok = unii(wc_ok); wn_ok = unii(wn_ok);
+                int o = front + in.sh - WX;
+                int use = 0;                                           // 1: Wc, 2: Wc = Wn (window up 128)
+                if (runb) {
+                    if (wc_ok && o >= 0 && o <= kWinMax) use = 1;
+                    else if (wn_ok && o >= 128 && o - 128 <= kWinMax) use = 2;
+                }
+                if (use == 2) { Wc = Wn; WX += 128; o -= 128; LZ_STAT(4, 1); }
+                if (!use) WX = ((front + in.sh) & ~3) - 128;          // (Wn below: the window from here on)
+                wc_ok = use != 0;
+                wn_ok = 0;
+                Wn = ld_b32(in.r, WX + 128 + 4 * lane);
+                if (use) {
+                    ps = p_side_win(Wc, o + lane);
+                } else {
+                    LZ_STAT(9, 1);
+                    ps = p_side_global(in, p);
+                }
+            } else if (R.has(front - 4, pmax + 28)) {
                 ps = kRec ? p_side_ring_m<false>(R, p) : p_side_ring(R, p);
             } else {
                 LZ_STAT(9, 1);
@@ -805,6 +870,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             else wait_vm();
             recs_st = false;
             R.ready = R.fill;
+            if (kRW) wn_ok = 1;                                        // (this batch's Wn has landed)
             wave_lds_fence();
             LZ_CLK(3);                                                 // exposed load wait
             // ring refill and output flush after the wait: they complete under the next batch
@@ -901,6 +967,16 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         eL = rdlanei(e, sl);
                         LZ_CLK(11);                            // (stats: the scalar walk)
                         // lanes strictly inside a member's match are not probed; ip-2 is inserted
+                        if (!kFast && LZH_LZ4_DPPEND) {
+                            // the end of the last member at or before each lane: members' ends increase along
+                            // the chain (the next member starts at or after the previous end), so it is the
+                            // running max of the members' ends -- DPP, no LDS round trip
+                            const bool mem = lane_on(Mm);
+                            const int ej = wave_incl_max(mem ? e : 0);
+                            const bool inside = !mem && lane < ej;
+                            E = ballot(lane >= lo && !inside && (!endip || lane < eL));
+                            I = ballot(!mem && lane == ej - 2);        // lz4.c:1146 (a member's own end is >= lane + 4)
+                        } else {
                         const uint64_t mle = Mm & (below | (1ull << lane));
                         const int j = mle ? 63 - __builtin_clzll(mle) : lane;
                         const int ej = (int)lane_gather((uint32_t)e, j);
@@ -911,6 +987,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                                          : lane_on(P0);        // member's end: its pattern
                         E = ballot(probed && (!endip || lane < eL));
                         I = ballot(mle && lane == ej - 2);             // lz4.c:1146
+                        }
                         endp = endip || (eL < LZH_WAVE && LZH_WAVE - 1 >= fv);   // or the search ran past mflimit
                     }
                     I = (Mm ? I : 0ull) | I0 | E;                          // (no stale bits from an earlier round)
@@ -995,7 +1072,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     }
                     // table: the last inserted lane of each slot, or the slot's old value
                     const bool inI = lane_on(I);
-                    if (vmask == ~0ull) {
+                    if (LZH_LZ4_RESTORE2 && !losers) {
+                        // (no two lanes share a slot: every claim stands, a lane not inserted puts its old value back)
+                        if (valid && !inI) T.put(h, old);
+                    } else if (vmask == ~0ull) {
                         // every lane stores its slot's final value (all lanes of a slot agree):
                         // the slot's last inserted lane, else its old value
                         const uint64_t gi = grp & I;
@@ -1188,11 +1268,11 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
     LDSA uint32_t* ring = tab + 4096;
     const rsrc_t nr = make_rsrc(nullptr, 0);
     if (n < 65547) {
-        if (acc > 1) lz4v3::compress_chunk<true, true, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
-        else lz4v3::compress_chunk<true, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
+        if (acc > 1) lz4v3::compress_chunk<true, true, true, true, false, LZH_LZ4_RW>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
+        else lz4v3::compress_chunk<true, true, true, false, false, LZH_LZ4_RW>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
     } else {
-        if (acc > 1) lz4v3::compress_chunk<false, true, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
-        else lz4v3::compress_chunk<false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
+        if (acc > 1) lz4v3::compress_chunk<false, true, true, true, false, LZH_LZ4_RW>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
+        else lz4v3::compress_chunk<false, true, true, false, false, LZH_LZ4_RW>(rin, n, rout, acc, tab, ring, nullptr, nullptr, stats, nr, hdr);
     }
 }
 
@@ -1207,7 +1287,9 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                      uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint64_t frame_size, uint32_t bpf) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + lz4v3::kRing / 4 + 8];   // table | ring + mirror
+    // table only (16 KiB: 10 waves per CU; the P sides from a register window, compress_chunk's kRW)
+    // (LZH_LZ4_PADLDS: extra bytes of LDS per wave -- an occupancy experiment, 0 in builds)
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + (LZH_LZ4_RW ? 0 : lz4v3::kRing / 4 + 8) + LZH_LZ4_PADLDS / 4];
     const uint64_t chunk = blockIdx.x;
     uint64_t off;
     int n;
@@ -1221,11 +1303,11 @@ lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, 
     const rsrc_t rr = make_rsrc(recs + chunk * rec_stride, (uint32_t)rec_stride);
     uint32_t* hdr = rec_hdr + 2 * chunk;
     if (n < 65547) {
-        if (acc > 1) lz4v3::compress_chunk<true, false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
-        else lz4v3::compress_chunk<true, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+        if (acc > 1) lz4v3::compress_chunk<true, false, true, true, false, LZH_LZ4_RW>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+        else lz4v3::compress_chunk<true, false, true, false, false, LZH_LZ4_RW>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
     } else {
-        if (acc > 1) lz4v3::compress_chunk<false, false, true, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
-        else lz4v3::compress_chunk<false, false, true>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+        if (acc > 1) lz4v3::compress_chunk<false, false, true, true, false, LZH_LZ4_RW>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
+        else lz4v3::compress_chunk<false, false, true, false, false, LZH_LZ4_RW>(rin, n, rout, acc, tab, ring, nullptr, nullptr, nullptr, rr, hdr);
     }
 }
 

@@ -7,8 +7,8 @@ lib = L.lib()
 f = lib.lzh_debug_lz4_stats
 f.restype = C.c_int
 f.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
-names = ["batches", "collision_batches", "slow_colliders", "sequences", "-", "catchup_slow", "count_slow", "-",
-         "-", "hash_ring_miss", "-", "-", "refills", "-", "-", "-"]
+names = ["batches", "collision_batches", "slow_colliders", "sequences", "window_moved", "catchup_slow", "count_slow", "-",
+         "-", "pside_from_memory", "-", "-", "refills", "-", "-", "-"]
 for corpus in sys.argv[1:] or ["text", "json"]:
     n = int(os.environ.get("STATS_MIB", "512")) << 20
     host = L.datagen(corpus, n, seed=12345)
