@@ -708,12 +708,13 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             PAT = 3ull | (PER << 2);
         }
 
-        // (kRW) register window over the input: Wc = the 256 bytes at descriptor offset WX (a multiple of 4), one
-        // dword a lane; Wn = the 256 bytes at WX + 128, loaded at the top of every batch (unconditionally, so no
-        // register merges with a load in flight) and ready after that batch's load wait.  A run batch at base
-        // uses Wc when its 64 positions' P sides lie in it (0 <= base + sh - WX <= kWinMax), else moves the
-        // window up by 128 (Wc = Wn) when that covers it, else takes its P sides from memory and restarts the
-        // window at its base.
+        // (kRW) register window over the input, one dword a lane: Wc = the 256 bytes at descriptor offset WX (a
+        // multiple of 4), Wn = those at WX + 128.  A run batch at base takes its P sides from Wc when its 64
+        // positions' bytes lie in it (0 <= base + sh - WX <= kWinMax), else moves the window up by 128 (Wc = Wn)
+        // when that covers it, else reads them from memory and restarts the window at its base (2.8 batches per
+        // 64 KiB chunk of text, profiles/r06_e).  Wn is reloaded in every batch (unconditionally, so no register
+        // merges with a load in flight), after its candidate loads: their wait -- the compiler's, by register --
+        // leaves it in flight, and the next batch's window move waits for it.
         constexpr int kWinMax = 168;           // lane 63's last dword ((o + 63) & ~3) + 24 stays below byte 256
         uint32_t Wc = 0, Wn = 0;
         int WX = 0, wc_ok = 0, wn_ok = 0;
@@ -779,16 +780,14 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             if (kRW) {
                 WX = unii(WX); wc_ok = unii(wc_ok); wn_ok = unii(wn_ok);
                 int o = front + in.sh - WX;
-                int use = 0;                                           // 1: Wc, 2: Wc = Wn (window up 128)
+                int use = 0;                                           // 1: Wc, 2: the window moved up 128
                 if (runb) {
                     if (wc_ok && o >= 0 && o <= kWinMax) use = 1;
                     else if (wn_ok && o >= 128 && o - 128 <= kWinMax) use = 2;
                 }
                 if (use == 2) { Wc = Wn; WX += 128; o -= 128; LZ_STAT(4, 1); }
-                if (!use) WX = ((front + in.sh) & ~3) - 128;          // (Wn below: the window from here on)
+                if (!use) WX = ((front + in.sh) & ~3) - 128;          // (Wn from here on: the next batch's Wc)
                 wc_ok = use != 0;
-                wn_ok = 0;
-                Wn = ld_b32(in.r, WX + 128 + 4 * lane);
                 if (use) {
                     ps = p_side_win(Wc, o + lane);
                 } else {
@@ -864,13 +863,19 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 bep = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
                 okp = valid && gw == ps.w;
             }
-            // the candidate loads; a record store issued after them need not be acknowledged
-            // (vector memory operations complete in issue order)
-            if (kRec && recs_st) wait_vm_but1();
-            else wait_vm();
+            if (kRW) {
+                // the window's next part, after the candidate loads (no explicit wait: the compiler waits for the
+                // candidate data by register, which leaves this load in flight)
+                Wn = ld_b32(in.r, WX + 128 + 4 * lane);
+                wn_ok = 1;                                             // (for the next batch, restarted or not)
+            } else {
+                // the candidate loads; a record store issued after them need not be acknowledged
+                // (vector memory operations complete in issue order)
+                if (kRec && recs_st) wait_vm_but1();
+                else wait_vm();
+            }
             recs_st = false;
             R.ready = R.fill;
-            if (kRW) wn_ok = 1;                                        // (this batch's Wn has landed)
             wave_lds_fence();
             LZ_CLK(3);                                                 // exposed load wait
             // ring refill and output flush after the wait: they complete under the next batch

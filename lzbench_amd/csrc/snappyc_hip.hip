@@ -25,9 +25,6 @@
 namespace snv2 {
 
 #define SN_STAT(i, v) do { if (stats && lane == 0) atomicAdd(&stats[i], (unsigned long long)(v)); } while (0)
-#ifndef LZH_SN_RW   // the parse kernel without its LDS input ring: register-window P sides, 5 waves per CU
-#define LZH_SN_RW 0
-#endif
 #ifndef LZH_SN_PADLDS
 #define LZH_SN_PADLDS 0
 #endif
@@ -359,33 +356,14 @@ __device__ __forceinline__ PS p_side(const Ring& R, const Bytes& in, bool ring, 
     v.q5 = __builtin_amdgcn_alignbyte(a6, a5, s);
     return v;
 }
-// the same from a register window (kRW): lane l of Wc holds the window's dword l, ol = the lane's position's byte
-// offset in it ((ol & ~3) + 24 < 256): seven dwords by ds_bpermute, no LDS allocation
-__device__ __forceinline__ PS p_side_win(uint32_t Wc, int ol) {
-    const int a = ol & ~3;
-    const uint32_t s = (uint32_t)ol & 3u;
-    const uint32_t a0 = lane_gather_b(Wc, a), a1 = lane_gather_b(Wc, a + 4), a2 = lane_gather_b(Wc, a + 8),
-                   a3 = lane_gather_b(Wc, a + 12), a4 = lane_gather_b(Wc, a + 16), a5 = lane_gather_b(Wc, a + 20),
-                   a6 = lane_gather_b(Wc, a + 24);
-    PS v;
-    v.w = __builtin_amdgcn_alignbyte(a1, a0, s);
-    v.q1 = __builtin_amdgcn_alignbyte(a2, a1, s);
-    v.q2 = __builtin_amdgcn_alignbyte(a3, a2, s);
-    v.q3 = __builtin_amdgcn_alignbyte(a4, a3, s);
-    v.q4 = __builtin_amdgcn_alignbyte(a5, a4, s);
-    v.q5 = __builtin_amdgcn_alignbyte(a6, a5, s);
-    return v;
-}
 // bytes matched after the first 4 (0..20) between two 24-byte windows
 __device__ __forceinline__ int match_after4(const PS& a, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t b4,
                                             uint32_t b5) {
     return first_diff20(a.q1 ^ b1, a.q2 ^ b2, a.q3 ^ b3, a.q4 ^ b4, a.q5 ^ b5);
 }
 
-// one fragment in[0, fn) appended at op (kRec: its records appended at nrec).  kRW (records only): no LDS input
-// ring -- the 32 KiB table alone leaves room for 5 waves per CU instead of 4 -- and the run batches' P sides from
-// a register window of the input (as the LZ4 parse kernel's kRW, lz4c_hip.hip)
-template <bool kRec, bool kRW = false>
+// one fragment in[0, fn) appended at op (kRec: its records appended at nrec)
+template <bool kRec>
 __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int op, LDSA uint16_t* tab,
                                  LDSA uint32_t* ringw, LDSA uint8_t* mark, unsigned long long* stats, rsrc_t recs,
                                  int& nrec, int fbase) {
@@ -398,9 +376,9 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
         const int nvec = (int)(tsize * 2 / 16);
         for (int i = lane; i < nvec; i += LZH_WAVE) lds_zero16(t4 + 4 * i);
     }
-    static_assert(!kRW || kRec, "the register window serves the records-only parse");
-    // (parse kernel: mirrored ring; without it and with every P side from memory 4-6 % slower, profiles/r05_snr)
-    Ring R{ringw, in.sh, 0, 0, !kRW, kRec};
+    // (parse kernel: mirrored ring; without it and with every P side from memory 4-6 % slower, profiles/r05_snr;
+    // with the register window of the LZ4 kernel instead -- 32 KiB, 5 waves per CU -- no faster, profiles/r06_f)
+    Ring R{ringw, in.sh, 0, 0, true, kRec};
     const int endX = fn + in.sh + 8;
     for (int s = 0; s < kRing / 256 && R.fill < endX; s++) R.refill(in.r, lane);
     wait_vm();
@@ -411,7 +389,6 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
     SREC_DECL;
 #ifdef LZH_SN_CLK
     uint64_t snclk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t snwin[3] = {0, 0, 0};   // (kRW) run batches with P sides from memory / the window / the moved window
     uint64_t snclk_last = __builtin_amdgcn_s_memtime();
 #endif
     if (fn >= 15) {
@@ -425,11 +402,6 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
         bool U = ip_limit - q0 >= 16;
         int ci0 = 0, cq0 = U ? q0 + 16 : q0;
         uint32_t cu0 = U ? 48u : 32u;
-        // (kRW) register window: Wc = 256 input bytes at descriptor offset WX (a multiple of 4), Wn = those at
-        // WX + 128, reloaded at the top of every batch and ready after its load wait (lz4c_hip.hip's kRW)
-        constexpr int kWinMax = 168;
-        uint32_t Wc = 0, Wn = 0;
-        int WX = 0, wc_ok = 0, wn_ok = 0;
         for (int guard = 0; guard < 4 * fn + 64; guard++) {
             runm = unii(runm) != 0; retest = unii(retest) != 0; U = unii(U) != 0;
             base = unii(base); org = unii(org); rt = unii(rt); q0 = unii(q0); t0 = unii(t0);
@@ -460,26 +432,8 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 const int p = base + lane;
                 const uint64_t P0 = (rt >= 0 ? 2ull : 0ull) | pat_from(org - base);
                 const uint64_t I0 = rt >= 0 ? 1ull : 0ull;              // lane 0 = rt-1 (inserted, snappy.cc:652)
-                PS ps;
-                if (kRW) {
-                    WX = unii(WX); wc_ok = unii(wc_ok); wn_ok = unii(wn_ok);
-                    int o = base + in.sh - WX;
-                    int use = 0;                                     // 1: Wc, 2: Wc = Wn (window up 128)
-                    if (wc_ok && o >= 0 && o <= kWinMax) use = 1;
-                    else if (wn_ok && o >= 128 && o - 128 <= kWinMax) use = 2;
-                    if (use == 2) { Wc = Wn; WX += 128; o -= 128; }
-                    if (!use) WX = ((base + in.sh) & ~3) - 128;
-                    wc_ok = use != 0;
-                    wn_ok = 0;
-                    Wn = ld_b32(in.r, WX + 128 + 4 * lane);
-                    ps = use ? p_side_win(Wc, o + lane) : p_side(R, in, false, p);
-#ifdef LZH_SN_CLK
-                    snwin[use]++;
-#endif
-                } else {
-                    const bool ring = R.has(base, base + LZH_WAVE + 28);
-                    ps = p_side(R, in, ring, p);
-                }
+                const bool ring = R.has(base, base + LZH_WAVE + 28);
+                const PS ps = p_side(R, in, ring, p);
                 const uint32_t h = (ps.w * 0x1e35a7bdu) >> shift;
                 const uint32_t old = T.get(h);
                 const uint32_t cand = old;
@@ -531,7 +485,6 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 SN_CLK(2);
                 wait_vm();
                 R.ready = R.fill;
-                if (kRW) wn_ok = 1;
                 wave_lds_fence();
                 SN_CLK(3);
                 {
@@ -757,12 +710,6 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
             SN_STAT(0, 1);
 
             uint32_t pw;
-            if (kRW) {   // (the window restarts at this batch's front: Wn loaded unconditionally, as in run batches)
-                WX = ((front + in.sh) & ~3) - 128;
-                wc_ok = 0;
-                wn_ok = 0;
-                Wn = ld_b32(in.r, WX + 128 + 4 * lane);
-            }
             if (R.has(front - 4, pmax + 12)) pw = R.u32(p);
             else { SN_STAT(9, 1); pw = in.w32(p); }
             const uint32_t h = (pw * 0x1e35a7bdu) >> shift;
@@ -789,7 +736,6 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
             }
             wait_vm();
             R.ready = R.fill;
-            if (kRW) wn_ok = 1;
             wave_lds_fence();
 
             bool ok = valid && __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)cX & 3u) == pw;
@@ -947,8 +893,6 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
     if (lane == 0)
         for (int i = 0; i < 8; i++) atomicAdd(&lzh_sn_clk_buf[i], (unsigned long long)snclk[i]);
     if (lane == 0) atomicAdd(&lzh_sn_clk_buf[8], 1ull);
-    if (lane == 0)
-        for (int i = 0; i < 3; i++) atomicAdd(&lzh_sn_clk_buf[9 + i], (unsigned long long)snwin[i]);
 #endif
     SREC_OUT();
     if (kRec) {   // the fragment's last literal run: a literal-only record
@@ -1013,9 +957,8 @@ constexpr int kFragRecs = 16384 + 32;
 extern "C" __global__ void __launch_bounds__(64)
 lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size,
                         uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint32_t frags) {
-    // table only (32 KiB: 5 waves per CU; P sides from a register window, compress_fragment's kRW)
     // (LZH_SN_PADLDS: extra bytes of LDS per wave -- an occupancy experiment, 0 in builds)
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + (LZH_SN_RW ? 0 : 256 + 8) + LZH_SN_PADLDS / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(1 << 13) + 256 + 8 + LZH_SN_PADLDS / 4];   // table | ring + mirror
     const uint64_t chunk = blockIdx.x / frags;
     const uint32_t f = blockIdx.x - (uint32_t)chunk * frags;
     const uint64_t off = chunk * chunk_size;
@@ -1031,8 +974,8 @@ lzh_snappy_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readabl
         Bytes rin, rout;
         rin.init(in + off + fpos, readable);
         rout.init(nullptr, 0);
-        snv2::compress_fragment<true, LZH_SN_RW>(rin, fn, rout, 0, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13),
-                                                 nullptr, nullptr, rr, nrec, (int)fpos);
+        snv2::compress_fragment<true>(rin, fn, rout, 0, (LDSA uint16_t*)lds, (LDSA uint32_t*)lds + (1 << 13), nullptr,
+                                      nullptr, rr, nrec, (int)fpos);
     }
     if (threadIdx.x == 0) hdr[f] = (uint32_t)nrec;
 }

@@ -26,7 +26,3 @@ tot = sum(int(x) for x in buf[:8]) or 1
 frags = int(buf[8]) or 1
 print(corpus, chunk >> 10, "KiB: clocks per fragment %.0f" % (tot / frags),
       {names[i]: "%.1f%%" % (100 * int(buf[i]) / tot) for i in range(8)})
-w = [int(x) for x in buf[9:12]]
-if sum(w):   # (register-window builds) run batches per fragment by P-side source
-    print("  run batches per fragment: P side from memory %.1f, window %.1f, moved window %.1f"
-          % tuple(x / frags for x in w))
