@@ -235,6 +235,12 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 #ifndef LZH_LZ4_RW   // the parse kernel without its LDS input ring: register-window P sides, 10 waves per CU
 #define LZH_LZ4_RW 1
 #endif
+#ifndef LZH_LZ4_WALK4   // the chain walk with one register (4 instructions a member instead of 6)
+#define LZH_LZ4_WALK4 1
+#endif
+#ifndef LZH_LZ4_MASKS   // the resolve's probed / inserted sets as lane masks (no VGPR round trips)
+#define LZH_LZ4_MASKS 1
+#endif
 #ifndef LZH_LZ4_PADLDS
 #define LZH_LZ4_PADLDS 0
 #endif
@@ -833,7 +839,8 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 LZ_STAT(1, 1);
                 // slot groups without a loop: every lane of a slot read back the same claim
                 // winner W (whichever lane the hardware let win), so equal W <=> same slot;
-                // equality of the 6-bit W is bit-sliced over 6 ballots
+                // equality of the 6-bit W is bit-sliced over 6 ballots (64 group masks in LDS, each lane ORing
+                // its bit into its winner's, measured 2 % slower: conflicting LDS atomics, profiles/r06_g)
                 const uint32_t W = back - (uint32_t)base;
                 uint32_t ne0 = 0, ne1 = 0;                         // lanes whose winner differs in a bit
 #pragma unroll
@@ -845,6 +852,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 }
                 const uint64_t ne = ((uint64_t)ne1 << 32) | ne0;
                 grp = valid ? (~ne & vmask) : (1ull << lane);
+
                 const uint64_t eb = grp & below;
                 prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
                 coll = ballot(prev >= 0);
@@ -947,11 +955,23 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         // (links strictly increase, so the walks end)
                         for (;;) {
                             int fs;
+                            if (LZH_LZ4_WALK4) {
+                                // common case: plain links, one register for the walk (the last member is the
+                                // highest bit of Mm afterwards: members increase) -- 4 instructions a member
+                                fs = unii(sl);
+                                Mm = uni64(Mm);   // (uniform already: readfirstlane keeps every instantiation in SGPRs)
+                                do {
+                                    asm("s_bitset1_b64 %0, %1" : "+s"(Mm) : "s"(fs));
+                                    fs = rdlanei(link, fs);
+                                } while (fs < LZH_WAVE);
+                                sl = 63 - __builtin_clzll(Mm);
+                            } else {
                             for (;;) {                                 // common case: plain links
                                 Mm |= 1ull << sl;
                                 fs = rdlanei(link, sl);
                                 if (fs >= LZH_WAVE) break;
                                 sl = fs;
+                            }
                             }
                             if (fs != 0x80) break;                     // the chain leaves the batch
                             int es;
@@ -978,9 +998,18 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                             // running max of the members' ends -- DPP, no LDS round trip
                             const bool mem = lane_on(Mm);
                             const int ej = wave_incl_max(mem ? e : 0);
+                            if (LZH_LZ4_MASKS) {
+                                // (as lane masks: one compare each, the rest scalar -- a ballot of a compound
+                                // condition goes through a VGPR and back)
+                                const uint64_t inside = ballot(lane < ej) & ~Mm;
+                                const uint64_t below_eL = endip && eL < LZH_WAVE ? (1ull << eL) - 1ull : ~0ull;
+                                E = (~0ull << lo) & ~inside & below_eL;
+                                I = ballot(lane + 2 == ej) & ~Mm;      // lz4.c:1146 (a member's own end is >= lane + 4)
+                            } else {
                             const bool inside = !mem && lane < ej;
                             E = ballot(lane >= lo && !inside && (!endip || lane < eL));
                             I = ballot(!mem && lane == ej - 2);        // lz4.c:1146 (a member's own end is >= lane + 4)
+                            }
                         } else {
                         const uint64_t mle = Mm & (below | (1ull << lane));
                         const int j = mle ? 63 - __builtin_clzll(mle) : lane;
@@ -1292,7 +1321,7 @@ lzh_lz4_compress_stats_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_r
 extern "C" __global__ void __launch_bounds__(64)
 lzh_lz4_parse_kernel(const uint8_t* in, uint64_t n_total, uint64_t in_readable, uint64_t chunk_size, int acc,
                      uint8_t* recs, uint64_t rec_stride, uint32_t* rec_hdr, uint64_t frame_size, uint32_t bpf) {
-    // table only (16 KiB: 10 waves per CU; the P sides from a register window, compress_chunk's kRW)
+    // table only (the P sides from a register window, compress_chunk's kRW)
     // (LZH_LZ4_PADLDS: extra bytes of LDS per wave -- an occupancy experiment, 0 in builds)
     __shared__ __attribute__((aligned(16))) uint32_t lds[4096 + (LZH_LZ4_RW ? 0 : lz4v3::kRing / 4 + 8) + LZH_LZ4_PADLDS / 4];
     const uint64_t chunk = blockIdx.x;

@@ -525,12 +525,15 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                         int sl = __builtin_ctzll(r0);
                         for (;;) {                                       // (links strictly increase)
                             int fs;
-                            for (;;) {
-                                Mm |= 1ull << sl;
-                                fs = rdlanei(link, sl);
-                                if (fs >= LZH_WAVE) break;
-                                sl = fs;
-                            }
+                            // one register for the walk, the last member the highest bit of Mm afterwards (members
+                            // increase): 5 instructions a member (as the LZ4 kernel's walk)
+                            fs = unii(sl);
+                            Mm = uni64(Mm);
+                            do {
+                                asm("s_bitset1_b64 %0, %1" : "+s"(Mm) : "s"(fs));
+                                fs = rdlanei(link, fs);
+                            } while (fs < LZH_WAVE);
+                            sl = 63 - __builtin_clzll(Mm);
                             if (fs != 0x80) break;
                             int es;
                             if (rdlane((uint32_t)lng, sl)) {             // copy runs past the window
@@ -568,12 +571,14 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                             // increase along the chain (after_copy(e) holds lanes >= e only)
                             const bool mem = lane_on(Mm);
                             ejm = wave_incl_max(mem ? e : 0);
+                            // (after_copy(ejm) at lane >= ejm is bit lane - ejm of kAfter: no per-lane 64-bit pattern)
+                            constexpr uint64_t kAfter = 1ull | (kPat0 << 1);
                             bool pr;
                             if (mem) pr = true;
                             else if (ejm == 0) pr = lane_on(P0);
-                            else pr = lane >= ejm && ((after_copy(ejm) >> lane) & 1ull);
+                            else pr = lane >= ejm && ((kAfter >> ((lane - ejm) & 63)) & 1ull);
                             E = ballot(pr && (!endp || lane < eL));
-                            I = ballot(!mem && lane == ejm - 1);
+                            I = ballot(lane + 1 == ejm) & ~Mm;
                         } else {
                         const uint64_t mle = Mm & (below | (1ull << lane));
                         const int j = mle ? 63 - __builtin_clzll(mle) : lane;
