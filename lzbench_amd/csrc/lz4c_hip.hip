@@ -786,14 +786,13 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             if (kRW) {
                 WX = unii(WX); wc_ok = unii(wc_ok); wn_ok = unii(wn_ok);
                 int o = front + in.sh - WX;
-                int use = 0;                                           // 1: Wc, 2: the window moved up 128
-                if (runb) {
-                    if (wc_ok && o >= 0 && o <= kWinMax) use = 1;
-                    else if (wn_ok && o >= 128 && o - 128 <= kWinMax) use = 2;
-                }
+                // 1: Wc, 2: the window moved up 128 (scalar ints and unsigned range tests: no lane-mask booleans)
+                const int c1 = runb & wc_ok & (int)((unsigned)o <= (unsigned)kWinMax);
+                const int c2 = runb & wn_ok & (int)((unsigned)(o - 128) <= (unsigned)kWinMax);
+                const int use = c1 ? 1 : (c2 ? 2 : 0);
                 if (use == 2) { Wc = Wn; WX += 128; o -= 128; LZ_STAT(4, 1); }
                 if (!use) WX = ((front + in.sh) & ~3) - 128;          // (Wn from here on: the next batch's Wc)
-                wc_ok = use != 0;
+                wc_ok = c1 | c2;
                 if (use) {
                     ps = p_side_win(Wc, o + lane);
                 } else {
@@ -817,7 +816,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             else if (valid) T.put(h, (uint32_t)p);
             wave_lds_fence();
             const uint32_t back = T.get(h);
-            const uint64_t losers = ballot(valid && back != (uint32_t)p);
+            const uint64_t losers = ballot(back != (uint32_t)p) & vmask;   // (one compare: no VGPR round trip)
             LZ_CLK(1);                                                 // table read/claim/read back, loads issued
             // ---- deferred records + emission of the previous batch (under the loads above)
             pr_m = uni64(pr_m); pr_base = unii(pr_base); pr_anchor = unii(pr_anchor);
@@ -855,7 +854,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
 
                 const uint64_t eb = grp & below;
                 prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
-                coll = ballot(prev >= 0);
+                coll = ballot(eb != 0ull) & vmask;                 // (= lanes with prev >= 0)
                 // a collider's candidate is usually its closest earlier slot member: evaluate
                 // that pair once per batch (the per-step test below then only selects)
                 const int k = prev >= 0 ? prev : lane;
