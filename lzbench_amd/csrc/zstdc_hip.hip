@@ -398,7 +398,6 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             const int q = Aj + half;
             ZMK(1);
             // ---- P side, rep side
-            const bool rok = valid && !half && r1 > 0;
             const uint64_t w8 = Ld.w8;
             const uint32_t rv = Ld.rv, rm = Ld.rm;
             const uint32_t h = zh<kMls>(w8, P.hlog, P.mls);
@@ -427,15 +426,17 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 uint64_t eq = vmask;
                 // (the first 6 bits unrolled, without the loop's scalar chain: bits at or past nbits are 0
                 // in every valid lane's offset, so those rounds leave eq as it is)
+                // (ballot of the single compare, masked with vmask in scalar: a ballot of a compound condition goes
+                // through a VGPR and back)
 #pragma unroll
                 for (int b = 0; b < 6; b++) {
                     const bool wb = (wr >> b) & 1u;
-                    const uint64_t bm = ballot(valid && wb);
+                    const uint64_t bm = ballot(wb) & vmask;
                     eq &= wb ? bm : ~bm;
                 }
                 for (int b = 6; b < nbits; b++) {
                     const bool wb = (wr >> b) & 1u;
-                    const uint64_t bm = ballot(valid && wb);
+                    const uint64_t bm = ballot(wb) & vmask;
                     eq &= wb ? bm : ~bm;
                 }
                 grp = valid ? eq : grp;
@@ -455,8 +456,9 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             }
             ZMK(3);
             // ---- candidate compare (an in-batch candidate is past the prefix start)
-            const bool rhit = rok && rv == rm;
-            const uint64_t R = ballot(rhit), H = ballot(hit), E = R | H;
+            // (R: the compare's ballot masked in scalar -- rok is vmask, even lanes, r1 > 0)
+            const uint64_t R = r1 > 0 ? ballot(rv == rm) & vmask & 0x5555555555555555ull : 0ull;
+            const uint64_t H = ballot(hit), E = R | H;
             ZMK(4);
             const uint64_t committed = E ? (vmask & (ffs64(E) == 63 ? ~0ull : ((2ull << ffs64(E)) - 1ull))) : vmask;
             // ---- slots: the value the sequential order leaves (no collision in the batch: each lane
