@@ -394,7 +394,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             ms.count(3);
             const int Aj = S.Aj, Dj = S.Dj, A32 = S.A32, D32 = S.D32, s32 = S.s32, n32 = S.n32;
             const bool valid = j == 0 || Aj + 1 + Dj < ilimit;
-            const uint64_t vmask = ballot(valid);
+            const uint64_t vmask = ballot(Aj + 1 + Dj < ilimit) | 3ull;   // (pair 0 = lanes 0, 1: one compare)
             const int q = Aj + half;
             ZMK(1);
             // ---- P side, rep side
@@ -413,7 +413,7 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             if (valid) T.claim(h, (uint32_t)q + 1);
             T.fence();
             if (valid) back = T.back(h);
-            const uint64_t losers = ballot(valid && back != (((uint32_t)q + 1) & Tab::kBackMask));
+            const uint64_t losers = ballot(back != (((uint32_t)q + 1) & Tab::kBackMask)) & vmask;
             uint64_t grp = 1ull << lane;
             int prev = -1;
             if (losers) {
@@ -444,21 +444,22 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
                 prev = (valid && eb) ? 63 - __builtin_clzll(eb) : -1;
             }
             uint32_t cand = old;
-            bool hit = ook && cwo == (uint32_t)w8;
+            // (hits as lane masks from single compares: a ballot of a compound or merged condition goes through
+            // a VGPR and back)
+            uint64_t H = ballot(cwo == (uint32_t)w8) & ballot(old > (uint32_t)pstart) & vmask;
             if (losers) {   // (a batch without a collision needs no gathers: most batches)
                 const int src = prev < 0 ? lane : prev;
                 const int qprev = lane_gather((uint32_t)q, src);
                 const uint32_t wprev = lane_gather((uint32_t)w8, src);
-                if (prev >= 0) {
-                    cand = (uint32_t)qprev + 1;
-                    hit = valid && wprev == (uint32_t)w8;
-                }
+                if (prev >= 0) cand = (uint32_t)qprev + 1;
+                const uint64_t PV = ballot(prev >= 0);              // colliders (valid lanes only)
+                H = (H & ~PV) | (ballot(wprev == (uint32_t)w8) & PV);
             }
             ZMK(3);
             // ---- candidate compare (an in-batch candidate is past the prefix start)
             // (R: the compare's ballot masked in scalar -- rok is vmask, even lanes, r1 > 0)
             const uint64_t R = r1 > 0 ? ballot(rv == rm) & vmask & 0x5555555555555555ull : 0ull;
-            const uint64_t H = ballot(hit), E = R | H;
+            const uint64_t E = R | H;
             ZMK(4);
             const uint64_t committed = E ? (vmask & (ffs64(E) == 63 ? ~0ull : ((2ull << ffs64(E)) - 1ull))) : vmask;
             // ---- slots: the value the sequential order leaves (no collision in the batch: each lane
@@ -526,7 +527,8 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
         int bk;
         {
             constexpr int kB = LZH_ZSTD_BWD;
-            const uint64_t m = ballot(!bl || ba != bb);
+            const int nbl = min(bmax, LZH_ZSTD_BWD);               // (the lanes of bl, as a scalar mask)
+            const uint64_t m = ~(nbl >= 64 ? ~0ull : (1ull << max(nbl, 0)) - 1ull) | ballot(ba != bb);
             bk = ffs64(m);
             if (bk >= kB && bmax > kB) bk = kB + count_bwd(in, m0 - kB, p0 - kB, bmax - kB, lane);
             bk = min(bk, bmax);
@@ -536,8 +538,8 @@ __device__ void fast_block(const Tab& T, const Bytes& in, const ZParams& P, int 
             const uint32_t x = fa ^ fb;
             int eq = x ? (int)(__builtin_ctz(x) >> 3) : 4;
             if (4 * lane + eq > fmax) eq = fmax - 4 * lane;
-            const bool st = fl && eq < 4;
-            const uint64_t m = ballot(st);
+            const int nfl = min(LZH_ZSTD_FWD, fmax > 0 ? (fmax + 3) >> 2 : 0);   // (the lanes of fl)
+            const uint64_t m = ballot(eq < 4) & (nfl >= 64 ? ~0ull : (1ull << nfl) - 1ull);
             constexpr int kF = 4 * LZH_ZSTD_FWD;
             if (m) fw = 4 * ffs64(m) + (int)rdlane((uint32_t)eq, ffs64(m));
             else fw = fmax <= kF ? max(fmax, 0) : kF + count_fwd(in, m0 + 4 + kF, p0 + 4 + kF, fmax - kF, lane);

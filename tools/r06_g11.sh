@@ -1,0 +1,11 @@
+# round 6 call 11: the zstd match finder's vmask / losers / hits / match-compare masks from single compares:
+# zstd compress tests + 1 GiB digest bench, A/B against the head (3 rounds, mixed and text -b128)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r06_k; mkdir -p $O
+timeout -k 10 300 python -u bench.py --no-e2e --no-cpu-baseline --codec zstd --chunk-kib 128 --corpus mixed > $O/bench_zstd.json 2> $O/bench_zstd.err || { tail $O/bench_zstd.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/bench_zstd.json'));print('zstd', d['value'], d['stage_ms'], 'bit_exact', d['bit_exact'])"
+timeout -k 10 800 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_zstd_compress.py > $O/pytest.log 2>&1 || { tail -20 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+PROF_ARGS="--codec zstd --level 1 --chunk-kib 128" AB_CORPORA="mixed text" AB_ROUNDS=3 timeout -k 10 500 bash tools/ab.sh head base > $O/abz.log 2>&1 || { tail $O/abz.log; exit 1; }
+cat $O/abz.log
