@@ -142,9 +142,10 @@ def _loaded_hashes():
     """kernel code hashes of the library this process loads (lzbench_amd.kernel_hash)"""
     global _HASHES
     if _HASHES is None:
+        import lzbench_amd
         from lzbench_amd import kernel_hash
         try:
-            _HASHES = kernel_hash.kernel_hashes(L.LIB_PATH)
+            _HASHES = kernel_hash.kernel_hashes(lzbench_amd.LIB_PATH)
         except (OSError, ValueError):
             _HASHES = {}
     return _HASHES
