@@ -47,3 +47,10 @@ def test_traffic_only_for_the_profiled_code(hashes, tmp_path, monkeypatch):
     del prof["kernels"][k]["kernel_hash"]                       # a profile from before the hashes
     (tmp_path / "profiles" / "traffic_a.json").write_text(json.dumps(prof))
     assert bench.traffic_for(k, "w")[0] is None
+
+
+def test_bench_reads_the_loaded_library(hashes, monkeypatch):
+    """bench.py hashes the library lzbench_amd loads (LIB_PATH), not a copy"""
+    import bench
+    monkeypatch.setattr(bench, "_HASHES", None)
+    assert bench._loaded_hashes() == hashes
