@@ -244,6 +244,9 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 #ifndef LZH_LZ4_PADLDS
 #define LZH_LZ4_PADLDS 0
 #endif
+#ifndef LZH_LZ4_AMASK   // the resolve's hit set A as a uniform mask built from single-compare ballots
+#define LZH_LZ4_AMASK 1
+#endif
 
 // Sequences found by one batch, one per member lane (the lane of the sequence's match start):
 // anchor, literal count, offset, match length - 4, first output byte within the batch's
@@ -448,7 +451,8 @@ __device__ __forceinline__ uint32_t byte_ctz(uint32_t x) { return (uint32_t)__bu
 
 
 // returns ok; sets bkr (0..4) and len (0..20)
-__device__ __forceinline__ bool eval_lane(const PSide& P, const MWin& W, bool valid, int& bkr, int& len) {
+__device__ __forceinline__ bool eval_lane(const PSide& P, const MWin& W, bool valid, int& bkr, int& len,
+                                          bool* eq = nullptr) {
     const uint32_t s = (uint32_t)W.sm;
     const uint32_t mm4 = __builtin_amdgcn_alignbyte(W.d1, W.d0, s);
     const uint32_t mw = __builtin_amdgcn_alignbyte(W.d2, W.d1, s);
@@ -461,6 +465,7 @@ __device__ __forceinline__ bool eval_lane(const PSide& P, const MWin& W, bool va
     len = l;
     const uint32_t y = P.m4 ^ mm4;
     bkr = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
+    if (eq) *eq = mw == P.w;                 // (the bare compare: its ballot is the compare's own mask)
     return valid && mw == P.w;
 }
 
@@ -833,6 +838,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             int prev = -1;
             const uint64_t below = (1ull << lane) - 1ull;
             bool okp = false;                                      // evaluation against lane prev
+            uint64_t OKP = 0;                                      // (as a lane mask)
             int bep = 0, lep = 0;
             if (runb && losers) {
                 LZ_STAT(1, 1);
@@ -869,6 +875,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 const uint32_t y = ps.m4 ^ gm4;
                 bep = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
                 okp = valid && gw == ps.w;
+                OKP = ballot(gw == ps.w) & vmask;
             }
             if (kRW) {
                 // the window's next part, after the candidate loads (no explicit wait: the compiler waits for the
@@ -892,8 +899,16 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             }
             if (!kRec && op - O.flushed >= 4 * LZH_WAVE) O.flush(out, ((op + O.sh) & ~3) - O.sh, lane);
             int bkr, len;
-            bool ok = eval_lane(ps, W, valid, bkr, len);
+            bool eqw;
+            bool ok = eval_lane(ps, W, valid, bkr, len, &eqw);
             if (!kSmall) ok = ok && (cand + 65535u >= (uint32_t)p);
+            // (LZH_LZ4_AMASK: `ok` as a lane mask, balloted next to its compares -- an i1 that crosses a block
+            // boundary goes through a VGPR to be balloted)
+            uint64_t OKM = 0;
+            if (LZH_LZ4_AMASK) {
+                OKM = ballot(eqw) & vmask;
+                if (!kSmall) OKM &= ballot(cand + 65535u >= (uint32_t)p);
+            }
 
             if (runb) {
                 // ================= run batch: resolve every sequence that starts in the batch
@@ -924,6 +939,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 // candidates until consistent (each round fixes a prefix of the batch).
                 int ak = prev;
                 bool oke = prev >= 0 ? okp : ok;
+                // (LZH_LZ4_AMASK) the lanes whose candidate matches, carried as a uniform mask: a ballot of the
+                // merged bool `oke` costs a VGPR round trip per round, the mask costs three scalar operations
+                const uint64_t Am0 = (coll & OKP) | (OKM & ~coll);
+                uint64_t Am = Am0;
                 uint32_t ce = prev >= 0 ? (uint32_t)(base + prev) : cand;
                 int be = prev >= 0 ? bep : bkr, le = prev >= 0 ? lep : len;
                 uint64_t Mm = 0, I = I0;                               // member lanes (sequence starts)
@@ -931,10 +950,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 int eL = 0;                                            // end lane of the last member
                 bool endp = false;                                     // the parse ends in this batch
                 for (int round = 0; round <= LZH_WAVE; round++) {
-                    const uint64_t A = ballot(oke);
+                    const uint64_t A = LZH_LZ4_AMASK ? uni64(Am) : ballot(oke);
                     // if lane l starts a sequence: match count, end lane, next hit at or after the end
                     cn = min(le, mlimit - (p + kMinMatch));
-                    const bool lng = oke && le == 20 && p + kMinMatch + 20 < mlimit;
+                    const bool lng = (LZH_LZ4_AMASK ? lane_on(A) : oke) && le == 20 && p + kMinMatch + 20 < mlimit;
                     e = lane + kMinMatch + cn;
                     int f = ctz64v(e < LZH_WAVE ? (A & (PAT << e)) : 0ull);
                     // chain walk (lz4.c:1142-1200: match end -> re-test -> search from ip+1)
@@ -1028,17 +1047,23 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                     const uint64_t mk = grp & below & I;
                     const int kt = mk ? 63 - __builtin_clzll(mk) : -1;
                     const bool fix = lane_on(E) && kt != ak;
-                    if (!ballot(fix)) break;
+                    const uint64_t FX = ballot(fix);
+                    if (!FX) break;
                     LZ_STAT(2, 1);
                     const bool far = fix && kt >= 0 && kt != prev;
+                    if (LZH_LZ4_AMASK) {
+                        const uint64_t KN = ballot(kt < 0);
+                        Am = (Am & ~FX) | (FX & ((KN & OKM) | (~KN & OKP)));
+                    }
                     if (fix) {
                         ak = kt;
-                        oke = kt < 0 ? ok : okp;
+                        if (!LZH_LZ4_AMASK) oke = kt < 0 ? ok : okp;
                         ce = kt < 0 ? cand : (uint32_t)(base + kt);
                         be = kt < 0 ? bkr : bep;
                         le = kt < 0 ? len : lep;
                     }
-                    if (ballot(far)) {                                 // an older member than prev
+                    const uint64_t FR = ballot(far);
+                    if (FR) {                                          // an older member than prev
                         const int k = far ? kt : lane;
                         const uint32_t gm4 = lane_gather(ps.m4, k), gw = lane_gather(ps.w, k),
                                        g0 = lane_gather(ps.q0, k), g1 = lane_gather(ps.q1, k),
@@ -1051,8 +1076,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                             le = l;
                             const uint32_t y = ps.m4 ^ gm4;
                             be = y ? (int)((uint32_t)__builtin_clz(y) >> 3) : 4;
-                            oke = valid && gw == ps.w;
+                            if (!LZH_LZ4_AMASK) oke = valid && gw == ps.w;
                         }
+                        if (LZH_LZ4_AMASK) Am = (Am & ~FR) | (FR & ballot(gw == ps.w) & vmask);
                     }
                 }
                 LZ_CLK(5);                                             // chain resolve

@@ -31,6 +31,9 @@ namespace snv2 {
 #ifndef LZH_SN_DPPEND   // the members' ends by a DPP running max (no lane_gather round trips)
 #define LZH_SN_DPPEND 1
 #endif
+#ifndef LZH_SN_AMASK   // the resolve's hit set and probed set as uniform masks from single-compare ballots
+#define LZH_SN_AMASK 1
+#endif
 #ifndef LZH_SN_RESTORE2   // the table restore of a batch without slot collisions: no per-lane last-insert search
 #define LZH_SN_RESTORE2 1
 #endif
@@ -460,6 +463,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 uint64_t grp = 1ull << lane, coll = 0;
                 int prev = -1;
                 bool okp = false;
+                uint64_t OKP = 0;                                        // (okp as a lane mask)
                 int lep = 0;
                 if (losers) {
                     SN_STAT(1, 1);
@@ -481,6 +485,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     lep = match_after4(ps, lane_gather(ps.q1, k), lane_gather(ps.q2, k), lane_gather(ps.q3, k),
                                        lane_gather(ps.q4, k), lane_gather(ps.q5, k));
                     okp = gw == ps.w;
+                    OKP = ballot(gw == ps.w);
                 }
                 SN_CLK(2);
                 wait_vm();
@@ -493,6 +498,7 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 }
                 const uint32_t cs = (uint32_t)(cand + in.sh) & 3u;
                 const bool ok = __builtin_amdgcn_alignbyte(d1, d0, cs) == ps.w;
+                const uint64_t OKM = ballot(ok);                         // (next to its compare: no VGPR trip)
                 const int len = match_after4(ps, __builtin_amdgcn_alignbyte(d2, d1, cs),
                                              __builtin_amdgcn_alignbyte(d3, d2, cs),
                                              __builtin_amdgcn_alignbyte(d4, d3, cs),
@@ -502,6 +508,8 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 // earlier slot member, walk, verify against the inserted set, repeat if needed
                 int ak = prev;
                 bool oke = prev >= 0 ? okp : ok;
+                // (LZH_SN_AMASK) oke as a uniform mask: a ballot of the merged bool goes through a VGPR each round
+                uint64_t Am = (coll & OKP) | (OKM & ~coll);
                 uint32_t ce = prev >= 0 ? (uint32_t)(base + prev) : cand;
                 int le = prev >= 0 ? lep : len;
                 uint64_t Mm = 0, I = I0;
@@ -509,9 +517,9 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                 int ejm = 0;                                             // (LZH_SN_DPPEND: the last round's running max)
                 bool endp = false;
                 for (int round = 0; round <= LZH_WAVE; round++) {
-                    const uint64_t A = ballot(oke);
+                    const uint64_t A = LZH_SN_AMASK ? uni64(Am) : ballot(oke);
                     cn = min(le, fn - (p + 4));                          // FindMatchLength limit (ip_end)
-                    const bool lng = oke && le == 20 && p + 24 < fn;
+                    const bool lng = (LZH_SN_AMASK ? lane_on(A) : oke) && le == 20 && p + 24 < fn;
                     e = lane + 4 + cn;
                     const int f = ctz64v(A & after_copy(e));
                     const int link = (lng || p + 4 + cn >= ip_limit) ? 0x80 : f;
@@ -573,11 +581,20 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                             ejm = wave_incl_max(mem ? e : 0);
                             // (after_copy(ejm) at lane >= ejm is bit lane - ejm of kAfter: no per-lane 64-bit pattern)
                             constexpr uint64_t kAfter = 1ull | (kPat0 << 1);
+                            if (LZH_SN_AMASK) {
+                                // members; lanes before the first member on the initial plan; lanes at or past the
+                                // last member's end on its pattern -- one compare per ballot, the rest scalar
+                                const uint64_t Z = ballot(ejm == 0), GE = ballot(lane >= ejm),
+                                               BT = ballot(((kAfter >> ((lane - ejm) & 63)) & 1ull) != 0ull);
+                                const uint64_t below_eL = endp && eL < LZH_WAVE ? (1ull << eL) - 1ull : ~0ull;
+                                E = (Mm | (Z & P0) | (~Z & GE & BT)) & below_eL;
+                            } else {
                             bool pr;
                             if (mem) pr = true;
                             else if (ejm == 0) pr = lane_on(P0);
                             else pr = lane >= ejm && ((kAfter >> ((lane - ejm) & 63)) & 1ull);
                             E = ballot(pr && (!endp || lane < eL));
+                            }
                             I = ballot(lane + 1 == ejm) & ~Mm;
                         } else {
                         const uint64_t mle = Mm & (below | (1ull << lane));
@@ -596,21 +613,28 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     const uint64_t mk = grp & below & I;
                     const int kt = mk ? 63 - __builtin_clzll(mk) : -1;
                     const bool fix = lane_on(E) && kt != ak;
-                    if (!ballot(fix)) break;
+                    const uint64_t FX = ballot(fix);
+                    if (!FX) break;
                     SN_STAT(2, 1);
                     const bool far = fix && kt >= 0 && kt != prev;
+                    if (LZH_SN_AMASK) {
+                        const uint64_t KN = ballot(kt < 0);
+                        Am = (Am & ~FX) | (FX & ((KN & OKM) | (~KN & OKP)));
+                    }
                     if (fix) {
                         ak = kt;
                         oke = kt < 0 ? ok : okp;
                         ce = kt < 0 ? cand : (uint32_t)(base + kt);
                         le = kt < 0 ? len : lep;
                     }
-                    if (ballot(far)) {                                   // an older member than prev
+                    const uint64_t FR = ballot(far);
+                    if (FR) {                                            // an older member than prev
                         const int k = far ? kt : lane;
                         const uint32_t gw = lane_gather(ps.w, k);
                         const int lf = match_after4(ps, lane_gather(ps.q1, k), lane_gather(ps.q2, k),
                                                     lane_gather(ps.q3, k), lane_gather(ps.q4, k), lane_gather(ps.q5, k));
                         if (far) { le = lf; oke = gw == ps.w; }
+                        if (LZH_SN_AMASK) Am = (Am & ~FR) | (FR & ballot(gw == ps.w));
                     }
                 }
                 SN_CLK(4);
