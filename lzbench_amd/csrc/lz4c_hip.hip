@@ -763,9 +763,16 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             // ---- lanes -> positions
             int p;
             bool valid;
+            // (the lane mask and the first position per branch, as uniform values: a ballot of the merged `valid`
+            // goes through a VGPR, and lane 0's position of a run batch is its base)
+            uint64_t vmask;
+            int front;
             if (runb) {
                 p = base + lane;
-                valid = p + 1 <= mfl1 && (!kLinked || p <= stop);   // forwardIp <= mflimitPlusOne (lz4.c:969)
+                vmask = ballot(p + 1 <= mfl1);                       // forwardIp <= mflimitPlusOne (lz4.c:969)
+                if (kLinked) vmask &= ballot(p <= stop);
+                valid = lane_on(vmask);
+                front = base;
             } else {
                 int64_t pp, nxt;
                 if (retest && lane == 0) {
@@ -780,9 +787,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 }
                 valid = nxt <= mfl1 && (!kLinked || pp <= stop);
                 p = valid ? (int)pp : 0;
+                vmask = ballot(valid);
+                front = rdlanei(p, 0);
             }
-            const uint64_t vmask = ballot(valid);
-            const int front = rdlanei(p, 0);
+            vmask = uni64(vmask); front = unii(front);
             const int pmax = vmask ? rdlanei(p, 63 - __builtin_clzll(vmask)) : front;
 
             // ---- P-side bytes (ring when it covers the batch), hash, table read / claim / read back
