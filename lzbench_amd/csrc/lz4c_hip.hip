@@ -244,6 +244,11 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 #ifndef LZH_LZ4_PADLDS
 #define LZH_LZ4_PADLDS 0
 #endif
+#ifndef LZH_LZ4_EXPECT   // run batches as the likely branch (block frequencies for the register allocator; the run
+                         // batch's state updates as selects instead were 1-2 % slower, profiles/r06_o)
+#define LZH_LZ4_EXPECT 1
+#endif
+#define RUNB_LIKELY(x) (LZH_LZ4_EXPECT ? __builtin_expect((x) != 0, 1) : (x) != 0)
 #ifndef LZH_LZ4_AMASK   // the resolve's hit set A as a uniform mask built from single-compare ballots
 #define LZH_LZ4_AMASK 1
 #endif
@@ -767,7 +772,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             // goes through a VGPR, and lane 0's position of a run batch is its base)
             uint64_t vmask;
             int front;
-            if (runb) {
+            if (RUNB_LIKELY(runb)) {
                 p = base + lane;
                 vmask = ballot(p + 1 <= mfl1);                       // forwardIp <= mflimitPlusOne (lz4.c:969)
                 if (kLinked) vmask &= ballot(p <= stop);
@@ -918,7 +923,7 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 if (!kSmall) OKM &= ballot(cand + 65535u >= (uint32_t)p);
             }
 
-            if (runb) {
+            if (RUNB_LIKELY(runb)) {
                 // ================= run batch: resolve every sequence that starts in the batch
                 // ("colliders" are re-evaluated per step against the in-batch candidate)
                 LZ_CLK(4);                                             // eval + slot groups
