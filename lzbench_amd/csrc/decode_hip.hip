@@ -317,28 +317,30 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 // done = final now (not an unresolved in-pass source); far = source only in global memory.
 template <class W, class SinkType>
 __device__ __forceinline__ uint32_t owned_byte(const W& w, const SinkType& O, int op, int pbase, int thr, int ob,
-                                               int total, int lend, int lsb, int msrc, int offk, int& src, bool& done,
-                                               bool& far) {
-    const bool act = ob < total;
-    const bool is_lit = ob < lend;
+                                               int total, int lend, int lsb, int msrc, int offk, int& src,
+                                               uint64_t& done, uint64_t& far) {
+    // (lane masks from single-compare ballots: a ballot of a compound bool goes through a VGPR)
+    const uint64_t il = ballot(ob < lend), act = ballot(ob < total);
+    const bool is_lit = lane_on(il);
     const uint32_t lb = w.lane_byte(lsb + (is_lit ? ob : lend - 1));
     src = msrc + ob;
-    if (ballot(act && !is_lit && ob >= lend + offk)) {             // overlapping copy: period offk
+    const uint64_t ov = ballot(ob >= lend + offk) & ~il;
+    if (ov & act) {                                                // overlapping copy: period offk
         const int md = (int)((uint32_t)(ob - lend) % (uint32_t)max(offk, 1));
-        src = (!is_lit && ob >= lend + offk) ? op + lend - offk + md : src;
+        src = lane_on(ov) ? op + lend - offk + md : src;
     }
-    const bool near = !is_lit && src >= O.ringlo && src >= thr;
-    const bool inpass = !is_lit && src >= pbase;
     const uint32_t g = O.get(src);
-    done = is_lit || (near && !inpass);
-    far = act && !is_lit && !near;
+    const uint64_t near = ballot(src >= O.ringlo) & ballot(src >= thr) & ~il;
+    const uint64_t inpass = ballot(src >= pbase) & ~il;
+    done = il | (near & ~inpass);
+    far = act & ~il & ~near;
     return is_lit ? lb : g;
 }
 
 // The part of a 128-byte pass after its far reads are issued (their data are used here first):
 // store the bytes, resolve in-pass sources in dependency rounds, flush.
 struct Tail {
-    bool far0, far1, done0, done1;
+    uint64_t far0, far1, done0, done1;   // (lane masks)
     uint32_t v0, v1, g0, g1;
     int src0, src1, ob0, ob1, pbase, op, total;
 };
@@ -346,28 +348,30 @@ struct Tail {
 template <class SinkType>
 __device__ __forceinline__ void pass_tail(SinkType& O, Tail& t, int lane) {
     constexpr int kP = 2 * LZH_WAVE;
-    const uint32_t v0 = t.far0 ? t.g0 : t.v0, v1 = t.far1 ? t.g1 : t.v1;
-    const bool done0 = t.done0 || t.far0, done1 = t.done1 || t.far1;
+    const uint32_t v0 = lane_on(t.far0) ? t.g0 : t.v0, v1 = lane_on(t.far1) ? t.g1 : t.v1;
     const int op = t.op, pbase = t.pbase, ob0 = t.ob0, ob1 = t.ob1, src0 = t.src0, src1 = t.src1;
     // (bytes past the group's end land in window slots at most 127 bytes past it, which no
     // later reader takes as near: the next group's threshold, SinkT::match's kWin - 128 reach)
     O.put(op + ob0, v0);
     O.put(op + ob1, v1);
     // in-pass sources: rounds until every byte read a finished source
-    uint64_t dm0 = ballot(done0 || ob0 >= t.total), dm1 = ballot(done1 || ob1 >= t.total);
+    uint64_t dm0 = t.done0 | t.far0 | ballot(ob0 >= t.total), dm1 = t.done1 | t.far1 | ballot(ob1 >= t.total);
     uint32_t w0 = v0, w1 = v1;
     for (int r = 0; r < kP && (~dm0 | ~dm1); r++) {
         DST(4, 1);
         const int s0 = src0 - pbase, s1 = src1 - pbase;
-        const bool rd0 = !lane_on(dm0) && (((s0 & 1 ? dm1 : dm0) >> ((s0 >> 1) & 63)) & 1ull);
-        const bool rd1 = !lane_on(dm1) && (((s1 & 1 ? dm1 : dm0) >> ((s1 >> 1) & 63)) & 1ull);
+        // (the lanes that read a finished source, as masks: one compare per ballot -- a ballot of the compound
+        // bool goes through a VGPR)
+        const uint64_t rm0 = ballot((((s0 & 1 ? dm1 : dm0) >> ((s0 >> 1) & 63)) & 1ull) != 0ull) & ~dm0;
+        const uint64_t rm1 = ballot((((s1 & 1 ? dm1 : dm0) >> ((s1 >> 1) & 63)) & 1ull) != 0ull) & ~dm1;
+        const bool rd0 = lane_on(rm0), rd1 = lane_on(rm1);
         const uint32_t q0 = O.get(src0), q1 = O.get(src1);
         w0 = rd0 ? q0 : w0;
         w1 = rd1 ? q1 : w1;
         O.put(op + ob0, w0);
         O.put(op + ob1, w1);
-        dm0 |= ballot(rd0);
-        dm1 |= ballot(rd1);
+        dm0 |= rm0;
+        dm1 |= rm1;
     }
     O.maybe_flush(min(pbase + kP, op + t.total), lane);
 }
@@ -421,17 +425,17 @@ __device__ __forceinline__ void emit_group(const W& w, SinkType& O, LDSA uint8_t
         const int thr = pbase + kP - SinkType::kWin;               // sources below: overwritten in the window
         const int ob0 = pb + 2 * lane, ob1 = ob0 + 1;
         int src0, src1;
-        bool done0, done1, far0, far1;
+        uint64_t done0, done1, far0, far1;
         const uint32_t v0 = owned_byte(w, O, op, pbase, thr, ob0, total, le0, ls0, ms0, of0, src0, done0, far0);
         const uint32_t v1 = owned_byte(w, O, op, pbase, thr, ob1, total, le1, ls1, ms1, of1, src1, done1, far1);
         DMARK(12);
         t.g0 = t.g1 = 0;
-        const bool anyfar = ballot(far0 || far1) != 0;
+        const bool anyfar = (far0 | far1) != 0;
         if (anyfar) {   // far sources were flushed long ago: their stores must be done
             DST(5, 1);
             wait_vm();
-            t.g0 = O.out.b_sc1(far0 ? src0 : 0);
-            t.g1 = O.out.b_sc1(far1 ? src1 : 0);
+            t.g0 = O.out.b_sc1(lane_on(far0) ? src0 : 0);
+            t.g1 = O.out.b_sc1(lane_on(far1) ? src1 : 0);
         }
         t.far0 = far0; t.far1 = far1; t.done0 = done0; t.done1 = done1;
         t.v0 = v0; t.v1 = v1; t.src0 = src0; t.src1 = src1; t.ob0 = ob0; t.ob1 = ob1;
@@ -460,7 +464,7 @@ __device__ __forceinline__ uint64_t chain_members(int link, int lane) {
     y = (int)lane_gather((uint32_t)J2, x); x = y <= lane ? y : x;
     y = (int)lane_gather((uint32_t)J1, x); x = y <= lane ? y : x;
     y = (int)lane_gather((uint32_t)J0, x); x = y <= lane ? y : x;
-    return ballot(x == lane && link != 255);
+    return ballot(x == lane) & ballot(link != 255);   // (single compares: no VGPR round trip)
 }
 
 template <class SinkType>
@@ -502,9 +506,10 @@ __device__ int lz4_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t* ma
         const int incl = wave_incl_scan(L);
         const int excl = incl - L;
         const int opm = op + excl + lit;
-        const bool bad = mem && (x >= cs || (ln == 15 && x + 1 >= cs - 15) || opm > cap - 12 || p1 + lit > cs - 8 ||
-                                 (mc == 15 && po + 3 >= cs - 4) || off == 0 || off > opm + prefix || opm + ml > cap - 5);
-        const uint64_t badm = ballot(bad);
+        // (the failing members as a mask of single-compare ballots: a ballot of the compound bool goes through a VGPR)
+        const uint64_t badm = M & (ballot(x >= cs) | (ballot(ln == 15) & ballot(x + 1 >= cs - 15)) | ballot(opm > cap - 12) |
+                                   ballot(p1 + lit > cs - 8) | (ballot(mc == 15) & ballot(po + 3 >= cs - 4)) |
+                                   ballot(off == 0) | ballot(off > opm + prefix) | ballot(opm + ml > cap - 5));
         const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
         if (!keep) {
             const int r = checked::lz4_one(in, cs, O, w, cap, ip, op, lane, prefix);
@@ -605,8 +610,8 @@ __device__ int snappy_decode(const Bytes& in, int cs, SinkType& O, LDSA uint8_t*
         const int incl = wave_incl_scan(L);
         const int excl = incl - L;
         const int opm = op + excl;
-        const bool bad = mem && (x >= cs || !okr || opm + len > ul || (kind != 0 && off > opm));
-        const uint64_t badm = ballot(bad);
+        const uint64_t badm = M & (ballot(x >= cs) | ~ballot(okr) | ballot(opm + len > ul) |
+                                   (ballot(kind != 0) & ballot(off > opm)));   // (single-compare ballots)
         const uint64_t keep = badm ? (M & ((1ull << __builtin_ctzll(badm)) - 1ull)) : M;
         if (!keep) {
             // one tag through the checked path (snappy.cc:848-952 rules)
