@@ -34,6 +34,9 @@ namespace snv2 {
 #ifndef LZH_SN_AMASK   // the resolve's hit set and probed set as uniform masks from single-compare ballots
 #define LZH_SN_AMASK 1
 #endif
+#ifndef LZH_SN_SHR   // the next hit after a copy from A shifted down by the copy's end (no per-lane pattern)
+#define LZH_SN_SHR 1
+#endif
 #ifndef LZH_SN_RESTORE2   // the table restore of a batch without slot collisions: no per-lane last-insert search
 #define LZH_SN_RESTORE2 1
 #endif
@@ -521,7 +524,11 @@ __device__ int compress_fragment(const Bytes& in, int fn, const Bytes& out, int 
                     cn = min(le, fn - (p + 4));                          // FindMatchLength limit (ip_end)
                     const bool lng = (LZH_SN_AMASK ? lane_on(A) : oke) && le == 20 && p + 24 < fn;
                     e = lane + 4 + cn;
-                    const int f = ctz64v(A & after_copy(e));
+                    // next hit at or after e on the pattern after a copy (LZH_SN_SHR: A shifted down by e, one 64-bit
+                    // shift per lane, instead of the pattern built per lane)
+                    constexpr uint64_t kAft = 1ull | (kPat0 << 1);
+                    const int f = LZH_SN_SHR ? (e < LZH_WAVE ? e + ctz64v((A >> (e & 63)) & kAft) : LZH_WAVE)
+                                             : ctz64v(A & after_copy(e));
                     const int link = (lng || p + 4 + cn >= ip_limit) ? 0x80 : f;
                     Mm = 0;
                     endp = false;
