@@ -249,6 +249,9 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 #define LZH_LZ4_EXPECT 1
 #endif
 #define RUNB_LIKELY(x) (LZH_LZ4_EXPECT ? __builtin_expect((x) != 0, 1) : (x) != 0)
+#ifndef LZH_LZ4_RUNB_SGPR   // the run / stride flag without a readfirstlane at the batch loop's head
+#define LZH_LZ4_RUNB_SGPR 1
+#endif
 #ifndef LZH_LZ4_AMASK   // the resolve's hit set A as a uniform mask built from single-compare ballots
 #define LZH_LZ4_AMASK 1
 #endif
@@ -740,7 +743,10 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             go = unii(go);
             if (kLinked) aborted = unii(aborted) != 0;
             if (!go || (kLinked && aborted) || guard >= 4 * n + 64) break;
-            runb = unii(runb); retest = unii(retest);
+            // (runb: no readfirstlane -- its phi is uniform from constants under uniform branches, and the
+            // readfirstlane kept it in a VGPR: a v_mov + v_readfirstlane a batch)
+            if (!LZH_LZ4_RUNB_SGPR) runb = unii(runb);
+            retest = unii(retest);
             base = unii(base); q = unii(q); qlim = unii(qlim); pins = unii(pins); s = unii(s); k0 = unii(k0);
             op = unii(op); anchor = unii(anchor); rc_tot = unii(rc_tot); nrec = unii(nrec);
             R.fill = unii(R.fill); R.ready = unii(R.ready); O.flushed = unii(O.flushed);
