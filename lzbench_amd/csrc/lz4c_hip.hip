@@ -252,6 +252,9 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 #ifndef LZH_LZ4_RUNB_SGPR   // the run / stride flag without a readfirstlane at the batch loop's head
 #define LZH_LZ4_RUNB_SGPR 1
 #endif
+#ifndef LZH_LZ4_PRFRESH   // the stride path writes the deferred record fields too (no back-edge VGPR copies)
+#define LZH_LZ4_PRFRESH 1
+#endif
 #ifndef LZH_LZ4_AMASK   // the resolve's hit set A as a uniform mask built from single-compare ballots
 #define LZH_LZ4_AMASK 1
 #endif
@@ -1181,6 +1184,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             }
 
             // ================= stride batch: first sequence only
+            // (the run path's deferred record fields are consumed by now: fresh values here too, so the batch loop's
+            // back edge needs no VGPR copies to merge the run and stride paths' values)
+            if (LZH_LZ4_PRFRESH) { pr_e = 0; pr_cn = 0; pr_be = 0; pr_ce = 0; }
             uint64_t hits = ballot(ok);
             const uint64_t tmask = ballot(!valid);
             const int fi = ffs64(tmask);
