@@ -252,6 +252,9 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 #ifndef LZH_LZ4_RUNB_SGPR   // the run / stride flag without a readfirstlane at the batch loop's head
 #define LZH_LZ4_RUNB_SGPR 1
 #endif
+#ifndef LZH_LZ4_SWP   // the switch to stride batches at the next batch's head (not on the run batches' back edge)
+#define LZH_LZ4_SWP 1
+#endif
 #ifndef LZH_LZ4_PRFRESH   // the stride path writes the deferred record fields too (no back-edge VGPR copies)
 #define LZH_LZ4_PRFRESH 1
 #endif
@@ -717,7 +720,9 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
         // re-test at a match end, then 64 step-1 search probes, lz4.c:955-969 / :1148-1200);
         // pins = a pending ip-2 table fill (lz4.c:1145-1146) sitting at base.  Stride batches
         // (any other schedule): one sequence per batch, the search from s with k0 probes done.
-        int runb = kFast || acc == 1, retest = 0, go = 1;   // (ints: uniform SGPR phis, not lane masks)
+        // (ints: uniform SGPR phis, not lane masks; runb 2 = a run batch's 64 probes found nothing, stride batches
+        // from the next batch's head on, LZH_LZ4_SWP)
+        int runb = kFast || acc == 1, retest = 0, go = 1;
         const int dlim = kFast ? 2 + 62 * acc : 64;      // last run-batch probe: segment origin + dlim
         int base = b0 + 1, q = b0 + 1, qlim = b0 + dlim, pins = -1;
         int so = b0;                             // segment origin (kFast pattern phase)
@@ -755,6 +760,12 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
             R.fill = unii(R.fill); R.ready = unii(R.ready); O.flushed = unii(O.flushed);
             so = unii(so);
             LZ_STAT(0, 1);
+            if (LZH_LZ4_SWP && runb == 2) {   // a run batch's 64 probes found nothing: stride batches from here
+                runb = 0;
+                s = so + 1;
+                k0 = LZH_WAVE;
+                retest = 0;
+            }
             if (kFast && runb && base + LZH_WAVE - 1 + acc > mfl1) {
                 // near the chunk end a probe's forwardIp may pass mflimit: stride batches take over
                 // (the pending ip-2 insert first, then the re-test or the next search probe)
@@ -1127,30 +1138,12 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                 };
                 if (endp) {
                     go = 0;
-                    if (Mm) anchor = base + eL;
                     if (kLinked) {   // the next block starts from this table: no ip-2 fill after a match
                         // ending past mflimit (lz4.c:1142-1146)
                         const bool endm = Mm && base + eL >= mfe;
                         restore(endm && eL - 2 < LZH_WAVE ? I & ~(1ull << (eL - 2)) : I);
                     }
                 } else {
-                    if (Mm) {
-                        const int ip = base + eL;
-                        anchor = ip;
-                        so = ip;
-                        if (eL < LZH_WAVE) {                           // searched to the batch end
-                            q = base + LZH_WAVE;
-                            qlim = ip + dlim;
-                            pins = -1;
-                        } else {                                       // re-test in a later batch
-                            q = ip;
-                            qlim = ip + dlim;
-                            pins = eL - 2 >= LZH_WAVE ? ip - 2 : -1;
-                        }
-                    } else {
-                        q = base + hi0 + 1;
-                        pins = -1;
-                    }
                     // table: the last inserted lane of each slot, or the slot's old value
                     const bool inI = lane_on(I);
                     if (LZH_LZ4_RESTORE2 && !losers) {
@@ -1169,14 +1162,39 @@ __device__ void compress_chunk(const Bytes& in, int n, const Bytes& out, int acc
                         if (wr) T.put(h, inI ? (uint32_t)p : old);
                     }
                     wave_lds_fence();
-                    if (!Mm && hi0 == qlim - base) {                   // 64 probes done: stride batches
+                }
+                // the loop state, after the parse's last batch too (the parse then reads only anchor, whose
+                // update is the same): one path into the back edge for the state, no copies merging an
+                // unchanged branch
+                const int swc = !Mm && hi0 == qlim - base;             // 64 probes done: stride batches
+                if (Mm) {
+                    const int ip = base + eL;
+                    anchor = ip;
+                    so = ip;
+                    if (eL < LZH_WAVE) {                               // searched to the batch end
+                        q = base + LZH_WAVE;
+                        qlim = ip + dlim;
+                        pins = -1;
+                    } else {                                           // re-test in a later batch
+                        q = ip;
+                        qlim = ip + dlim;
+                        pins = eL - 2 >= LZH_WAVE ? ip - 2 : -1;
+                    }
+                } else {
+                    q = base + hi0 + 1;
+                    pins = -1;
+                }
+                if (swc) {
+                    if (LZH_LZ4_SWP) {
+                        runb = 2;   // (the switch itself at the next batch's head: off the run batches' back edge)
+                    } else {
                         runb = 0;
                         s = so + 1;
                         k0 = LZH_WAVE;
                         retest = 0;
-                    } else {
-                        base = pins >= 0 ? pins : q;
                     }
+                } else {
+                    base = pins >= 0 ? pins : q;
                 }
                 __builtin_amdgcn_s_setprio(0);
                 LZ_CLK(8);                                             // table restore
