@@ -13,7 +13,7 @@ objs=""
 for f in lz4c_hip snappyc_hip decode_hip pack_hip zstdc_hip frame_hip; do
   # per-file flags as in the Makefile; SCHED_<file> (e.g. SCHED_decode_hip) overrides one file's
   case $f in
-    lz4c_hip) sf="-mllvm -amdgpu-sched-strategy=max-ilp" ;;
+    lz4c_hip) sf="-mllvm -amdgpu-sched-strategy=max-memory-clause" ;;
     snappyc_hip) sf="-mllvm -amdgpu-sched-strategy=max-memory-clause" ;;
     zstdc_hip) sf="-mllvm -amdgpu-atomic-optimizer-strategy=None" ;;
     decode_hip) sf="-mllvm -amdgpu-sched-strategy=max-ilp" ;;
