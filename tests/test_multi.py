@@ -71,6 +71,31 @@ def test_two_rank_shard_gather_equals_single(codec, chunk, mode):
     assert tmax == 2.0
 
 
+@pytest.mark.parametrize("world,nchunks", [(4, 7), (8, 5)])
+def test_more_ranks_shard_gather_equals_single(world, nchunks):
+    """the N=4 / N=8 launches of bench.py --gpus N rehearsed on gloo: uneven shares, and at N=8 with 5 chunks
+    (4 full + a ragged tail) three ranks own no chunk at all; rank 0's gather is still the single-process loop's
+    output byte for byte, and the max-over-ranks reduction sees every rank"""
+    import lzbench_amd as L
+    chunk = 65536
+    n = (nchunks - 1) * chunk + 777
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "lz4", chunk, n, q, False, None)) for r in range(world)]
+    for p in procs:
+        p.start()
+    packed, cs, tmax = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=90)
+        assert p.exitcode == 0
+    data = L.datagen("json", n, seed=77)
+    ep, ec = O.compress_chunks(data, "lz4", chunk)
+    assert np.frombuffer(packed, np.uint8).tobytes() == ep.tobytes()
+    assert cs == ec.tolist()
+    assert tmax == float(world)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("codec,chunk", [("lz4", 65536), ("snappy", 262144), ("lz4frame", 65536)])
 def test_two_rank_shard_gather_hip_codec(codec, chunk):
